@@ -1,0 +1,218 @@
+/*
+ * segkern.h -- C-ABI of the MI355X (gfx950) segmentation training path.
+ *
+ * This library replaces the TensorFlow 1.x kernels that the reference's hot
+ * path executes inside `sess.run(train_step)`.  Each entry
+ * point names the TF op / reference call site it stands in for.  The Python
+ * host layer (`semanticsegmentation_tensorflow_amd/layers.py`) mirrors the
+ * reference's layer builders on top of these calls.
+ *
+ * Conventions
+ *  - Plain C types only: device pointers as `void*`/`float*`, sizes as int /
+ *    size_t, the HIP stream as `void*` (a `hipStream_t`; NULL = null stream).
+ *  - The caller owns every buffer, including workspaces; the library never
+ *    allocates on the hot path.  `seg_*_workspace` reports the bytes needed.
+ *  - Activations are NHWC; the channel dimension is padded to a multiple of
+ *    8 (`C`, `K` in the descriptors) and the padding channels hold zeros.
+ *    `ldx`/`ldy` (elements between consecutive pixels) allow channel-slice
+ *    views, e.g. a layer writing into a concat buffer.
+ *  - Every function returns 0 on success or a SEG_E* code; shapes are
+ *    validated with TF's rules (incl. the conv2d_transpose shape rule).
+ *    `seg_status_string()` turns a code into text.
+ */
+#ifndef SEGKERN_H
+#define SEGKERN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum seg_dtype { SEG_F32 = 0, SEG_BF16 = 1 };
+
+enum seg_status {
+    SEG_OK = 0,
+    SEG_EINVAL = 1,      /* bad argument (null pointer, bad dtype, ...)        */
+    SEG_ESHAPE = 2,      /* TF shape rule violated (InvalidArgumentError)      */
+    SEG_EALIGN = 3,      /* channel count / stride not a multiple of 8         */
+    SEG_EWORKSPACE = 4,  /* workspace too small                                */
+    SEG_ELAUNCH = 5      /* HIP launch failure                                 */
+};
+
+/* Convolution descriptor.  For Conv2D: input [N,H,W,C], filter [R,S,C,K]
+ * (HWIO), output [N,OH,OW,K].  For conv2d_transpose: input [N,H,W,C],
+ * filter [R,S,K,C] (TF's [kh,kw,out,in]), output [N,OH,OW,K].
+ * C and K are padded channel counts (multiples of 8); c_valid/k_valid are
+ * the real counts used to address the fp32 master filter. */
+typedef struct seg_conv_desc {
+    int N, H, W, C;
+    int OH, OW, K;
+    int R, S;
+    int stride_h, stride_w;
+    int dil_h, dil_w;
+    int pad_top, pad_bottom, pad_left, pad_right;
+    int ldx, ldy;          /* pixel strides (elements) of input / output   */
+    int c_valid, k_valid;  /* unpadded channel counts                      */
+    int dtype;             /* enum seg_dtype of activations and packed W   */
+} seg_conv_desc;
+
+/* Epilogue fused into a convolution's output write:
+ *   v = acc * scale[k] + shift[k] (+ bias[k]);  v = relu(v) if relu;
+ *   v = v / keep_prob * floor(keep_prob + U) if keep_prob < 1 (TF1 dropout);
+ *   v += residual[pixel, k]  (tf.add skip fusion)                          */
+typedef struct seg_epilogue {
+    const float* bias;
+    const float* scale;
+    const float* shift;
+    const void* residual;
+    int ld_residual;
+    int relu;
+    float keep_prob;
+    uint64_t seed;
+} seg_epilogue;
+
+/* ---- descriptor helpers ------------------------------------------------ */
+/* Fill a Conv2D descriptor with TF SAME/VALID padding (padding: 0=SAME,
+ * 1=VALID).  Mirrors tf.nn.conv2d's shape function (Network/model/FCN.py:130). */
+int seg_conv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int K, int R, int S,
+                       int stride, int dilation, int padding, int dtype);
+/* Fill a conv2d_transpose descriptor from the requested output shape; fails
+ * with SEG_ESHAPE unless ceil(out/stride) == in (SAME) -- TF's rule
+ * (Network/model/FCN.py:155, :106). */
+int seg_tconv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int OH, int OW, int K,
+                        int R, int S, int stride, int padding, int dtype);
+
+/* ---- Conv2D (Network/model/FCN.py:130-134, Network/utils/utils.py:182) --- */
+/* w_krsc: packed filter [K][R][S][C] in `dtype` (seg_pack_filter mode 0). */
+int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_krsc,
+                   const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
+/* Conv2DBackpropInput.  w_hwio: packed filter [R][S][C][K] in `dtype`
+ * (seg_pack_filter mode 1).  dx may be a channel-slice view (ldx). */
+int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,
+                        void* dx, void* ws, size_t ws_bytes, void* stream);
+/* Conv2DBackpropFilter: dw_f32 is the fp32 master-gradient layout
+ * [R][S][c_valid][k_valid]; written (not accumulated). */
+int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
+                          float* dw_f32, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- conv2d_transpose (Network/model/FCN.py:155, :106; utils.py:272) ---- */
+/* w_rskc: packed filter [R][S][K][C] in `dtype` (TF layout, seg_pack_filter mode 2). */
+int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_rskc,
+                    const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
+/* Gradient w.r.t. the tconv input = strided Conv2D of dy.  w_crsk: packed
+ * [C][R][S][K] (seg_pack_filter mode 3). */
+int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_crsk,
+                         void* dx, void* ws, size_t ws_bytes, void* stream);
+/* Filter gradient in TF layout [R][S][k_valid][c_valid], fp32. */
+int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
+                           float* dw_f32, void* ws, size_t ws_bytes, void* stream);
+
+/* Workspace bytes for op: 0 fwd, 1 bwd_data, 2 bwd_filter, 3 tconv fwd,
+ * 4 tconv bwd_data, 5 tconv bwd_filter. */
+size_t seg_conv_workspace(const seg_conv_desc* d, int op);
+
+/* ---- filter packing: fp32 master -> compute copy ----------------------- */
+/* src: fp32 master [R][S][A][B] with A=a_valid, B=b_valid; dst (dtype,
+ * channel dims padded to a_pad/b_pad with zeros):
+ *   mode 0: [B][R][S][A]   (conv fwd, K-major "KRSC")
+ *   mode 1: [R][S][A][B]   (conv bwd_data, HWIO)
+ *   mode 2: [R][S][A][B]   (tconv fwd; same as 1, TF [kh,kw,out,in])
+ *   mode 3: [B][R][S][A]   (tconv bwd_data)                             */
+int seg_pack_filter(const float* src, void* dst, int R, int S, int a_valid, int b_valid,
+                    int a_pad, int b_pad, int mode, int dtype, void* stream);
+
+/* ---- ReluGrad + BiasAddGrad (implicit in minimize, FCN.py:340) --------- */
+/* dz = dy * (y > 0) if relu else dy; dbias[k] = sum over pixels of dz
+ * (k < k_valid; dbias may be NULL).  dz may alias dy.
+ * ws >= seg_bias_grad_workspace() (always required). */
+int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int ld_y, void* dz, int ld_dz,
+                      float* dbias, long P, int K, int k_valid, int relu, int dtype,
+                      void* ws, size_t ws_bytes, void* stream);
+size_t seg_bias_grad_workspace(long P, int K);
+
+/* ---- MaxPool / AvgPool 2x2 stride 2 VALID (FCN.py:161-163; utils.py:309) */
+int seg_maxpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy,
+                       int dtype, void* stream);
+/* dx (dense [N,H,W,C], ldx) is fully written; routes dy to the first max
+ * in row-major window order (TF CPU MaxPoolGrad tie rule). */
+int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H,
+                       int W, int C, int ldx, int ldy, int dtype, void* stream);
+int seg_avgpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy,
+                       int dtype, void* stream);
+int seg_avgpool2x2_bwd(const void* dy, void* dx, int N, int H, int W, int C, int ldx, int ldy,
+                       int dtype, void* stream);
+
+/* ---- elementwise -------------------------------------------------------- */
+/* y = a + b  (tf.add, FCN.py:171), dense, n elements. */
+int seg_add(const void* a, const void* b, void* y, long n, int dtype, void* stream);
+/* y = x / kp * floor(kp + U[0,1)), U from a counter hash of (seed, index)
+ * (tf.nn.dropout, FCN.py:167). */
+int seg_dropout_fwd(const void* x, void* y, long n, float keep_prob, uint64_t seed, int dtype,
+                    void* stream);
+int seg_dropout_bwd(const void* dy, void* dx, long n, float keep_prob, uint64_t seed, int dtype,
+                    void* stream);
+/* Frozen-stat BatchNorm (+ReLU): y = relu?(x*scale[c] + shift[c])
+ * (Network/utils/utils.py:300-301).  scale = gamma/sqrt(1+eps). */
+int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const float* gamma,
+                    const float* beta, float eps, long P, int C, int c_valid, int relu,
+                    int dtype, void* stream);
+/* dx = dy*(y>0)*scale; dgamma = sum(dy*(y>0)*x)/sqrt(1+eps); dbeta = sum(dy*(y>0)). */
+int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy,
+                    void* dx, int lddx, const float* gamma, float eps, float* dgamma,
+                    float* dbeta, long P, int C, int c_valid, int relu, int dtype, void* ws,
+                    size_t ws_bytes, void* stream);
+/* resize_bilinear(align_corners=True) (Network/utils/utils.py:329-330). */
+int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW,
+                            int dtype, void* stream);
+/* dx is zeroed then scatter-added (fp32 dx only). */
+int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, int W, int C, int OH,
+                            int OW, int dtype, void* stream);
+/* Channel-slice copy: y[p, 0:C] = x[p, 0:C] (tf.concat building block). */
+int seg_copy_channels(const void* x, int ldx, void* y, int ldy, long P, int C, int dtype,
+                      void* stream);
+/* fp32 NHWC image (values 0..255, c_in channels, H x W) -> dtype NHWC padded
+ * to [N, HP, WP, CP] with zeros (SURVEY.md 0-3 pad policy). */
+int seg_prepare_input(const float* img, void* x, int N, int H, int W, int c_in, int HP, int WP,
+                      int CP, int dtype, void* stream);
+
+/* ---- loss / prediction (FCN.py:334, :111) ------------------------------- */
+/* Per pixel over the valid region (h < valid_h, w < valid_w) of
+ * logits [N,H,W,ld] (classes 0..C-1), labels uint8 class index:
+ *   loss_sum += logsumexp(z) - z[label];
+ *   dlogits = (softmax(z) - onehot) * grad_scale   (0 outside valid region
+ *   and in padding channels).  loss_sum is written (fp32, 1 element). */
+int seg_softmax_xent_fwd_bwd(const void* logits, int ld, const uint8_t* labels, int N, int H,
+                             int W, int C, int valid_h, int valid_w, float grad_scale,
+                             float* loss_sum, void* dlogits, int ld_d, int dtype, void* ws,
+                             size_t ws_bytes, void* stream);
+size_t seg_xent_workspace(int N, int H, int W);
+/* Soft-label variant (labels [N,H,W,C] fp32, e.g. one-hot from process_gt_image). */
+int seg_softmax_xent_soft_fwd_bwd(const void* logits, int ld, const float* labels, int N, int H,
+                                  int W, int C, int valid_h, int valid_w, float grad_scale,
+                                  float* loss_sum, void* dlogits, int ld_d, int dtype, void* ws,
+                                  size_t ws_bytes, void* stream);
+/* pred[p] = argmax_c logits[p, c] (ties -> lowest index). */
+int seg_argmax(const void* logits, int ld, int C, long P, int64_t* pred, int dtype, void* stream);
+/* Confusion matrix counts conf[t*C+p] += 1 over the valid region (mIoU). */
+int seg_confusion(const int64_t* pred, const uint8_t* labels, int N, int H, int W, int valid_h,
+                  int valid_w, int C, unsigned long long* conf, void* stream);
+
+/* ---- AdamOptimizer (FCN.py:338-340), TF1 epsilon placement -------------- */
+/* In place over a flat fp32 parameter buffer:
+ *   g' = g*grad_scale; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2;
+ *   p -= lr*sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps).                    */
+int seg_adam_tf1_step(float* p, const float* g, float* m, float* v, long n, float lr,
+                      float beta1, float beta2, float eps, int t, float grad_scale, void* stream);
+
+/* ---- misc ---------------------------------------------------------------- */
+int seg_fill(void* y, long n, float value, int dtype, void* stream);
+int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);
+const char* seg_status_string(int status);
+int seg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEGKERN_H */

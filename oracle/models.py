@@ -1,0 +1,198 @@
+"""CPU restatements of the reference models (TEST INFRASTRUCTURE ONLY).
+
+`fcn_forward` follows `Network/model/FCN.py:49-114` exactly, including the
+reference's quirks: 14-conv encoder with a
+4-conv block 4, 7x7 SAME conv6, ReLU on conv8, feature-width skip fusion
+(conv_t1 2->512 + pool4, conv_t2 512->256 + pool3) and a 16x16 stride-8
+conv_t3 with variable name `conv_t3/bias` (`:103`).
+
+`fcdensenet_forward` follows `Network/model/FCDenseNet.py:23-163` with the
+layer builders of `Network/utils/utils.py:164-333` (bias-free convs,
+frozen-statistics BN, avg-pool transitions, skip-concat decoder).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import tf1_ops as tf
+
+# (name, out_channels, kernel) in build order, FCN.py:52-86
+FCN_CONVS = [
+    ("conv1_1", 64, 3), ("conv1_2", 64, 3),
+    ("conv2_1", 128, 3), ("conv2_2", 128, 3),
+    ("conv3_1", 256, 3), ("conv3_2", 256, 3), ("conv3_3", 256, 3),
+    ("conv4_1", 512, 3), ("conv4_2", 512, 3), ("conv4_3", 512, 3), ("conv4_4", 512, 3),
+    ("conv5_1", 512, 3), ("conv5_2", 512, 3), ("conv5_3", 512, 3),
+    ("conv6", 4096, 7), ("conv7", 4096, 1),
+]
+POOL_AFTER = {"conv1_2": "pool1", "conv2_2": "pool2", "conv3_3": "pool3",
+              "conv4_4": "pool4", "conv5_3": "pool5"}
+
+
+def fcn_param_shapes(in_channels=3, num_classes=2):
+    """TF variable name -> shape, in creation order (FCN.py:117-159, :101-103)."""
+    shapes = {}
+    c = in_channels
+    for name, k, r in FCN_CONVS:
+        shapes[f"{name}/weights"] = (r, r, c, k)
+        shapes[f"{name}/biases"] = (k,)
+        c = k
+    shapes["conv8/weights"] = (1, 1, 4096, num_classes)
+    shapes["conv8/biases"] = (num_classes,)
+    # deconv_layer: W [4,4, shape[3], num_filters]; num_filters = INPUT depth (FCN.py:143)
+    shapes["conv_t1/weights"] = (4, 4, 512, num_classes)
+    shapes["conv_t1/biases"] = (512,)
+    shapes["conv_t2/weights"] = (4, 4, 256, 512)
+    shapes["conv_t2/biases"] = (256,)
+    shapes["conv_t3/weights"] = (16, 16, num_classes, 256)
+    shapes["conv_t3/bias"] = (num_classes,)
+    return shapes
+
+
+def conv_layer(x, p, name):
+    """FCN.py:117-136: relu(conv2d(x, W, SAME) + b)."""
+    return tf.relu(tf.bias_add(tf.conv2d(x, p[f"{name}/weights"]), p[f"{name}/biases"]))
+
+
+def deconv_layer(x, p, name, out_shape, stride=2):
+    """FCN.py:138-159: conv2d_transpose(x, W, output_shape, s, SAME) + b."""
+    return tf.bias_add(tf.conv2d_transpose(x, p[f"{name}/weights"], out_shape, stride),
+                       p[f"{name}/biases"])
+
+
+def fcn_forward(p, x, keep_prob=1.0, dropout_u=None, num_classes=2, return_acts=False):
+    """Returns (pred [N,H,W,1] int64, logits [N,H,W,C]) like FCN.create() (FCN.py:114)."""
+    acts = {}
+    h = x
+    for name, _, _ in FCN_CONVS[:14]:
+        h = conv_layer(h, p, name)
+        acts[name] = h
+        if name in POOL_AFTER:
+            h = tf.max_pool2x2(h)
+            acts[POOL_AFTER[name]] = h
+    du = dropout_u or {}
+    h = conv_layer(h, p, "conv6")
+    h = tf.dropout(h, keep_prob, du.get("dropout6"))
+    h = conv_layer(h, p, "conv7")
+    h = tf.dropout(h, keep_prob, du.get("dropout7"))
+    conv8 = conv_layer(h, p, "conv8")
+    pool4, pool3 = acts["pool4"], acts["pool3"]
+    t1 = deconv_layer(conv8, p, "conv_t1", tuple(pool4.shape))
+    fuse1 = tf.add(t1, pool4)
+    t2 = deconv_layer(fuse1, p, "conv_t2", tuple(pool3.shape))
+    fuse2 = tf.add(t2, pool3)
+    N, H, W, _ = x.shape
+    t3 = tf.conv2d_transpose(fuse2, p["conv_t3/weights"], (N, H, W, num_classes), 8)
+    logits = tf.bias_add(t3, p["conv_t3/bias"])
+    pred = tf.argmax(logits).unsqueeze(-1)
+    if return_acts:
+        acts.update(conv8=conv8, fuse_1=fuse1, fuse_2=fuse2)
+        return pred, logits, acts
+    return pred, logits
+
+
+# ---------------------------------------------------------------------------
+# FC-DenseNet ("U-Net" config), FCDenseNet.py:83-163
+# ---------------------------------------------------------------------------
+DENSENET_LAYERS = [4, 5, 7, 10, 12, 15]
+DENSENET_GROWTH = 16
+DENSENET_FIRST = 48
+DENSENET_THETA = 0.5
+
+
+class _BNCounter:
+    """tf.layers.batch_normalization auto-names 'batch_normalization', '_1', ..."""
+
+    def __init__(self):
+        self.i = 0
+
+    def next(self):
+        name = "batch_normalization" if self.i == 0 else f"batch_normalization_{self.i}"
+        self.i += 1
+        return name
+
+
+def fcdensenet_param_shapes(in_channels=3, num_classes=2):
+    shapes = {}
+    bn = _BNCounter()
+
+    def conv(name, r, cin, cout):
+        shapes[f"{name}/weights"] = (r, r, cin, cout)
+
+    def bnv(c):
+        n = bn.next()
+        shapes[f"{n}/gamma"] = (c,)
+        shapes[f"{n}/beta"] = (c,)
+
+    conv("dense_init", 3, in_channels, DENSENET_FIRST)
+    c = DENSENET_FIRST
+    skips = []
+    for b, nl in enumerate(DENSENET_LAYERS):
+        name = f"denseblock{b + 1}"
+        cin = c
+        for i in range(nl + 1):
+            ln = f"{name}bottleneck_layer_{i}"
+            bnv(cin)
+            conv(f"{ln}_conv1", 1, cin, 4 * DENSENET_GROWTH)
+            bnv(4 * DENSENET_GROWTH)
+            conv(f"{ln}_conv2", 3, 4 * DENSENET_GROWTH, DENSENET_GROWTH)
+            cin += DENSENET_GROWTH
+        c = cin
+        if b < 5:
+            skips.append(c)
+            bnv(c)
+            conv(f"transition_layer{b + 1}_conv", 1, c, int(c * DENSENET_THETA))
+            c = int(c * DENSENET_THETA)
+    for u in range(5):
+        skip_c = skips[4 - u]
+        shapes[f"transition_up{u + 1}/weights"] = (4, 4, skip_c, c)
+        c = skip_c + skip_c
+    shapes["final_conv/weights"] = (1, 1, c, num_classes)
+    return shapes
+
+
+def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
+    bn = _BNCounter()
+
+    def BN(h):
+        n = bn.next()
+        return tf.batch_norm_frozen(h, p[f"{n}/gamma"], p[f"{n}/beta"])
+
+    def conv(h, name):
+        return tf.conv2d(h, p[f"{name}/weights"])
+
+    def bottleneck(h, name):                       # FCDenseNet.py:23-35
+        h = conv(tf.relu(BN(h)), f"{name}_conv1")
+        h = tf.dropout(h, keep_prob)
+        h = conv(tf.relu(BN(h)), f"{name}_conv2")
+        return tf.dropout(h, keep_prob)
+
+    def dense_block(h, nl, name):                  # FCDenseNet.py:48-61
+        feats = [h]
+        h = bottleneck(h, f"{name}bottleneck_layer_0")
+        feats.append(h)
+        for i in range(nl):
+            h = tf.concat(feats)
+            h = bottleneck(h, f"{name}bottleneck_layer_{i + 1}")
+            feats.append(h)
+        return tf.concat(feats)
+
+    def transition(h, name):                       # FCDenseNet.py:37-46
+        h = tf.relu(BN(h))
+        h = conv(h, f"{name}_conv")
+        return tf.avg_pool2x2(h)
+
+    h = conv(x, "dense_init")
+    dbs = []
+    for b, nl in enumerate(DENSENET_LAYERS):
+        h = dense_block(h, nl, f"denseblock{b + 1}")
+        if b < 5:
+            dbs.append(h)
+            h = transition(h, f"transition_layer{b + 1}")
+    for u in range(5):                              # FCDenseNet.py:141-154
+        skip = dbs[4 - u]
+        t = tf.conv2d_transpose(h, p[f"transition_up{u + 1}/weights"], tuple(skip.shape), 2)
+        h = tf.concat([t, skip])
+    logits = conv(h, "final_conv")
+    pred = tf.argmax(logits).unsqueeze(-1)
+    return pred, logits

@@ -1,0 +1,162 @@
+"""Build and load `libsegkern.so`, the gfx950 HIP library behind the C-ABI in
+`include/segkern.h`.
+
+The library is built in-tree (it travels with the repo snapshot to the GPU
+box) by `build()`; `lib()` loads it with ctypes and fails loudly when it is
+missing -- there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(PKG_DIR, "build")
+LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
+SOURCES = ["igemm.hip", "conv.hip", "eltwise.hip"]
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
+          "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics"]
+
+
+class SegKernelError(RuntimeError):
+    pass
+
+
+def _newer(a, b):
+    return os.path.exists(b) and os.path.getmtime(b) >= os.path.getmtime(a)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every HIP source for gfx950 and link libsegkern.so in-tree."""
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(REPO_DIR, "include", "segkern.h"))
+    newest_header = max(os.path.getmtime(h) for h in headers)
+
+    def compile_one(src):
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        if (not force and _newer(s, o) and os.path.getmtime(o) >= newest_header):
+            return o
+        cmd = [HIPCC, *CFLAGS, "-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise SegKernelError(f"hipcc failed for {src}:\n{r.stderr}")
+        return o
+
+    with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    if force or not os.path.exists(LIB_PATH) or any(
+            os.path.getmtime(o) > os.path.getmtime(LIB_PATH) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise SegKernelError(f"link failed:\n{r.stderr}")
+    return LIB_PATH
+
+
+_LIB = None
+_LOCK = threading.Lock()
+
+
+class SegConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "N", "H", "W", "C", "OH", "OW", "K", "R", "S", "stride_h", "stride_w", "dil_h", "dil_w",
+        "pad_top", "pad_bottom", "pad_left", "pad_right", "ldx", "ldy", "c_valid", "k_valid", "dtype")]
+
+
+class SegEpilogue(ctypes.Structure):
+    _fields_ = [("bias", ctypes.c_void_p), ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
+                ("residual", ctypes.c_void_p), ("ld_residual", ctypes.c_int), ("relu", ctypes.c_int),
+                ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+_DP = ctypes.POINTER(SegConvDesc)
+_EP = ctypes.POINTER(SegEpilogue)
+
+# symbol -> (restype, argtypes); must match include/segkern.h exactly
+SIGNATURES = {
+    "seg_conv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "seg_tconv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "seg_conv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_tconv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_conv_workspace": (_Z, [_DP, _I]),
+    "seg_pack_filter": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_bias_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _P, _Z, _P]),
+    "seg_bias_grad_workspace": (_Z, [_L, _I]),
+    "seg_maxpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_maxpool2x2_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_avgpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_avgpool2x2_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_add": (_I, [_P, _P, _P, _L, _I, _P]),
+    "seg_dropout_fwd": (_I, [_P, _P, _L, _F, ctypes.c_uint64, _I, _P]),
+    "seg_dropout_bwd": (_I, [_P, _P, _L, _F, ctypes.c_uint64, _I, _P]),
+    "seg_bn_relu_fwd": (_I, [_P, _I, _P, _I, _P, _P, _F, _L, _I, _I, _I, _I, _P]),
+    "seg_bn_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _P, _F, _P, _P, _L, _I, _I, _I, _I,
+                             _P, _Z, _P]),
+    "seg_resize_bilinear_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_resize_bilinear_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_copy_channels": (_I, [_P, _I, _P, _I, _L, _I, _I, _P]),
+    "seg_prepare_input": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_softmax_xent_fwd_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I, _P,
+                                      _Z, _P]),
+    "seg_xent_workspace": (_Z, [_I, _I, _I]),
+    "seg_softmax_xent_soft_fwd_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I,
+                                           _P, _Z, _P]),
+    "seg_argmax": (_I, [_P, _I, _I, _L, _P, _I, _P]),
+    "seg_confusion": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "seg_adam_tf1_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _I, _F, _P]),
+    "seg_fill": (_I, [_P, _L, _F, _I, _P]),
+    "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
+    "seg_status_string": (ctypes.c_char_p, [_I]),
+    "seg_version": (_I, []),
+}
+
+
+def load(path: str = LIB_PATH):
+    """Load the library and bind every C-ABI symbol (no GPU work)."""
+    if not os.path.exists(path):
+        raise SegKernelError(
+            f"{path} not found: the HIP kernel library is required (no CPU fallback). "
+            "Run `python -c 'import __graft_entry__ as g; g.build()'` first.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        with _LOCK:
+            if _LIB is None:
+                _LIB = load()
+    return _LIB
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = lib().seg_status_string(status).decode()
+        if status == 2:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg} (status {status})")

@@ -1,0 +1,294 @@
+// C-ABI convolution entry points: Conv2D / Conv2DBackpropInput /
+// Conv2DBackpropFilter and conv2d_transpose (forward + both gradients),
+// each mapped onto the implicit-GEMM kernels of igemm.hip.
+#include "common.h"
+#include "igemm.h"
+
+using seg::NTParams;
+using seg::TNParams;
+
+static inline int round8(int c) { return (c + 7) & ~7; }
+
+static int same_pads(int in, int k, int s, int d, int* out, int* pb, int* pa) {
+    const int keff = k + (k - 1) * (d - 1);
+    *out = (in + s - 1) / s;
+    int total = (*out - 1) * s + keff - in;
+    if (total < 0) total = 0;
+    *pb = total / 2;
+    *pa = total - total / 2;
+    return 0;
+}
+
+static int valid_out(int in, int k, int s, int d) {
+    const int keff = k + (k - 1) * (d - 1);
+    return (in - keff) / s + 1;
+}
+
+static int check_desc(const seg_conv_desc* d) {
+    if (!d) return SEG_EINVAL;
+    if (d->dtype != SEG_F32 && d->dtype != SEG_BF16) return SEG_EINVAL;
+    if (d->N <= 0 || d->H <= 0 || d->W <= 0 || d->OH <= 0 || d->OW <= 0 || d->R <= 0 || d->S <= 0) return SEG_ESHAPE;
+    if ((d->C & 7) || (d->K & 7) || (d->ldx & 7) || (d->ldy & 7)) return SEG_EALIGN;
+    if (d->ldx < d->C || d->ldy < d->K) return SEG_EALIGN;
+    if (d->c_valid > d->C || d->k_valid > d->K || d->c_valid <= 0 || d->k_valid <= 0) return SEG_EINVAL;
+    return SEG_OK;
+}
+
+extern "C" int seg_conv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int K, int R, int S,
+                                  int stride, int dilation, int padding, int dtype) {
+    if (!d || stride <= 0 || dilation <= 0 || N <= 0 || H <= 0 || W <= 0 || C <= 0 || K <= 0) return SEG_EINVAL;
+    seg_conv_desc z = {};
+    z.N = N; z.H = H; z.W = W;
+    z.C = round8(C); z.K = round8(K);
+    z.c_valid = C; z.k_valid = K;
+    z.R = R; z.S = S;
+    z.stride_h = z.stride_w = stride;
+    z.dil_h = z.dil_w = dilation;
+    if (padding == 0) {
+        same_pads(H, R, stride, dilation, &z.OH, &z.pad_top, &z.pad_bottom);
+        same_pads(W, S, stride, dilation, &z.OW, &z.pad_left, &z.pad_right);
+    } else {
+        z.OH = valid_out(H, R, stride, dilation);
+        z.OW = valid_out(W, S, stride, dilation);
+        if (z.OH <= 0 || z.OW <= 0) return SEG_ESHAPE;
+    }
+    z.ldx = z.C; z.ldy = z.K;
+    z.dtype = dtype;
+    *d = z;
+    return SEG_OK;
+}
+
+extern "C" int seg_tconv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int OH, int OW, int K,
+                                   int R, int S, int stride, int padding, int dtype) {
+    if (!d || stride <= 0 || N <= 0 || H <= 0 || W <= 0 || C <= 0 || K <= 0 || OH <= 0 || OW <= 0) return SEG_EINVAL;
+    seg_conv_desc z = {};
+    z.N = N; z.H = H; z.W = W; z.OH = OH; z.OW = OW;
+    z.C = round8(C); z.K = round8(K);
+    z.c_valid = C; z.k_valid = K;
+    z.R = R; z.S = S;
+    z.stride_h = z.stride_w = stride;
+    z.dil_h = z.dil_w = 1;
+    // TF: the forward conv of the output shape must give the input shape
+    int eh, ew;
+    if (padding == 0) {
+        same_pads(OH, R, stride, 1, &eh, &z.pad_top, &z.pad_bottom);
+        same_pads(OW, S, stride, 1, &ew, &z.pad_left, &z.pad_right);
+    } else {
+        eh = valid_out(OH, R, stride, 1);
+        ew = valid_out(OW, S, stride, 1);
+    }
+    if (eh != H || ew != W) return SEG_ESHAPE;
+    z.ldx = z.C; z.ldy = z.K;
+    z.dtype = dtype;
+    *d = z;
+    return SEG_OK;
+}
+
+static seg::EpiParams make_epi(const seg_epilogue* e, int n_valid, long res_img) {
+    seg::EpiParams r = {};
+    r.n_valid = n_valid;
+    r.keep_prob = 1.f;
+    if (e) {
+        r.bias = e->bias; r.scale = e->scale; r.shift = e->shift;
+        r.residual = e->residual; r.ld_res = e->ld_residual; r.res_img = res_img;
+        r.relu = e->relu; r.keep_prob = e->keep_prob > 0.f ? e->keep_prob : 1.f; r.seed = e->seed;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// parameter builders (shared by the launchers and the workspace queries)
+// ---------------------------------------------------------------------------
+static NTParams conv_fwd_params(const seg_conv_desc* d) {
+    NTParams p = {};
+    p.M = d->N * d->OH * d->OW; p.N = d->K; p.K = d->R * d->S * d->C;
+    p.x_img = (long)d->H * d->W * d->ldx; p.IH = d->H; p.IW = d->W; p.C = d->C; p.ldx = d->ldx;
+    p.Ha = d->OH; p.Wa = d->OW; p.ish = d->stride_h; p.isw = d->stride_w;
+    p.ioh = -d->pad_top; p.iow = -d->pad_left; p.tsh = d->dil_h; p.tsw = d->dil_w; p.taps_w = d->S;
+    p.w_col = (long)d->R * d->S * d->C; p.w_tap = d->C; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
+    p.y_img = (long)d->OH * d->OW * d->ldy; p.OH = d->OH; p.OW = d->OW; p.ldy = d->ldy; p.osh = 1; p.osw = 1;
+    return p;
+}
+
+static NTParams conv_bwd_data_params(const seg_conv_desc* d) {
+    NTParams p = {};
+    p.M = d->N * d->H * d->W; p.N = d->C; p.K = d->R * d->S * d->K;
+    p.x_img = (long)d->OH * d->OW * d->ldy; p.IH = d->OH; p.IW = d->OW; p.C = d->K; p.ldx = d->ldy;
+    p.Ha = d->H; p.Wa = d->W; p.ish = 1; p.isw = 1;
+    p.ioh = d->pad_top; p.iow = d->pad_left; p.tsh = -d->dil_h; p.tsw = -d->dil_w; p.taps_w = d->S;
+    p.w_col = d->K; p.w_tap = (long)d->C * d->K; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
+    p.y_img = (long)d->H * d->W * d->ldx; p.OH = d->H; p.OW = d->W; p.ldy = d->ldx; p.osh = 1; p.osw = 1;
+    p.epi.n_valid = d->C; p.epi.keep_prob = 1.f;
+    return p;
+}
+
+static TNParams conv_bwd_filter_params(const seg_conv_desc* d) {
+    TNParams p = {};
+    p.M = d->R * d->S * d->C; p.N = d->K; p.P = d->N * d->OH * d->OW;
+    p.x_img = (long)d->H * d->W * d->ldx; p.IH = d->H; p.IW = d->W; p.Cg = d->C; p.ldx = d->ldx;
+    p.Ha = d->OH; p.Wa = d->OW; p.ish = d->stride_h; p.isw = d->stride_w;
+    p.ioh = -d->pad_top; p.iow = -d->pad_left; p.tsh = d->dil_h; p.tsw = d->dil_w; p.taps_w = d->S;
+    p.ldb = d->ldy;
+    p.o_tap = (long)d->c_valid * d->k_valid; p.o_c = d->k_valid; p.o_n = 1;
+    p.c_valid = d->c_valid; p.n_valid = d->k_valid;
+    return p;
+}
+
+static NTParams tconv_fwd_params(const seg_conv_desc* d) {
+    NTParams p = {};
+    const int sh = d->stride_h, sw = d->stride_w;
+    p.N = d->K; p.K = (d->R / sh) * (d->S / sw) * d->C;
+    p.x_img = (long)d->H * d->W * d->ldx; p.IH = d->H; p.IW = d->W; p.C = d->C; p.ldx = d->ldx;
+    p.ish = 1; p.isw = 1; p.tsh = -1; p.tsw = -1; p.taps_w = d->S / sw;
+    p.w_col = d->C; p.w_tap = (long)d->K * d->C; p.rstep = sh; p.sstep = sw; p.Sfull = d->S;
+    p.y_img = (long)d->OH * d->OW * d->ldy; p.OH = d->OH; p.OW = d->OW; p.ldy = d->ldy; p.osh = sh; p.osw = sw;
+    p.phase = 1; p.st_h = sh; p.st_w = sw; p.pad_t = d->pad_top; p.pad_l = d->pad_left; p.Nimg = d->N;
+    p.M = d->N * ((d->OH + sh - 1) / sh) * ((d->OW + sw - 1) / sw);   // max over phases
+    p.Ha = (d->OH + sh - 1) / sh; p.Wa = (d->OW + sw - 1) / sw;
+    return p;
+}
+
+static NTParams tconv_bwd_data_params(const seg_conv_desc* d) {
+    NTParams p = {};
+    p.M = d->N * d->H * d->W; p.N = d->C; p.K = d->R * d->S * d->K;
+    p.x_img = (long)d->OH * d->OW * d->ldy; p.IH = d->OH; p.IW = d->OW; p.C = d->K; p.ldx = d->ldy;
+    p.Ha = d->H; p.Wa = d->W; p.ish = d->stride_h; p.isw = d->stride_w;
+    p.ioh = -d->pad_top; p.iow = -d->pad_left; p.tsh = 1; p.tsw = 1; p.taps_w = d->S;
+    p.w_col = (long)d->R * d->S * d->K; p.w_tap = d->K; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
+    p.y_img = (long)d->H * d->W * d->ldx; p.OH = d->H; p.OW = d->W; p.ldy = d->ldx; p.osh = 1; p.osw = 1;
+    p.epi.n_valid = d->C; p.epi.keep_prob = 1.f;
+    return p;
+}
+
+static TNParams tconv_bwd_filter_params(const seg_conv_desc* d) {
+    TNParams p = {};
+    p.M = d->R * d->S * d->K; p.N = d->C; p.P = d->N * d->H * d->W;
+    p.x_img = (long)d->OH * d->OW * d->ldy; p.IH = d->OH; p.IW = d->OW; p.Cg = d->K; p.ldx = d->ldy;
+    p.Ha = d->H; p.Wa = d->W; p.ish = d->stride_h; p.isw = d->stride_w;
+    p.ioh = -d->pad_top; p.iow = -d->pad_left; p.tsh = 1; p.tsw = 1; p.taps_w = d->S;
+    p.ldb = d->ldx;
+    p.o_tap = (long)d->k_valid * d->c_valid; p.o_c = d->c_valid; p.o_n = 1;
+    p.c_valid = d->k_valid; p.n_valid = d->c_valid;
+    return p;
+}
+
+extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
+    if (check_desc(d) != SEG_OK) return 0;
+    switch (op) {
+        case 0: { NTParams p = conv_fwd_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
+        case 1: { NTParams p = conv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
+        case 2: { TNParams p = conv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
+        case 3: return 0;
+        case 4: { NTParams p = tconv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
+        case 5: { TNParams p = tconv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
+    }
+    return 0;
+}
+
+extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
+                              void* y, void* ws, size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !w || !y) return SEG_EINVAL;
+    NTParams p = conv_fwd_params(d);
+    p.x = x; p.w = w; p.y = y;
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, void* dx, void* ws,
+                                   size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!dy || !w || !dx) return SEG_EINVAL;
+    if (d->stride_h != 1 || d->stride_w != 1) return SEG_EINVAL;  // FCN / FC-DenseNet convs are stride 1
+    NTParams p = conv_bwd_data_params(d);
+    p.x = dy; p.w = w; p.y = dx;
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
+                                     size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !dy || !dw) return SEG_EINVAL;
+    TNParams p = conv_bwd_filter_params(d);
+    p.x = x; p.b = dy; p.out = dw;
+    return seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
+                               void* y, void* ws, size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !w || !y) return SEG_EINVAL;
+    if (d->R % d->stride_h || d->S % d->stride_w) return SEG_EINVAL;
+    NTParams p = tconv_fwd_params(d);
+    p.x = x; p.w = w; p.y = y;
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    return seg::launch_nt(p, d->dtype, d->stride_h * d->stride_w, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, void* dx, void* ws,
+                                    size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!dy || !w || !dx) return SEG_EINVAL;
+    NTParams p = tconv_bwd_data_params(d);
+    p.x = dy; p.w = w; p.y = dx;
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
+                                      size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !dy || !dw) return SEG_EINVAL;
+    TNParams p = tconv_bwd_filter_params(d);
+    p.x = dy; p.b = x; p.out = dw;
+    return seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------
+// filter packing
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_filter_k(const float* __restrict__ src, T* __restrict__ dst, int R, int S, int av, int bv,
+                              int ap, int bp, int bmajor) {
+    const long total = (long)R * S * ap * bp;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        int a, b, rs;
+        if (bmajor) {  // dst [bp][R][S][ap]
+            a = (int)(i % ap);
+            long t = i / ap;
+            rs = (int)(t % (R * S));
+            b = (int)(t / (R * S));
+        } else {       // dst [R][S][ap][bp]
+            b = (int)(i % bp);
+            long t = i / bp;
+            a = (int)(t % ap);
+            rs = (int)(t / ap);
+        }
+        float v = 0.f;
+        if (a < av && b < bv) v = src[((long)rs * av + a) * bv + b];
+        dst[i] = from_f32<T>(v);
+    }
+}
+
+extern "C" int seg_pack_filter(const float* src, void* dst, int R, int S, int a_valid, int b_valid, int a_pad,
+                               int b_pad, int mode, int dtype, void* stream) {
+    if (!src || !dst || a_pad < a_valid || b_pad < b_valid || mode < 0 || mode > 3) return SEG_EINVAL;
+    const int bmajor = (mode == 0 || mode == 3);
+    const long total = (long)R * S * a_pad * b_pad;
+    const int grid = seg_grid_1d(total, 256);
+    if (dtype == SEG_BF16)
+        hipLaunchKernelGGL(pack_filter_k<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst, R,
+                           S, a_valid, b_valid, a_pad, b_pad, bmajor);
+    else if (dtype == SEG_F32)
+        hipLaunchKernelGGL(pack_filter_k<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, (float*)dst, R,
+                           S, a_valid, b_valid, a_pad, b_pad, bmajor);
+    else
+        return SEG_EINVAL;
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}

@@ -1,0 +1,861 @@
+// HBM-bound kernels of the training path: bias/ReLU gradients, pooling,
+// dropout, frozen-stat BatchNorm+ReLU, bilinear resize, softmax
+// cross-entropy, argmax / confusion counts, TF1 Adam, and small utilities.
+// All per-pixel work moves 16-byte chunks (8 bf16 / 4 fp32) per lane;
+// channel reductions are two-stage (per-workgroup partials in a caller
+// workspace, then one ordered pass) so results are run-to-run deterministic.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ uint4 ldc(const T* p) { return *reinterpret_cast<const uint4*>(p); }
+template <typename T>
+__device__ __forceinline__ void stc(T* p, const uint4& v) { *reinterpret_cast<uint4*>(p) = v; }
+
+constexpr int RED_BLOCKS = 1024;
+
+// ---------------------------------------------------------------------------
+// channel-reduction skeleton: each workgroup covers a contiguous pixel range
+// and all K channels; LPP lanes span the channel chunks of one pixel.
+// ---------------------------------------------------------------------------
+struct RedGeom {
+    int CK, LPP, rows, iters;
+};
+__host__ __device__ inline RedGeom red_geom(int K, int epc) {
+    RedGeom g;
+    g.CK = K / epc;
+    g.LPP = g.CK < 256 ? g.CK : 256;
+    g.rows = 256 / g.LPP;
+    g.iters = (g.CK + 255) / 256;
+    return g;
+}
+
+// ReluGrad + BiasAddGrad
+template <typename T>
+__global__ __launch_bounds__(256) void bias_relu_bwd_k(const T* __restrict__ dy, int ld_dy, const T* __restrict__ y,
+                                                       int ld_y, T* __restrict__ dz, int ld_dz, float* __restrict__ part,
+                                                       long P, int K, int relu) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    extern __shared__ __attribute__((aligned(16))) float red[];
+    const RedGeom g = red_geom(K, EPC);
+    const int t = threadIdx.x;
+    const int c8 = t % g.LPP, prow = t / g.LPP;
+    const bool active = prow < g.rows;
+    const long per = (P + gridDim.x - 1) / gridDim.x;
+    const long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+    constexpr int MAXIT = 16 / EPC;
+    float acc[MAXIT][EPC];
+#pragma unroll
+    for (int j = 0; j < MAXIT; ++j)
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) acc[j][e] = 0.f;
+    if (active) {
+        for (long pix = p0 + prow; pix < p1; pix += g.rows) {
+#pragma unroll
+            for (int j = 0; j < MAXIT; ++j) {
+                if (j >= g.iters) break;
+                const int cc = c8 + j * g.LPP;
+                if (cc >= g.CK) break;
+                float d[EPC];
+                Chunk<T>::unpack(ldc(dy + pix * ld_dy + cc * EPC), d);
+                if (relu) {
+                    float yy[EPC];
+                    Chunk<T>::unpack(ldc(y + pix * ld_y + cc * EPC), yy);
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) d[e] = yy[e] > 0.f ? d[e] : 0.f;
+                    stc(dz + pix * ld_dz + cc * EPC, Chunk<T>::pack(d));
+                } else if (dz != dy) {
+                    stc(dz + pix * ld_dz + cc * EPC, Chunk<T>::pack(d));
+                }
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) acc[j][e] += d[e];
+            }
+        }
+    }
+    // block reduction over prow: red[prow][K]
+#pragma unroll
+    for (int j = 0; j < MAXIT; ++j) {
+        const int cc = c8 + j * g.LPP;
+        if (active && j < g.iters && cc < g.CK)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) red[prow * K + cc * EPC + e] = acc[j][e];
+    }
+    __syncthreads();
+    for (int k = t; k < K; k += 256) {
+        float s = 0.f;
+        for (int r = 0; r < g.rows; ++r) s += red[r * K + k];
+        part[(long)blockIdx.x * K + k] = s;
+    }
+}
+
+__global__ void reduce_rows_k(const float* __restrict__ part, int nrows, int K, int k_valid, float* __restrict__ out,
+                              int ncols_out_stride) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= k_valid) return;
+    float s = 0.f;
+    for (int r = 0; r < nrows; ++r) s += part[(long)r * K + k];
+    out[k] = s;
+}
+
+// ---------------------------------------------------------------------------
+// 2x2 pooling
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int ldx, int ldy) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2, OW = W / 2, CK = C / EPC;
+    const long total = (long)N * OH * OW * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cc = (int)(i % CK);
+        long t = i / CK;
+        const int ow = (int)(t % OW);
+        t /= OW;
+        const int oh = (int)(t % OH);
+        const int n = (int)(t / OH);
+        const T* b = x + (((long)n * H + 2 * oh) * W + 2 * ow) * ldx + cc * EPC;
+        float v0[EPC], v1[EPC], v2[EPC], v3[EPC];
+        Chunk<T>::unpack(ldc(b), v0);
+        Chunk<T>::unpack(ldc(b + ldx), v1);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx), v2);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx + ldx), v3);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            float m = v0[e];
+            m = v1[e] > m ? v1[e] : m;
+            m = v2[e] > m ? v2[e] : m;
+            m = v3[e] > m ? v3[e] : m;
+            v0[e] = m;
+        }
+        stc(y + (((long)n * OH + oh) * OW + ow) * ldy + cc * EPC, Chunk<T>::pack(v0));
+    }
+}
+
+// One thread per (2x2 input block, chunk); blocks past the pooled region
+// (odd H / W) receive zero gradient.
+template <typename T>
+__global__ void maxpool_bwd_k(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, int N, int H,
+                              int W, int C, int ldx, int ldy) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2, OW = W / 2, BH = (H + 1) / 2, BW = (W + 1) / 2, CK = C / EPC;
+    const long total = (long)N * BH * BW * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cc = (int)(i % CK);
+        long t = i / CK;
+        const int bw = (int)(t % BW);
+        t /= BW;
+        const int bh = (int)(t % BH);
+        const int n = (int)(t / BH);
+        const long base = (((long)n * H + 2 * bh) * W + 2 * bw) * ldx + cc * EPC;
+        float o[4][EPC];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) o[q][e] = 0.f;
+        if (bh < OH && bw < OW) {
+            float v[4][EPC], d[EPC];
+            Chunk<T>::unpack(ldc(x + base), v[0]);
+            Chunk<T>::unpack(ldc(x + base + ldx), v[1]);
+            Chunk<T>::unpack(ldc(x + base + (long)W * ldx), v[2]);
+            Chunk<T>::unpack(ldc(x + base + (long)W * ldx + ldx), v[3]);
+            Chunk<T>::unpack(ldc(dy + (((long)n * OH + bh) * OW + bw) * ldy + cc * EPC), d);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                int a = 0;
+                float m = v[0][e];
+                if (v[1][e] > m) { m = v[1][e]; a = 1; }
+                if (v[2][e] > m) { m = v[2][e]; a = 2; }
+                if (v[3][e] > m) { m = v[3][e]; a = 3; }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q][e] = (q == a) ? d[e] : 0.f;
+            }
+        }
+        const bool h1 = 2 * bh + 1 < H, w1 = 2 * bw + 1 < W;
+        stc(dx + base, Chunk<T>::pack(o[0]));
+        if (w1) stc(dx + base + ldx, Chunk<T>::pack(o[1]));
+        if (h1) stc(dx + base + (long)W * ldx, Chunk<T>::pack(o[2]));
+        if (h1 && w1) stc(dx + base + (long)W * ldx + ldx, Chunk<T>::pack(o[3]));
+    }
+}
+
+template <typename T>
+__global__ void avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int ldx, int ldy) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2, OW = W / 2, CK = C / EPC;
+    const long total = (long)N * OH * OW * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cc = (int)(i % CK);
+        long t = i / CK;
+        const int ow = (int)(t % OW);
+        t /= OW;
+        const int oh = (int)(t % OH);
+        const int n = (int)(t / OH);
+        const T* b = x + (((long)n * H + 2 * oh) * W + 2 * ow) * ldx + cc * EPC;
+        float v0[EPC], v1[EPC], v2[EPC], v3[EPC];
+        Chunk<T>::unpack(ldc(b), v0);
+        Chunk<T>::unpack(ldc(b + ldx), v1);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx), v2);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx + ldx), v3);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v0[e] = ((v0[e] + v1[e]) + (v2[e] + v3[e])) * 0.25f;
+        stc(y + (((long)n * OH + oh) * OW + ow) * ldy + cc * EPC, Chunk<T>::pack(v0));
+    }
+}
+
+template <typename T>
+__global__ void avgpool_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C, int ldx, int ldy) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2, OW = W / 2, BH = (H + 1) / 2, BW = (W + 1) / 2, CK = C / EPC;
+    const long total = (long)N * BH * BW * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cc = (int)(i % CK);
+        long t = i / CK;
+        const int bw = (int)(t % BW);
+        t /= BW;
+        const int bh = (int)(t % BH);
+        const int n = (int)(t / BH);
+        const long base = (((long)n * H + 2 * bh) * W + 2 * bw) * ldx + cc * EPC;
+        float d[EPC];
+        if (bh < OH && bw < OW) {
+            Chunk<T>::unpack(ldc(dy + (((long)n * OH + bh) * OW + bw) * ldy + cc * EPC), d);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) d[e] *= 0.25f;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) d[e] = 0.f;
+        }
+        const uint4 v = Chunk<T>::pack(d);
+        const bool h1 = 2 * bh + 1 < H, w1 = 2 * bw + 1 < W;
+        stc(dx + base, v);
+        if (w1) stc(dx + base + ldx, v);
+        if (h1) stc(dx + base + (long)W * ldx, v);
+        if (h1 && w1) stc(dx + base + (long)W * ldx + ldx, v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// elementwise
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void add_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f32<T>(to_f32(a[i]) + to_f32(b[i]));
+}
+
+template <typename T>
+__global__ void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n, float kp, uint64_t seed) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float u = seg_uniform(seed, (uint64_t)i);
+        y[i] = from_f32<T>((to_f32(x[i]) / kp) * floorf(kp + u));
+    }
+}
+
+template <typename T>
+__global__ void fill_k(T* y, long n, float v) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f32<T>(v);
+}
+
+template <typename A, typename B>
+__global__ void cast_k(const A* __restrict__ x, B* __restrict__ y, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f32<B>(to_f32(x[i]));
+}
+
+template <typename T>
+__global__ void copy_channels_k(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, long P, int C) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int CK = C / EPC;
+    const long total = P * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / CK;
+        const int cc = (int)(i - p * CK);
+        stc(y + p * ldy + cc * EPC, ldc(x + p * ldx + cc * EPC));
+    }
+}
+
+template <typename T>
+__global__ void prepare_input_k(const float* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
+                                int WP, int CP) {
+    const long total = (long)N * HP * WP * CP;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % CP);
+        long t = i / CP;
+        const int w = (int)(t % WP);
+        t /= WP;
+        const int h = (int)(t % HP);
+        const int n = (int)(t / HP);
+        float v = 0.f;
+        if (c < cin && h < H && w < W) v = img[(((long)n * H + h) * W + w) * cin + c];
+        x[i] = from_f32<T>(v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// frozen-stat BatchNorm (+ ReLU)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void bn_relu_fwd_k(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, float inv, long P, int C, int cv, int relu) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int CK = C / EPC;
+    const long total = P * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / CK;
+        const int cc = (int)(i - p * CK);
+        float v[EPC];
+        Chunk<T>::unpack(ldc(x + p * ldx + cc * EPC), v);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            const int c = cc * EPC + e;
+            float o = 0.f;
+            if (c < cv) {
+                o = v[e] * (gamma[c] * inv) + beta[c];
+                if (relu) o = fmaxf(o, 0.f);
+            }
+            v[e] = o;
+        }
+        stc(y + p * ldy + cc * EPC, Chunk<T>::pack(v));
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, int ldx, const T* __restrict__ y, int ldy,
+                                                     const T* __restrict__ dy, int lddy, T* __restrict__ dx, int lddx,
+                                                     const float* __restrict__ gamma, float inv,
+                                                     float* __restrict__ part, long P, int C, int cv, int relu) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    extern __shared__ __attribute__((aligned(16))) float red[];
+    const RedGeom g = red_geom(C, EPC);
+    const int t = threadIdx.x;
+    const int c8 = t % g.LPP, prow = t / g.LPP;
+    const bool active = prow < g.rows;
+    const long per = (P + gridDim.x - 1) / gridDim.x;
+    const long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+    constexpr int MAXIT = 16 / EPC;
+    float sg[MAXIT][EPC], sb[MAXIT][EPC];
+#pragma unroll
+    for (int j = 0; j < MAXIT; ++j)
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) sg[j][e] = sb[j][e] = 0.f;
+    if (active) {
+        for (long pix = p0 + prow; pix < p1; pix += g.rows) {
+#pragma unroll
+            for (int j = 0; j < MAXIT; ++j) {
+                if (j >= g.iters) break;
+                const int cc = c8 + j * g.LPP;
+                if (cc >= g.CK) break;
+                float xv[EPC], yv[EPC], d[EPC];
+                Chunk<T>::unpack(ldc(x + pix * ldx + cc * EPC), xv);
+                Chunk<T>::unpack(ldc(y + pix * ldy + cc * EPC), yv);
+                Chunk<T>::unpack(ldc(dy + pix * lddy + cc * EPC), d);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                    const int c = cc * EPC + e;
+                    float dz = (relu && !(yv[e] > 0.f)) ? 0.f : d[e];
+                    if (c >= cv) dz = 0.f;
+                    sb[j][e] += dz;
+                    sg[j][e] += dz * xv[e];
+                    d[e] = c < cv ? dz * (gamma[c] * inv) : 0.f;
+                }
+                stc(dx + pix * lddx + cc * EPC, Chunk<T>::pack(d));
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXIT; ++j) {
+        const int cc = c8 + j * g.LPP;
+        if (active && j < g.iters && cc < g.CK)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                red[prow * 2 * C + cc * EPC + e] = sg[j][e];
+                red[prow * 2 * C + C + cc * EPC + e] = sb[j][e];
+            }
+    }
+    __syncthreads();
+    for (int k = t; k < 2 * C; k += 256) {
+        float s = 0.f;
+        for (int r = 0; r < g.rows; ++r) s += red[r * 2 * C + k];
+        part[(long)blockIdx.x * 2 * C + k] = s;
+    }
+}
+
+__global__ void bn_finish_k(const float* __restrict__ part, int nrows, int C, int cv, float inv, float* dgamma,
+                            float* dbeta) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cv) return;
+    float g = 0.f, b = 0.f;
+    for (int r = 0; r < nrows; ++r) {
+        g += part[(long)r * 2 * C + k];
+        b += part[(long)r * 2 * C + C + k];
+    }
+    dgamma[k] = g * inv;
+    dbeta[k] = b;
+}
+
+// ---------------------------------------------------------------------------
+// resize_bilinear(align_corners=True)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void resize_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int OH, int OW) {
+    const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+    const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+    const long total = (long)N * OH * OW * C;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        long t = i / C;
+        const int ow = (int)(t % OW);
+        t /= OW;
+        const int oh = (int)(t % OH);
+        const int n = (int)(t / OH);
+        const float fy = oh * sh, fx = ow * sw;
+        const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
+        const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+        const float ly = fy - y0, lx = fx - x0;
+        const T* b = x + (long)n * H * W * C + c;
+        const float tl = to_f32(b[((long)y0 * W + x0) * C]), tr = to_f32(b[((long)y0 * W + x1) * C]);
+        const float bl = to_f32(b[((long)y1 * W + x0) * C]), br = to_f32(b[((long)y1 * W + x1) * C]);
+        const float top = tl + (tr - tl) * lx, bot = bl + (br - bl) * lx;
+        y[i] = from_f32<T>(top + (bot - top) * ly);
+    }
+}
+
+template <typename T>
+__global__ void resize_bwd_k(const T* __restrict__ dy, float* __restrict__ dx, int N, int H, int W, int C, int OH, int OW) {
+    const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+    const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+    const long total = (long)N * OH * OW * C;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        long t = i / C;
+        const int ow = (int)(t % OW);
+        t /= OW;
+        const int oh = (int)(t % OH);
+        const int n = (int)(t / OH);
+        const float fy = oh * sh, fx = ow * sw;
+        const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
+        const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+        const float ly = fy - y0, lx = fx - x0;
+        const float g = to_f32(dy[i]);
+        float* b = dx + (long)n * H * W * C + c;
+        atomicAdd(b + ((long)y0 * W + x0) * C, g * (1.f - ly) * (1.f - lx));
+        atomicAdd(b + ((long)y0 * W + x1) * C, g * (1.f - ly) * lx);
+        atomicAdd(b + ((long)y1 * W + x0) * C, g * ly * (1.f - lx));
+        atomicAdd(b + ((long)y1 * W + x1) * C, g * ly * lx);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// softmax cross-entropy (fused forward + backward) and prediction
+// ---------------------------------------------------------------------------
+constexpr int XENT_MAXC = 16;
+
+template <typename T, bool SOFT>
+__global__ __launch_bounds__(256) void xent_k(const T* __restrict__ logits, int ld, const uint8_t* __restrict__ lab_idx,
+                                              const float* __restrict__ lab_soft, int N, int H, int W, int C,
+                                              int vh, int vw, float scale, T* __restrict__ dlog, int ldd,
+                                              float* __restrict__ part) {
+    __shared__ float wsum[4];
+    const long P = (long)N * H * W;
+    float lsum = 0.f;
+    for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+        const int w = (int)(p % W);
+        const int h = (int)((p / W) % H);
+        const bool valid = h < vh && w < vw;
+        float z[XENT_MAXC];
+        float mx = -INFINITY;
+        for (int c = 0; c < C; ++c) {
+            z[c] = to_f32(logits[p * ld + c]);
+            mx = fmaxf(mx, z[c]);
+        }
+        float se = 0.f;
+        for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
+        const float lse = mx + __logf(se);
+        const float inv = 1.f / se;
+        float ysum = 0.f, yz = 0.f;
+        for (int c = 0; c < C; ++c) {
+            float yc;
+            if (SOFT) yc = lab_soft[p * C + c];
+            else yc = (lab_idx[p] == c) ? 1.f : 0.f;
+            ysum += yc;
+            yz += yc * z[c];
+        }
+        for (int c = 0; c < C; ++c) {
+            float yc;
+            if (SOFT) yc = lab_soft[p * C + c];
+            else yc = (lab_idx[p] == c) ? 1.f : 0.f;
+            const float g = valid ? (__expf(z[c] - mx) * inv * ysum - yc) * scale : 0.f;
+            dlog[p * ldd + c] = from_f32<T>(g);
+        }
+        for (int c = C; c < ldd; ++c) dlog[p * ldd + c] = from_f32<T>(0.f);
+        if (valid) lsum += ysum * lse - yz;
+    }
+    // wave64 then workgroup reduction
+    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_down(lsum, off, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+__global__ void sum_k(const float* __restrict__ part, int n, float* out) {
+    __shared__ float s[256];
+    float v = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) v += part[i];
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = s[0];
+}
+
+template <typename T>
+__global__ void argmax_k(const T* __restrict__ logits, int ld, int C, long P, int64_t* __restrict__ pred) {
+    for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+        float best = to_f32(logits[p * ld]);
+        int arg = 0;
+        for (int c = 1; c < C; ++c) {
+            const float v = to_f32(logits[p * ld + c]);
+            if (v > best) { best = v; arg = c; }
+        }
+        pred[p] = arg;
+    }
+}
+
+__global__ void confusion_k(const int64_t* __restrict__ pred, const uint8_t* __restrict__ lab, int N, int H, int W,
+                            int vh, int vw, int C, unsigned long long* conf) {
+    const long P = (long)N * H * W;
+    for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+        const int w = (int)(p % W);
+        const int h = (int)((p / W) % H);
+        if (h >= vh || w >= vw) continue;
+        const int t = lab[p], q = (int)pred[p];
+        if (t < C && q < C) atomicAdd(conf + t * C + q, 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TF1 Adam over a flat fp32 buffer (4 params / lane / iteration)
+// ---------------------------------------------------------------------------
+__global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                       long n, float lr_t, float b1, float b2, float eps, float gs) {
+    const long n4 = n / 4;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+        float4 pp = reinterpret_cast<float4*>(p)[i];
+        const float4 gg = reinterpret_cast<const float4*>(g)[i];
+        float4 mm = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+#define ADAM1(c)                                                  \
+    {                                                             \
+        const float gc = gg.c * gs;                               \
+        mm.c = b1 * mm.c + (1.f - b1) * gc;                       \
+        vv.c = b2 * vv.c + (1.f - b2) * gc * gc;                  \
+        pp.c = pp.c - lr_t * mm.c / (sqrtf(vv.c) + eps);          \
+    }
+        ADAM1(x) ADAM1(y) ADAM1(z) ADAM1(w)
+#undef ADAM1
+        reinterpret_cast<float4*>(p)[i] = pp;
+        reinterpret_cast<float4*>(m)[i] = mm;
+        reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float gc = g[i] * gs;
+        m[i] = b1 * m[i] + (1.f - b1) * gc;
+        v[i] = b2 * v[i] + (1.f - b2) * gc * gc;
+        p[i] = p[i] - lr_t * m[i] / (sqrtf(v[i]) + eps);
+    }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+#define DISPATCH_T(dtype, KERNEL_CALL)                  \
+    do {                                                \
+        if ((dtype) == SEG_BF16) {                      \
+            typedef bf16 T;                             \
+            KERNEL_CALL;                                \
+        } else if ((dtype) == SEG_F32) {                \
+            typedef float T;                            \
+            KERNEL_CALL;                                \
+        } else                                          \
+            return SEG_EINVAL;                          \
+    } while (0)
+
+static inline int epc_of(int dtype) { return dtype == SEG_BF16 ? 8 : 4; }
+
+extern "C" size_t seg_bias_grad_workspace(long P, int K) {
+    (void)P;
+    return (size_t)RED_BLOCKS * 2 * K * sizeof(float);
+}
+
+static int red_blocks(long P) {
+    long b = (P + 63) / 64;
+    if (b > RED_BLOCKS) b = RED_BLOCKS;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int ld_y, void* dz, int ld_dz, float* dbias,
+                                 long P, int K, int k_valid, int relu, int dtype, void* ws, size_t ws_bytes,
+                                 void* stream) {
+    if (!dy || !dz || (relu && !y) || (K & 7) || P <= 0) return SEG_EINVAL;
+    if (K > 4096) return SEG_EINVAL;
+    const int nb = red_blocks(P);
+    hipStream_t s = (hipStream_t)stream;
+    const RedGeom g = red_geom(K, epc_of(dtype));
+    const size_t shm = (size_t)g.rows * K * sizeof(float);
+    float* part = (float*)ws;
+    if (!ws || ws_bytes < (size_t)nb * K * sizeof(float)) return SEG_EWORKSPACE;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(bias_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)dy, ld_dy,
+                                         (const T*)y, ld_y, (T*)dz, ld_dz, part, P, K, relu));
+    SEG_CHECK_LAUNCH();
+    if (dbias) {
+        hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 255) / 256), dim3(256), 0, s, part, nb, K, k_valid, dbias, 0);
+        SEG_CHECK_LAUNCH();
+    }
+    return SEG_OK;
+}
+
+extern "C" int seg_maxpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy, int dtype,
+                                  void* stream) {
+    if (!x || !y || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2) return SEG_EINVAL;
+    const long total = (long)N * (H / 2) * (W / 2) * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, ldx, ldy));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H, int W, int C,
+                                  int ldx, int ldy, int dtype, void* stream) {
+    (void)y;
+    if (!x || !dy || !dx || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2) return SEG_EINVAL;
+    const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (const T*)dy, (T*)dx, N, H, W, C, ldx, ldy));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_avgpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy, int dtype,
+                                  void* stream) {
+    if (!x || !y || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2) return SEG_EINVAL;
+    const long total = (long)N * (H / 2) * (W / 2) * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(avgpool_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, ldx, ldy));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_avgpool2x2_bwd(const void* dy, void* dx, int N, int H, int W, int C, int ldx, int ldy, int dtype,
+                                  void* stream) {
+    if (!dy || !dx || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2) return SEG_EINVAL;
+    const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(avgpool_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)dy, (T*)dx, N, H, W, C, ldx, ldy));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_add(const void* a, const void* b, void* y, long n, int dtype, void* stream) {
+    if (!a || !b || !y || n < 0) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(add_k<T>, dim3(seg_grid_1d(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)a, (const T*)b, (T*)y, n));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_dropout_fwd(const void* x, void* y, long n, float kp, uint64_t seed, int dtype, void* stream) {
+    if (!x || !y || !(kp > 0.f) || kp > 1.f) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_k<T>, dim3(seg_grid_1d(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, (T*)y, n, kp, seed));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_dropout_bwd(const void* dy, void* dx, long n, float kp, uint64_t seed, int dtype, void* stream) {
+    // the same mask and 1/kp scale: dx = dy / kp * floor(kp + U)
+    return seg_dropout_fwd(dy, dx, n, kp, seed, dtype, stream);
+}
+
+extern "C" int seg_fill(void* y, long n, float v, int dtype, void* stream) {
+    if (!y) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(fill_k<T>, dim3(seg_grid_1d(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                                         (T*)y, n, v));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_cast(const void* x, int xd, void* y, int yd, long n, void* stream) {
+    if (!x || !y) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int g = seg_grid_1d(n, 256);
+    if (xd == SEG_F32 && yd == SEG_BF16) hipLaunchKernelGGL((cast_k<float, bf16>), dim3(g), dim3(256), 0, s, (const float*)x, (bf16*)y, n);
+    else if (xd == SEG_BF16 && yd == SEG_F32) hipLaunchKernelGGL((cast_k<bf16, float>), dim3(g), dim3(256), 0, s, (const bf16*)x, (float*)y, n);
+    else if (xd == SEG_F32 && yd == SEG_F32) hipLaunchKernelGGL((cast_k<float, float>), dim3(g), dim3(256), 0, s, (const float*)x, (float*)y, n);
+    else if (xd == SEG_BF16 && yd == SEG_BF16) hipLaunchKernelGGL((cast_k<bf16, bf16>), dim3(g), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n);
+    else return SEG_EINVAL;
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_copy_channels(const void* x, int ldx, void* y, int ldy, long P, int C, int dtype, void* stream) {
+    if (!x || !y || (C & 7) || (ldx & 7) || (ldy & 7)) return SEG_EINVAL;
+    const long total = P * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(copy_channels_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, ldx, (T*)y, ldy, P, C));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_prepare_input(const float* img, void* x, int N, int H, int W, int cin, int HP, int WP, int CP,
+                                 int dtype, void* stream) {
+    if (!img || !x || HP < H || WP < W || CP < cin) return SEG_EINVAL;
+    const long total = (long)N * HP * WP * CP;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(prepare_input_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const float* gamma, const float* beta,
+                               float eps, long P, int C, int cv, int relu, int dtype, void* stream) {
+    if (!x || !y || !gamma || !beta || (C & 7)) return SEG_EINVAL;
+    const float inv = 1.0f / sqrtf(1.0f + eps);
+    const long total = P * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, ldx, (T*)y, ldy, gamma, beta, inv, P, C, cv,
+                                         relu));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
+                               int lddx, const float* gamma, float eps, float* dgamma, float* dbeta, long P, int C,
+                               int cv, int relu, int dtype, void* ws, size_t ws_bytes, void* stream) {
+    if (!x || !y || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7)) return SEG_EINVAL;
+    if (C > 4096) return SEG_EINVAL;
+    const int nb = red_blocks(P);
+    if (!ws || ws_bytes < (size_t)nb * 2 * C * sizeof(float)) return SEG_EWORKSPACE;
+    const float inv = 1.0f / sqrtf(1.0f + eps);
+    const RedGeom g = red_geom(C, epc_of(dtype));
+    const size_t shm = (size_t)g.rows * 2 * C * sizeof(float);
+    if (shm > 64 * 1024) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)x, ldx, (const T*)y,
+                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, inv, (float*)ws, P, C, cv, relu));
+    SEG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_finish_k, dim3((cv + 255) / 256), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
+                                       void* stream) {
+    if (!x || !y) return SEG_EINVAL;
+    const long total = (long)N * OH * OW * C;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, OH, OW));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, int W, int C, int OH, int OW,
+                                       int dtype, void* stream) {
+    if (!dy || !dx) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(dx, 0, (size_t)N * H * W * C * sizeof(float), s) != hipSuccess) return SEG_ELAUNCH;
+    const long total = (long)N * OH * OW * C;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s,
+                                         (const T*)dy, dx, N, H, W, C, OH, OW));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" size_t seg_xent_workspace(int N, int H, int W) {
+    (void)N; (void)H; (void)W;
+    return 2048 * sizeof(float);
+}
+
+static int xent_launch(const void* logits, int ld, const uint8_t* li, const float* ls, int N, int H, int W, int C,
+                       int vh, int vw, float scale, float* loss, void* dl, int ldd, void* ws, size_t wsb,
+                       void* stream, int dtype) {
+    if (!logits || !loss || !dl || C < 1 || C > XENT_MAXC || ld < C || ldd < C) return SEG_EINVAL;
+    if (!ws || wsb < 2048 * sizeof(float)) return SEG_EWORKSPACE;
+    const long P = (long)N * H * W;
+    int nb = seg_grid_1d(P, 256, 2048);
+    hipStream_t s = (hipStream_t)stream;
+    if (ls) {
+        DISPATCH_T(dtype, hipLaunchKernelGGL((xent_k<T, true>), dim3(nb), dim3(256), 0, s, (const T*)logits, ld, li,
+                                             ls, N, H, W, C, vh, vw, scale, (T*)dl, ldd, (float*)ws));
+    } else {
+        DISPATCH_T(dtype, hipLaunchKernelGGL((xent_k<T, false>), dim3(nb), dim3(256), 0, s, (const T*)logits, ld, li,
+                                             ls, N, H, W, C, vh, vw, scale, (T*)dl, ldd, (float*)ws));
+    }
+    SEG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sum_k, dim3(1), dim3(256), 0, s, (const float*)ws, nb, loss);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_softmax_xent_fwd_bwd(const void* logits, int ld, const uint8_t* labels, int N, int H, int W, int C,
+                                        int vh, int vw, float scale, float* loss, void* dl, int ldd, int dtype,
+                                        void* ws, size_t wsb, void* stream) {
+    if (!labels) return SEG_EINVAL;
+    return xent_launch(logits, ld, labels, nullptr, N, H, W, C, vh, vw, scale, loss, dl, ldd, ws, wsb, stream,
+                       dtype);
+}
+
+extern "C" int seg_softmax_xent_soft_fwd_bwd(const void* logits, int ld, const float* labels, int N, int H, int W,
+                                             int C, int vh, int vw, float scale, float* loss, void* dl, int ldd,
+                                             int dtype, void* ws, size_t wsb, void* stream) {
+    if (!labels) return SEG_EINVAL;
+    return xent_launch(logits, ld, nullptr, labels, N, H, W, C, vh, vw, scale, loss, dl, ldd, ws, wsb, stream,
+                       dtype);
+}
+
+extern "C" int seg_argmax(const void* logits, int ld, int C, long P, int64_t* pred, int dtype, void* stream) {
+    if (!logits || !pred || C < 1) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(argmax_k<T>, dim3(seg_grid_1d(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)logits, ld, C, P, pred));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_confusion(const int64_t* pred, const uint8_t* labels, int N, int H, int W, int vh, int vw, int C,
+                             unsigned long long* conf, void* stream) {
+    if (!pred || !labels || !conf) return SEG_EINVAL;
+    const long P = (long)N * H * W;
+    hipLaunchKernelGGL(confusion_k, dim3(seg_grid_1d(P, 256)), dim3(256), 0, (hipStream_t)stream, pred, labels, N, H,
+                       W, vh, vw, C, conf);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_adam_tf1_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                                 float eps, int t, float gs, void* stream) {
+    if (!p || !g || !m || !v || t < 1) return SEG_EINVAL;
+    if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return SEG_EALIGN;
+    const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+    hipLaunchKernelGGL(adam_k, dim3(seg_grid_1d(n / 4 + 1, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                       (float)lr_t, b1, b2, eps, gs);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" const char* seg_status_string(int s) {
+    switch (s) {
+        case SEG_OK: return "ok";
+        case SEG_EINVAL: return "invalid argument";
+        case SEG_ESHAPE: return "shape rule violated (TF InvalidArgumentError)";
+        case SEG_EALIGN: return "channel count / stride / pointer not 16-byte aligned";
+        case SEG_EWORKSPACE: return "workspace too small";
+        case SEG_ELAUNCH: return "HIP kernel launch failed";
+    }
+    return "unknown status";
+}
+
+extern "C" int seg_version(void) { return 1; }

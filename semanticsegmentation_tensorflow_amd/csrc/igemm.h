@@ -1,0 +1,69 @@
+// Internal parameter blocks of the implicit-GEMM kernels (not part of the C-ABI).
+#pragma once
+#include "common.h"
+
+namespace seg {
+
+struct EpiParams {
+    const float* bias;
+    const float* scale;
+    const float* shift;
+    const void* residual;
+    long res_img;     // elements per image of the residual
+    int ld_res;
+    int relu;
+    float keep_prob;
+    uint64_t seed;
+    int n_valid;      // columns >= n_valid are written as 0 (padding channels)
+};
+
+// C[m][n] = sum_k A[m][k] B[n][k].  Row m -> (img, a, b) on an Ha x Wa grid;
+// reduction k -> (tap=(j,i), channel c), taps_w taps along w.
+// A element: x[img, a*ish + j*tsh + ioh, b*isw + i*tsw + iow, c]  (0 outside)
+// B element: w[n*w_col + ((rb + rstep*j)*Sfull + (sb + sstep*i))*w_tap + c]
+// Output   : y[img, a*osh + ooh, b*osw + oow, n]
+struct NTParams {
+    int M, N, K;
+    const void* x;
+    long x_img;
+    int IH, IW, C, ldx;
+    int Ha, Wa, ish, isw, ioh, iow, tsh, tsw, taps_w;
+    const void* w;
+    long w_col, w_tap;
+    int rb, rstep, sb, sstep, Sfull;
+    void* y;
+    long y_img;
+    int OH, OW, ldy, osh, osw, ooh, oow;
+    EpiParams epi;
+    float* partial;
+    int kt_per_split;
+    // conv2d_transpose phase split: blockIdx.z = ph*st_w + pw
+    int phase, st_h, st_w, pad_t, pad_l, Nimg;
+};
+
+// C[m][n] = sum_p A[p][m] B[p][n].  p -> (img, a, b) on an Ha x Wa grid;
+// m -> (tap=(j,i), c) with Cg channels per tap.
+// A element: x[img, a*ish + j*tsh + ioh, b*isw + i*tsw + iow, c]
+// B element: b[p*ldb + n]
+// Output   : out[tap*o_tap + c*o_c + n*o_n] for c < c_valid, n < n_valid.
+struct TNParams {
+    int M, N, P;
+    const void* x;
+    long x_img;
+    int IH, IW, Cg, ldx;
+    int Ha, Wa, ish, isw, ioh, iow, tsh, tsw, taps_w;
+    const void* b;
+    int ldb;
+    float* out;
+    long o_tap, o_c, o_n;
+    int c_valid, n_valid;
+    float* partial;
+    int kt_per_split;
+};
+
+int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
+int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
+size_t nt_workspace(int M, int N, int K, int dtype, int phase);
+size_t tn_workspace(int M, int N, int P, int dtype);
+
+}  // namespace seg

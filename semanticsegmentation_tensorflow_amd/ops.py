@@ -1,0 +1,352 @@
+"""Typed wrappers over the C-ABI (`include/segkern.h`) on torch device tensors.
+
+Every function here launches hand-written gfx950 kernels from libsegkern.so on
+the caller's current HIP stream; torch provides only memory and the stream.
+Activation tensors are NHWC with the channel dim padded to a multiple of 8
+(`round8`); a channel-slice view is allowed (its pixel stride is read from the
+tensor's stride).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import SegConvDesc, SegEpilogue, check
+
+F32, BF16 = 0, 1
+_TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16}
+SAME, VALID = 0, 1
+
+
+def round8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def seg_dtype(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise TypeError(f"unsupported activation dtype {t.dtype}")
+
+
+def torch_dtype(d: int):
+    return _TORCH_DT[d]
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def pixel_stride(t: torch.Tensor) -> int:
+    """Elements between consecutive pixels of an NHWC(-view) tensor."""
+    if t.stride(-1) != 1:
+        raise ValueError("channel dim must be unit-stride")
+    return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+
+
+class Workspace:
+    """Grow-only device scratch buffer (allocated outside hot loops)."""
+
+    def __init__(self, device=None):
+        self.device = device
+        self.buf = None
+
+    def get(self, nbytes: int):
+        nbytes = max(int(nbytes), 256)
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self.buf
+
+    def ptr_size(self, nbytes):
+        b = self.get(nbytes)
+        return ctypes.c_void_p(b.data_ptr()), ctypes.c_size_t(b.numel())
+
+
+# ---------------------------------------------------------------------------
+# descriptors
+# ---------------------------------------------------------------------------
+def conv_desc(N, H, W, C, K, R, S, stride=1, dilation=1, padding="SAME", dtype=BF16):
+    d = SegConvDesc()
+    check(_lib.lib().seg_conv_desc_init(ctypes.byref(d), N, H, W, C, K, R, S, stride, dilation,
+                                        SAME if padding == "SAME" else VALID, dtype), "conv2d")
+    return d
+
+
+def tconv_desc(N, H, W, C, OH, OW, K, R, S, stride, padding="SAME", dtype=BF16):
+    d = SegConvDesc()
+    check(_lib.lib().seg_tconv_desc_init(ctypes.byref(d), N, H, W, C, OH, OW, K, R, S, stride,
+                                         SAME if padding == "SAME" else VALID, dtype),
+          "conv2d_transpose")
+    return d
+
+
+def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_prob=1.0, seed=0):
+    e = SegEpilogue()
+    e.bias = None if bias is None else bias.data_ptr()
+    e.scale = None if scale is None else scale.data_ptr()
+    e.shift = None if shift is None else shift.data_ptr()
+    e.residual = None if residual is None else residual.data_ptr()
+    e.ld_residual = 0 if residual is None else pixel_stride(residual)
+    e.relu = 1 if relu else 0
+    e.keep_prob = float(keep_prob)
+    e.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return e
+
+
+OP_FWD, OP_BWD_DATA, OP_BWD_FILTER, OP_TFWD, OP_TBWD_DATA, OP_TBWD_FILTER = range(6)
+
+
+def conv_workspace(desc, op):
+    return int(_lib.lib().seg_conv_workspace(ctypes.byref(desc), op))
+
+
+# ---------------------------------------------------------------------------
+# convolutions
+# ---------------------------------------------------------------------------
+def _with_ld(desc, x=None, y=None):
+    d = SegConvDesc.from_buffer_copy(desc)
+    if x is not None:
+        d.ldx = pixel_stride(x)
+    if y is not None:
+        d.ldy = pixel_stride(y)
+    return d
+
+
+def conv2d_fwd(desc, x, w_krsc, y, epi=None, ws=None, stream=None):
+    d = _with_ld(desc, x, y)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_FWD))
+    check(_lib.lib().seg_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(w_krsc),
+                                    None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
+                                    stream_ptr(stream)), "conv2d")
+    return y
+
+
+def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None):
+    d = _with_ld(desc, dx, dy)
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_BWD_DATA))
+    check(_lib.lib().seg_conv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_hwio), ptr(dx), wsp, wss,
+                                         stream_ptr(stream)), "conv2d_backprop_input")
+    return dx
+
+
+def conv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None):
+    d = _with_ld(desc, x, dy)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_BWD_FILTER))
+    check(_lib.lib().seg_conv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw), wsp, wss,
+                                           stream_ptr(stream)), "conv2d_backprop_filter")
+    return dw
+
+
+def tconv2d_fwd(desc, x, w_rskc, y, epi=None, ws=None, stream=None):
+    d = _with_ld(desc, x, y)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_TFWD))
+    check(_lib.lib().seg_tconv2d_fwd(ctypes.byref(d), ptr(x), ptr(w_rskc),
+                                     None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
+                                     stream_ptr(stream)), "conv2d_transpose")
+    return y
+
+
+def tconv2d_bwd_data(desc, dy, w_crsk, dx, ws=None, stream=None):
+    d = _with_ld(desc, dx, dy)
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_TBWD_DATA))
+    check(_lib.lib().seg_tconv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_crsk), ptr(dx), wsp, wss,
+                                          stream_ptr(stream)), "conv2d_transpose_grad_input")
+    return dx
+
+
+def tconv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None):
+    d = _with_ld(desc, x, dy)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_TBWD_FILTER))
+    check(_lib.lib().seg_tconv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw), wsp, wss,
+                                            stream_ptr(stream)), "conv2d_transpose_grad_filter")
+    return dw
+
+
+PACK_KRSC, PACK_HWIO, PACK_TCONV_FWD, PACK_TCONV_BWD = 0, 1, 2, 3
+
+
+def pack_filter(src, dst, a_pad, b_pad, mode, stream=None):
+    """src fp32 [R,S,A,B] master -> dst packed compute copy (see segkern.h)."""
+    R, S, A, B = src.shape
+    check(_lib.lib().seg_pack_filter(ptr(src), ptr(dst), R, S, A, B, a_pad, b_pad, mode,
+                                     seg_dtype(dst), stream_ptr(stream)), "pack_filter")
+    return dst
+
+
+def packed_shape(R, S, A, B, mode):
+    a, b = round8(A), round8(B)
+    if mode in (PACK_KRSC, PACK_TCONV_BWD):
+        return (b, R, S, a)
+    return (R, S, a, b)
+
+
+# ---------------------------------------------------------------------------
+# HBM-bound ops
+# ---------------------------------------------------------------------------
+def bias_relu_bwd(dy, y, dz, dbias, k_valid, relu=True, ws=None, stream=None):
+    N, H, W, K = dy.shape
+    P = N * H * W
+    need = int(_lib.lib().seg_bias_grad_workspace(P, K))
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(need)
+    check(_lib.lib().seg_bias_relu_bwd(ptr(dy), pixel_stride(dy), ptr(y),
+                                       pixel_stride(y) if y is not None else 0, ptr(dz),
+                                       pixel_stride(dz), ptr(dbias), P, K, k_valid,
+                                       1 if relu else 0, seg_dtype(dy), wsp, wss,
+                                       stream_ptr(stream)), "bias_relu_bwd")
+    return dz
+
+
+def maxpool2x2_fwd(x, y, stream=None):
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_maxpool2x2_fwd(ptr(x), ptr(y), N, H, W, C, pixel_stride(x),
+                                        pixel_stride(y), seg_dtype(x), stream_ptr(stream)),
+          "max_pool")
+    return y
+
+
+def maxpool2x2_bwd(x, y, dy, dx, stream=None):
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_maxpool2x2_bwd(ptr(x), ptr(y), ptr(dy), ptr(dx), N, H, W, C,
+                                        pixel_stride(dx), pixel_stride(dy), seg_dtype(x),
+                                        stream_ptr(stream)), "max_pool_grad")
+    return dx
+
+
+def avgpool2x2_fwd(x, y, stream=None):
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_avgpool2x2_fwd(ptr(x), ptr(y), N, H, W, C, pixel_stride(x),
+                                        pixel_stride(y), seg_dtype(x), stream_ptr(stream)),
+          "avg_pool")
+    return y
+
+
+def avgpool2x2_bwd(dy, dx, stream=None):
+    N, H, W, C = dx.shape
+    check(_lib.lib().seg_avgpool2x2_bwd(ptr(dy), ptr(dx), N, H, W, C, pixel_stride(dx),
+                                        pixel_stride(dy), seg_dtype(dx), stream_ptr(stream)),
+          "avg_pool_grad")
+    return dx
+
+
+def add(a, b, y, stream=None):
+    check(_lib.lib().seg_add(ptr(a), ptr(b), ptr(y), y.numel(), seg_dtype(y), stream_ptr(stream)),
+          "add")
+    return y
+
+
+def dropout_fwd(x, y, keep_prob, seed, stream=None):
+    check(_lib.lib().seg_dropout_fwd(ptr(x), ptr(y), x.numel(), float(keep_prob), int(seed),
+                                     seg_dtype(x), stream_ptr(stream)), "dropout")
+    return y
+
+
+def bn_relu_fwd(x, y, gamma, beta, c_valid, relu=True, eps=1e-3, stream=None):
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_bn_relu_fwd(ptr(x), pixel_stride(x), ptr(y), pixel_stride(y), ptr(gamma),
+                                     ptr(beta), float(eps), N * H * W, C, c_valid,
+                                     1 if relu else 0, seg_dtype(x), stream_ptr(stream)),
+          "batch_norm")
+    return y
+
+
+def bn_relu_bwd(x, y, dy, dx, gamma, dgamma, dbeta, c_valid, relu=True, eps=1e-3, ws=None,
+                stream=None):
+    N, H, W, C = x.shape
+    P = N * H * W
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(1024 * 2 * C * 4)
+    check(_lib.lib().seg_bn_relu_bwd(ptr(x), pixel_stride(x), ptr(y), pixel_stride(y), ptr(dy),
+                                     pixel_stride(dy), ptr(dx), pixel_stride(dx), ptr(gamma),
+                                     float(eps), ptr(dgamma), ptr(dbeta), P, C, c_valid,
+                                     1 if relu else 0, seg_dtype(x), wsp, wss, stream_ptr(stream)),
+          "batch_norm_grad")
+    return dx
+
+
+def resize_bilinear_fwd(x, y, stream=None):
+    N, H, W, C = x.shape
+    _, OH, OW, _ = y.shape
+    check(_lib.lib().seg_resize_bilinear_fwd(ptr(x), ptr(y), N, H, W, C, OH, OW, seg_dtype(x),
+                                             stream_ptr(stream)), "resize_bilinear")
+    return y
+
+
+def resize_bilinear_bwd(dy, dx_f32, stream=None):
+    N, OH, OW, C = dy.shape
+    _, H, W, _ = dx_f32.shape
+    check(_lib.lib().seg_resize_bilinear_bwd(ptr(dy), ptr(dx_f32), N, H, W, C, OH, OW,
+                                             seg_dtype(dy), stream_ptr(stream)),
+          "resize_bilinear_grad")
+    return dx_f32
+
+
+def copy_channels(x, y, stream=None):
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_copy_channels(ptr(x), pixel_stride(x), ptr(y), pixel_stride(y), N * H * W,
+                                       round8(C), seg_dtype(x), stream_ptr(stream)), "concat")
+    return y
+
+
+def prepare_input(img_f32, x, stream=None):
+    """fp32 [N,H,W,c] -> padded compute tensor x [N,HP,WP,CP] (zeros outside)."""
+    N, H, W, c = img_f32.shape
+    _, HP, WP, CP = x.shape
+    check(_lib.lib().seg_prepare_input(ptr(img_f32), ptr(x), N, H, W, c, HP, WP, CP, seg_dtype(x),
+                                       stream_ptr(stream)), "prepare_input")
+    return x
+
+
+def softmax_xent(logits, labels, dlogits, loss_sum, num_classes, valid_hw=None, grad_scale=1.0,
+                 ws=None, stream=None):
+    N, H, W, _ = logits.shape
+    vh, vw = valid_hw if valid_hw is not None else (H, W)
+    wsp, wss = (ws or Workspace(logits.device)).ptr_size(
+        int(_lib.lib().seg_xent_workspace(N, H, W)))
+    L = _lib.lib()
+    if labels.dtype == torch.uint8:
+        st = L.seg_softmax_xent_fwd_bwd(ptr(logits), pixel_stride(logits), ptr(labels), N, H, W,
+                                        num_classes, vh, vw, float(grad_scale), ptr(loss_sum),
+                                        ptr(dlogits), pixel_stride(dlogits), seg_dtype(logits),
+                                        wsp, wss, stream_ptr(stream))
+    else:
+        st = L.seg_softmax_xent_soft_fwd_bwd(ptr(logits), pixel_stride(logits), ptr(labels), N, H,
+                                             W, num_classes, vh, vw, float(grad_scale),
+                                             ptr(loss_sum), ptr(dlogits), pixel_stride(dlogits),
+                                             seg_dtype(logits), wsp, wss, stream_ptr(stream))
+    check(st, "softmax_cross_entropy_with_logits")
+    return loss_sum
+
+
+def argmax(logits, pred, num_classes, stream=None):
+    N, H, W, _ = logits.shape
+    check(_lib.lib().seg_argmax(ptr(logits), pixel_stride(logits), num_classes, N * H * W,
+                                ptr(pred), seg_dtype(logits), stream_ptr(stream)), "argmax")
+    return pred
+
+
+def confusion(pred, labels, conf, num_classes, valid_hw=None, stream=None):
+    N, H, W = labels.shape[:3]
+    vh, vw = valid_hw if valid_hw is not None else (H, W)
+    check(_lib.lib().seg_confusion(ptr(pred), ptr(labels), N, H, W, vh, vw, num_classes, ptr(conf),
+                                   stream_ptr(stream)), "confusion")
+    return conf
+
+
+def adam_tf1_step(p, g, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0,
+                  stream=None):
+    check(_lib.lib().seg_adam_tf1_step(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr),
+                                       float(beta1), float(beta2), float(eps), int(t),
+                                       float(grad_scale), stream_ptr(stream)), "adam")
+
+
+def fill(y, value, stream=None):
+    check(_lib.lib().seg_fill(ptr(y), y.numel(), float(value), seg_dtype(y), stream_ptr(stream)),
+          "fill")
+    return y

@@ -1,0 +1,357 @@
+"""Op-level parity: every HIP kernel vs the CPU oracle (oracle/tf1_ops.py).
+
+fp32 path: exact-f32 MFMA, compared at ~1e-5 relative (of max |ref|).
+bf16 path: the oracle sees the same bf16-rounded inputs; tolerance covers
+fp32-accumulation order + one bf16 output rounding (~2^-8 relative).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import tf1_ops as tf
+from semanticsegmentation_tensorflow_amd import ops
+from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
+
+pytestmark = pytest.mark.gpu
+DTYPES = [torch.float32, torch.bfloat16]
+DT = {torch.float32: ops.F32, torch.bfloat16: ops.BF16}
+
+# (N, H, W, C, K, R, S(=R), stride, dilation, padding)
+CONV_CASES = [
+    (2, 9, 11, 8, 16, 3, 3, 1, 1, "SAME"),
+    (1, 12, 10, 3, 64, 3, 3, 1, 1, "SAME"),     # conv1_1-like: C=3 padded to 8
+    (2, 7, 9, 64, 136, 3, 3, 1, 1, "SAME"),     # N tail (136 = 128 + 8)
+    (1, 6, 5, 24, 40, 1, 1, 1, 1, "SAME"),      # 1x1
+    (1, 5, 7, 16, 32, 7, 7, 1, 1, "SAME"),      # conv6-like 7x7 SAME on tiny map
+    (2, 8, 8, 16, 24, 4, 4, 1, 1, "SAME"),      # even kernel: asymmetric SAME pad
+    (1, 11, 13, 16, 16, 3, 3, 2, 1, "SAME"),    # strided
+    (1, 12, 12, 8, 16, 3, 3, 1, 2, "SAME"),     # atrous (dilation 2)
+    (1, 10, 10, 16, 8, 3, 3, 1, 1, "VALID"),
+    (3, 20, 20, 128, 256, 3, 3, 1, 1, "SAME"),  # multi-tile M and N, uniform-tap path
+]
+
+
+def _conv_case(case, seed):
+    N, H, W, C, K, R, S, st, dil, pad = case
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    w = torch.randn(R, S, C, K, generator=g, dtype=torch.float64) / math.sqrt(R * S * C)
+    b = torch.randn(K, generator=g, dtype=torch.float64) * 0.1
+    return x, w, b
+
+
+def _pack(w64, mode, dtype, dev):
+    R, S, A, B = w64.shape
+    src = w64.float().to(dev).contiguous()
+    dst = torch.empty(ops.packed_shape(R, S, A, B, mode), dtype=dtype, device=dev)
+    return ops.pack_filter(src, dst, ops.round8(A), ops.round8(B), mode)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_fwd_bias_relu(dev, case, dtype):
+    N, H, W, C, K, R, S, st, dil, pad = case
+    x, w, b = _conv_case(case, 1)
+    xr, wr = rnd(x, dtype), rnd(w, dtype)
+    ref = tf.relu(tf.bias_add(tf.conv2d(xr, wr, st, pad, dil), rnd(b.float().double(), torch.float32)))
+    d = ops.conv_desc(N, H, W, C, K, R, S, st, dil, pad, DT[dtype])
+    xd = to_dev(x, dtype, dev)
+    wk = _pack(w, ops.PACK_KRSC, dtype, dev)
+    bd = b.float().to(dev)
+    y = torch.empty(N, d.OH, d.OW, d.K, dtype=dtype, device=dev)
+    ops.conv2d_fwd(d, xd, wk, y, ops.epilogue(bias=bd, relu=True))
+    torch.cuda.synchronize()
+    assert_close(from_dev(y, K), ref, dtype, f"conv fwd {case}")
+    if d.K > K:   # padding channels stay exactly zero
+        assert y[..., K:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[7] == 1])
+def test_conv2d_bwd_data(dev, case, dtype):
+    N, H, W, C, K, R, S, st, dil, pad = case
+    x, w, _ = _conv_case(case, 2)
+    wr = rnd(w, dtype)
+    xr = x.clone().requires_grad_(True)
+    y = tf.conv2d(xr, wr, st, pad, dil)
+    g = torch.Generator().manual_seed(7)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    d = ops.conv_desc(N, H, W, C, K, R, S, st, dil, pad, DT[dtype])
+    dyd = to_dev(dy, dtype, dev)
+    wh = _pack(w, ops.PACK_HWIO, dtype, dev)
+    dx = torch.full((N, H, W, d.C), float("nan"), dtype=dtype, device=dev)
+    ops.conv2d_bwd_data(d, dyd, wh, dx)
+    torch.cuda.synchronize()
+    assert_close(from_dev(dx, C), xr.grad, dtype, f"conv bwd_data {case}")
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_bwd_filter(dev, case, dtype):
+    N, H, W, C, K, R, S, st, dil, pad = case
+    x, w, _ = _conv_case(case, 3)
+    xr = rnd(x, dtype)
+    wr = w.clone().requires_grad_(True)
+    y = tf.conv2d(xr, wr, st, pad, dil)
+    g = torch.Generator().manual_seed(8)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    d = ops.conv_desc(N, H, W, C, K, R, S, st, dil, pad, DT[dtype])
+    dw = torch.full((R, S, C, K), float("nan"), dtype=torch.float32, device=dev)
+    ops.conv2d_bwd_filter(d, to_dev(x, dtype, dev), to_dev(dy, dtype, dev), dw)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dtype == torch.float32 else 2e-3   # fp32 accumulation of bf16 products
+    assert_close(dw.double().cpu(), wr.grad, dtype, f"conv bwd_filter {case}", tol)
+
+
+# (N, IH, IW, C_in, OH, OW, C_out, k, stride)
+TCONV_CASES = [
+    (2, 3, 5, 16, 6, 10, 8, 4, 2),       # conv_t1/t2-like k4 s2
+    (1, 3, 4, 2, 6, 8, 512, 4, 2),       # conv_t1 exact channel shape (2 -> 512)
+    (1, 6, 6, 16, 11, 12, 16, 4, 2),     # odd output: asymmetric tconv pads
+    (1, 2, 3, 16, 16, 24, 2, 16, 8),     # conv_t3-like k16 s8 -> 2 classes
+    (2, 4, 4, 136, 8, 8, 72, 4, 2),      # tails in both channel dims
+]
+
+
+def _tconv_case(case, seed):
+    N, IH, IW, Ci, OH, OW, Co, k, s = case
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, IH, IW, Ci, generator=g, dtype=torch.float64)
+    w = torch.randn(k, k, Co, Ci, generator=g, dtype=torch.float64) / math.sqrt(Ci * 4)
+    b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
+    return x, w, b
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", TCONV_CASES)
+def test_tconv2d_fwd_bias_residual(dev, case, dtype):
+    N, IH, IW, Ci, OH, OW, Co, k, s = case
+    x, w, b = _tconv_case(case, 4)
+    g = torch.Generator().manual_seed(5)
+    res = rnd(torch.randn(N, OH, OW, Co, generator=g, dtype=torch.float64), dtype)
+    ref = tf.conv2d_transpose(rnd(x, dtype), rnd(w, dtype), (N, OH, OW, Co), s) + b.float().double() + res
+    d = ops.tconv_desc(N, IH, IW, Ci, OH, OW, Co, k, k, s, "SAME", DT[dtype])
+    wp = _pack(w, ops.PACK_TCONV_FWD, dtype, dev)
+    y = torch.full((N, OH, OW, d.K), float("nan"), dtype=dtype, device=dev)
+    resd = to_dev(res, dtype, dev)
+    ops.tconv2d_fwd(d, to_dev(x, dtype, dev), wp, y, ops.epilogue(bias=b.float().to(dev), residual=resd))
+    torch.cuda.synchronize()
+    assert_close(from_dev(y, Co), ref, dtype, f"tconv fwd {case}")
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", TCONV_CASES)
+def test_tconv2d_grads(dev, case, dtype):
+    N, IH, IW, Ci, OH, OW, Co, k, s = case
+    x, w, _ = _tconv_case(case, 6)
+    xr = rnd(x, dtype).requires_grad_(True)
+    wr = rnd(w, dtype).requires_grad_(True)
+    y = tf.conv2d_transpose(xr, wr, (N, OH, OW, Co), s)
+    g = torch.Generator().manual_seed(9)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    d = ops.tconv_desc(N, IH, IW, Ci, OH, OW, Co, k, k, s, "SAME", DT[dtype])
+    dyd = to_dev(dy, dtype, dev)
+    wb = _pack(w, ops.PACK_TCONV_BWD, dtype, dev)
+    dx = torch.full((N, IH, IW, d.C), float("nan"), dtype=dtype, device=dev)
+    ops.tconv2d_bwd_data(d, dyd, wb, dx)
+    dw = torch.full((k, k, Co, Ci), float("nan"), dtype=torch.float32, device=dev)
+    ops.tconv2d_bwd_filter(d, to_dev(x, dtype, dev), dyd, dw)
+    torch.cuda.synchronize()
+    assert_close(from_dev(dx, Ci), xr.grad, dtype, f"tconv bwd_data {case}")
+    tol = 2e-5 if dtype == torch.float32 else 2e-3
+    assert_close(dw.double().cpu(), wr.grad, dtype, f"tconv bwd_filter {case}", tol)
+
+
+def test_tconv_shape_rule_rejects_375(dev):
+    """375x1242 cannot pass FCN's conv_t2 (ceil(375/8)=47 -> pool3 46): TF raises."""
+    with pytest.raises(ValueError):
+        ops.tconv_desc(1, 11, 38, 512, 23, 77, 256, 4, 4, 2)   # pool5 11x38 -> pool4 23x77
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(2, 6, 8, 16), (1, 7, 9, 24), (1, 5, 5, 8)])
+def test_maxpool_fwd_bwd(dev, shape, dtype):
+    N, H, W, C = shape
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    x[0, 0, 0, :] = x[0, 0, 1, :]          # exact ties -> first in scan order
+    x = rnd(x, dtype).requires_grad_(True)
+    y = tf.max_pool2x2(x)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    xd = to_dev(x.detach(), dtype, dev)
+    yd = torch.empty(N, H // 2, W // 2, ops.round8(C), dtype=dtype, device=dev)
+    ops.maxpool2x2_fwd(xd, yd)
+    dxd = torch.full_like(xd, float("nan"))
+    ops.maxpool2x2_bwd(xd, yd, to_dev(dy, dtype, dev), dxd)
+    torch.cuda.synchronize()
+    assert torch.equal(from_dev(yd, C), y.detach())
+    assert torch.equal(from_dev(dxd, C), x.grad)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_avgpool_fwd_bwd(dev, dtype):
+    N, H, W, C = 2, 7, 6, 16
+    g = torch.Generator().manual_seed(11)
+    x = rnd(torch.randn(N, H, W, C, generator=g, dtype=torch.float64), dtype).requires_grad_(True)
+    y = tf.avg_pool2x2(x)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    xd = to_dev(x.detach(), dtype, dev)
+    yd = torch.empty(N, H // 2, W // 2, C, dtype=dtype, device=dev)
+    ops.avgpool2x2_fwd(xd, yd)
+    dxd = torch.full_like(xd, float("nan"))
+    ops.avgpool2x2_bwd(to_dev(dy, dtype, dev), dxd)
+    torch.cuda.synchronize()
+    assert_close(from_dev(yd), y.detach(), dtype, "avgpool fwd")
+    assert_close(from_dev(dxd), x.grad, dtype, "avgpool bwd")
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("K", [16, 64, 4096, 8])
+def test_bias_relu_bwd(dev, dtype, K):
+    N, H, W = 2, 9, 13
+    g = torch.Generator().manual_seed(12)
+    y = rnd(torch.relu(torch.randn(N, H, W, K, generator=g, dtype=torch.float64)), dtype)
+    dy = rnd(torch.randn(N, H, W, K, generator=g, dtype=torch.float64), dtype)
+    dz = dy * (y > 0)
+    kv = K if K != 8 else 2
+    db = dz[..., :kv].sum(dim=(0, 1, 2))
+    yd, dyd = to_dev(y, dtype, dev), to_dev(dy, dtype, dev)
+    dzd = torch.empty_like(dyd)
+    dbd = torch.zeros(kv, dtype=torch.float32, device=dev)
+    ops.bias_relu_bwd(dyd, yd, dzd, dbd, kv, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(from_dev(dzd), dz)
+    assert_close(dbd.double().cpu(), db, torch.float32, "dbias", 1e-5)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("labels_kind", ["index", "onehot"])
+def test_softmax_xent(dev, dtype, labels_kind):
+    N, H, W, C = 2, 12, 16, 2
+    g = torch.Generator().manual_seed(13)
+    z = rnd(torch.randn(N, H, W, C, generator=g, dtype=torch.float64) * 3, dtype).requires_grad_(True)
+    lab = torch.randint(0, C, (N, H, W), generator=g)
+    vh, vw = 10, 13
+    mask = torch.zeros(N, H, W, dtype=torch.float64)
+    mask[:, :vh, :vw] = 1
+    y1 = tf.one_hot(lab, C)
+    loss = tf.mean_softmax_xent(z, y1, mask)
+    loss.backward()
+    zd = to_dev(z.detach(), dtype, dev)
+    dz = torch.full_like(zd, float("nan"))
+    ls = torch.zeros(1, dtype=torch.float32, device=dev)
+    cnt = N * vh * vw
+    labd = lab.to(torch.uint8).to(dev) if labels_kind == "index" else y1.float().to(dev).contiguous()
+    ops.softmax_xent(zd, labd, dz, ls, C, (vh, vw), grad_scale=1.0 / cnt)
+    torch.cuda.synchronize()
+    assert abs(ls.item() / cnt - loss.item()) <= 1e-5 * max(1.0, abs(loss.item()))
+    assert_close(from_dev(dz, C), z.grad, dtype, "dlogits")
+    assert dz[..., C:].abs().max().item() == 0
+
+
+def test_argmax_and_confusion(dev):
+    g = torch.Generator().manual_seed(14)
+    z = torch.randn(2, 5, 7, 2, generator=g)
+    z[0, 0, 0] = torch.tensor([1.0, 1.0])   # tie -> class 0
+    zd = to_dev(z.double(), torch.float32, dev)
+    pred = torch.empty(2 * 5 * 7, dtype=torch.int64, device=dev)
+    ops.argmax(zd, pred, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(pred.cpu().view(2, 5, 7), tf.argmax(z.double()))
+    lab = torch.randint(0, 2, (2, 5, 7), generator=g, dtype=torch.uint8)
+    conf = torch.zeros(4, dtype=torch.int64, device=dev)
+    ops.confusion(pred, lab.to(dev), conf, 2, (4, 6))
+    torch.cuda.synchronize()
+    p = pred.cpu().view(2, 5, 7)[:, :4, :6].reshape(-1)
+    t = lab[:, :4, :6].reshape(-1).long()
+    ref = torch.bincount(t * 2 + p, minlength=4)
+    assert torch.equal(conf.cpu(), ref)
+
+
+def test_adam_tf1(dev):
+    n = 1003
+    g = torch.Generator().manual_seed(15)
+    p0 = torch.randn(n, generator=g, dtype=torch.float64)
+    opt = tf.AdamTF1(lr=1e-3)
+    params = {"p": p0.clone()}
+    pd = p0.float().to(dev)
+    m = torch.zeros_like(pd)
+    v = torch.zeros_like(pd)
+    for t in range(1, 4):
+        gr = torch.randn(n, generator=g, dtype=torch.float64) * 1e-3
+        params = opt.apply(params, {"p": gr.float().double() * 9.0})
+        ops.adam_tf1_step(pd, gr.float().to(dev), m, v, 1e-3, t, grad_scale=9.0)
+    torch.cuda.synchronize()
+    assert_close(pd.double().cpu(), params["p"], torch.float32, "adam", 1e-6)
+
+
+def _np_uniform(seed, idx):
+    M = (1 << 64) - 1
+    z = (seed * 0x9E3779B97F4A7C15 + idx + 0x632BE59BD9B4E019) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    z = z ^ (z >> 31)
+    return (z >> 40) / 16777216.0
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_dropout_tf1(dev, dtype):
+    n, kp, seed = 4096, 0.8, 1234
+    x = torch.ones(n, dtype=dtype, device=dev)
+    y = torch.empty_like(x)
+    ops.dropout_fwd(x, y, kp, seed)
+    torch.cuda.synchronize()
+    u = np.array([_np_uniform(seed, i) for i in range(n)])
+    ref = tf.dropout(torch.ones(n, dtype=torch.float64), kp, torch.from_numpy(u))
+    assert_close(y.double().cpu(), ref, dtype, "dropout")
+    keep = (y > 0).float().mean().item()
+    assert abs(keep - kp) < 0.03
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_bn_relu(dev, dtype):
+    N, H, W, C = 2, 5, 6, 24
+    g = torch.Generator().manual_seed(16)
+    x = rnd(torch.randn(N, H, W, C, generator=g, dtype=torch.float64), dtype).requires_grad_(True)
+    gamma = (1 + 0.1 * torch.randn(C, generator=g, dtype=torch.float64)).float().double().requires_grad_(True)
+    beta = (0.1 * torch.randn(C, generator=g, dtype=torch.float64)).float().double().requires_grad_(True)
+    y = torch.relu(tf.batch_norm_frozen(x, gamma, beta))
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    xd = to_dev(x.detach(), dtype, dev)
+    yd = torch.empty_like(xd)
+    gd, bd = gamma.detach().float().to(dev), beta.detach().float().to(dev)
+    ops.bn_relu_fwd(xd, yd, gd, bd, C)
+    dxd = torch.empty_like(xd)
+    dg = torch.zeros(C, device=dev)
+    dbt = torch.zeros(C, device=dev)
+    ops.bn_relu_bwd(xd, yd, to_dev(dy, dtype, dev), dxd, gd, dg, dbt, C)
+    torch.cuda.synchronize()
+    assert_close(from_dev(yd), y.detach(), dtype, "bn fwd")
+    assert_close(from_dev(dxd), x.grad, dtype, "bn dx")
+    assert_close(dg.double().cpu(), gamma.grad, torch.float32, "dgamma", 1e-4)
+    assert_close(dbt.double().cpu(), beta.grad, torch.float32, "dbeta", 1e-4)
+
+
+def test_resize_bilinear(dev):
+    N, H, W, C, OH, OW = 1, 5, 7, 3, 9, 15
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).float().double().requires_grad_(True)
+    y = tf.resize_bilinear(x, (OH, OW))
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64).float().double()
+    (y * dy).sum().backward()
+    xd = x.detach().float().to(dev).contiguous()
+    yd = torch.empty(N, OH, OW, C, device=dev)
+    ops.resize_bilinear_fwd(xd, yd)
+    dxd = torch.empty(N, H, W, C, device=dev)
+    ops.resize_bilinear_bwd(dy.float().to(dev).contiguous(), dxd)
+    torch.cuda.synchronize()
+    assert_close(yd.double().cpu(), y.detach(), torch.float32, "resize fwd", 1e-5)
+    assert_close(dxd.double().cpu(), x.grad, torch.float32, "resize bwd", 1e-5)
