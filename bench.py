@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""Headline benchmark: FCN training images/sec on synthetic KITTI-shaped
+375x1242 2-class batches (BASELINE.json config C2 at N=1, C4 for N>1).
+
+One "step" = one sess.run(train_step) of the reference's FCN.py training
+graph (forward, softmax-xent loss, backward, TF1 Adam on all 138.9 M
+parameters) over a batch of 4 images per GPU that are already resident in
+HBM.  375x1242 is zero-padded to 384x1248 (the reference cannot run
+375x1242 through FCN); the loss is masked to 375x1242; FLOPs
+are counted at the executed shape.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Rank 0 prints ONE JSON line.  Extra objects: "roofline" (dominant kernel,
+HIP-event timed inside this run) and "cpu_baseline" (the CPU oracle
+restatement timed on this host's cores, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "train images/sec on KITTI 375×1242 2-class at 1/2/4/8 MI355X; mIoU parity"
+PEAK = {"bf16": 2.5e15, "f32": 157.3e12}          # dense MFMA peaks (MI355X_MICROARCH.md)
+FCN_TRAIN_FLOP_PER_IMG = 1348.97e9                 # SURVEY.md 8d at 384x1248, C_in=3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="images per GPU")
+    ap.add_argument("--height", type=int, default=375)
+    ap.add_argument("--width", type=int, default=1242)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--keep-prob", type=float, default=0.8)
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--kernel-table", action="store_true", help="print per-launch timings to stderr")
+    return ap.parse_args()
+
+
+def pad32(x):
+    return (x + 31) // 32 * 32
+
+
+def synthetic(batch, H, W, HP, WP, seed, device):
+    """Images: integers uniform in [0,255] (uint8 PNG fed raw, FCN.py:395);
+    labels: a lower-image 'road' trapezoid + 5% pixel noise, uint8 class index
+    (process_gt_image, FCN.py:195-201)."""
+    import torch
+    g = torch.Generator(device=device).manual_seed(seed)
+    img = torch.zeros(batch, HP, WP, 3, dtype=torch.float32, device=device)
+    img[:, :H, :W] = torch.randint(0, 256, (batch, H, W, 3), generator=g, device=device).float()
+    yy = torch.arange(HP, device=device).view(HP, 1).float()
+    xx = torch.arange(WP, device=device).view(1, WP).float()
+    half = (yy - H * 0.45).clamp(min=0) / (H * 0.55) * (W * 0.45) + W * 0.05
+    road = ((yy > H * 0.45) & ((xx - W / 2).abs() < half)).to(torch.uint8)
+    lab = road.expand(batch, HP, WP).clone()
+    noise = torch.rand(batch, HP, WP, generator=g, device=device) < 0.05
+    lab = torch.where(noise, 1 - lab, lab)
+    lab[:, H:, :] = 0
+    lab[:, :, W:] = 0
+    return img, lab.contiguous()
+
+
+def cpu_baseline(H, W, HP, WP, steps):
+    """The oracle's FCN forward+backward (torch-CPU fp32) on this host."""
+    import numpy as np
+    import torch
+    from oracle import models as M
+    from oracle import tf1_ops as T
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    p = {k: torch.from_numpy((rng.standard_normal(s, dtype=np.float32) * 0.01).astype(np.float32)
+                             ).requires_grad_(True)
+         for k, s in M.fcn_param_shapes(3, 2).items()}
+    x = torch.zeros(1, HP, WP, 3)
+    x[:, :H, :W] = torch.from_numpy(rng.integers(0, 256, (1, H, W, 3)).astype(np.float32))
+    lab = torch.zeros(1, HP, WP, dtype=torch.long)
+    lab[:, H // 2:, W // 4:3 * W // 4] = 1
+    mask = torch.zeros(1, HP, WP)
+    mask[:, :H, :W] = 1
+    y1 = T.one_hot(lab, 2, torch.float32)
+
+    def step():
+        for v in p.values():
+            v.grad = None
+        _, logits = M.fcn_forward(p, x)
+        T.mean_softmax_xent(logits, y1, mask).backward()
+
+    step()                              # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(1.0 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle FCN fwd+bwd, torch-CPU fp32, 1 image {HP}x{WP} ({H}x{W} padded), "
+                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dp = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+        from semanticsegmentation_tensorflow_amd.dp import DataParallel
+        dp = DataParallel(bucket_mb=args.bucket_mb)
+
+    from semanticsegmentation_tensorflow_amd import graph as G
+    from semanticsegmentation_tensorflow_amd import ops, tf
+    from semanticsegmentation_tensorflow_amd.fcn import FCN
+
+    H, W = args.height, args.width
+    HP, WP = pad32(H), pad32(W)
+    B = args.batch
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
+    labels = tf.placeholder(tf.uint8, [None, HP, WP], name="annotation")
+    keep = tf.placeholder(tf.float32, name="keep_probability")
+    pred, logits = FCN(image, keep, 2).create()
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
+                                                                   valid_hw=(H, W)))
+    train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp)
+    sess.run(tf.global_variables_initializer())
+    img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
+    feed = {image: img, labels: lab, keep: args.keep_prob}
+
+    for _ in range(args.warmup):
+        sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    if dp:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    if dp:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dp:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_val = float(sess.run(loss, feed_dict=feed))
+
+    # ---- per-kernel timing (HIP events on the launch stream) for the roofline
+    sess.timer = []
+    sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    per = {}
+    step_conv_flops = 0.0
+    rows = []
+    for desc, op, s, e in sess.timer:
+        name, splits, flops = ops.conv_kernel_info(desc, op)
+        ms = s.elapsed_time(e)
+        step_conv_flops += flops
+        rows.append((name, op, splits, flops, ms, desc.N, desc.H, desc.W, desc.c_valid, desc.k_valid, desc.R))
+        a = per.setdefault(name, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += flops
+        a[2] += ms
+    sess.timer = None
+    dom = max(per.items(), key=lambda kv: kv[1][2])
+    dname, (dn, dflops, dms) = dom
+    achieved = (dflops / dn) / (dms / dn * 1e-3)
+    if args.kernel_table and rank == 0:
+        for r in rows:
+            print("KERNEL %-26s op=%d split=%-3d GF=%8.2f ms=%8.3f TF/s=%7.1f N=%d %dx%d C=%d K=%d R=%d"
+                  % (r[0], r[1], r[2], r[3] / 1e9, r[4], r[3] / r[4] / 1e9, *r[5:]), file=sys.stderr)
+        for k, (n, f, m) in sorted(per.items(), key=lambda kv: -kv[1][2]):
+            print(f"GROUP {k}: launches={n} ms={m:.3f} TF/s={f / m / 1e9:.1f}", file=sys.stderr)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+    peak = PEAK[args.dtype]
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic",
+        "config": {
+            "workload": "FCN (reference Network/model/FCN.py topology) train step: fwd + softmax-xent "
+                        "+ bwd + TF1 Adam, 375x1242x3 zero-padded to 384x1248",
+            "global_batch": B * world,
+            "batch_per_gpu": B,
+            "image": f"{H}x{W} -> {HP}x{WP}",
+            "parallelism": f"dp{world}",
+            "keep_prob": args.keep_prob,
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": dname,
+            "achieved": round(achieved / 1e12, 2),
+            "peak": round(peak / 1e12, 1),
+            "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": None,
+            "launches_per_step": dn,
+            "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
+            "avg_launch_ms": round(dms / dn, 4),
+        },
+        "step_mfma_frac": round(FCN_TRAIN_FLOP_PER_IMG * B / (ms_per_step * 1e-3) / peak, 4)
+        if (HP, WP) == (384, 1248) else None,
+        "conv_gflop_per_step_measured": round(step_conv_flops / 1e9, 2),
+        "loss_after": round(loss_val, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps)
+        except Exception as exc:  # report, never crash the headline line
+            result["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dp:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -113,6 +113,13 @@ int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy
  * 4 tconv bwd_data, 5 tconv bwd_filter. */
 size_t seg_conv_workspace(const seg_conv_desc* d, int op);
 
+/* Which kernel instantiation an op (numbering as seg_conv_workspace) will
+ * launch ("igemm_nt<bf16,128,128>"), its split-K factor (>1 adds a reduce
+ * kernel) and its algorithmic FLOPs (2 * MACs over unpadded channels).
+ * Host-only; used by bench.py to attribute HIP-event timings. */
+int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, int len, int* splits,
+                         double* flops);
+
 /* ---- filter packing: fp32 master -> compute copy ----------------------- */
 /* src: fp32 master [R][S][A][B] with A=a_valid, B=b_valid; dst (dtype,
  * channel dims padded to a_pad/b_pad with zeros):
@@ -124,11 +131,13 @@ int seg_pack_filter(const float* src, void* dst, int R, int S, int a_valid, int 
                     int a_pad, int b_pad, int mode, int dtype, void* stream);
 
 /* ---- ReluGrad + BiasAddGrad (implicit in minimize, FCN.py:340) --------- */
-/* dz = dy * (y > 0) if relu else dy; dbias[k] = sum over pixels of dz
- * (k < k_valid; dbias may be NULL).  dz may alias dy.
+/* dz = scale * dy * (y > 0) if relu else scale * dy; dbias[k] = sum over
+ * pixels of dz (k < k_valid; dbias may be NULL).  dz may alias dy.  scale is
+ * 1/keep_prob when TF1 dropout followed the ReLU (y is then the dropped
+ * output, so y > 0 also encodes the dropout mask).
  * ws >= seg_bias_grad_workspace() (always required). */
 int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int ld_y, void* dz, int ld_dz,
-                      float* dbias, long P, int K, int k_valid, int relu, int dtype,
+                      float* dbias, long P, int K, int k_valid, int relu, float scale, int dtype,
                       void* ws, size_t ws_bytes, void* stream);
 size_t seg_bias_grad_workspace(long P, int K);
 

@@ -99,8 +99,10 @@ SIGNATURES = {
     "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
     "seg_conv_workspace": (_Z, [_DP, _I]),
+    "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
+                                  ctypes.POINTER(ctypes.c_double)]),
     "seg_pack_filter": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "seg_bias_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _P, _Z, _P]),
+    "seg_bias_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _F, _I, _P, _Z, _P]),
     "seg_bias_grad_workspace": (_Z, [_L, _I]),
     "seg_maxpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_maxpool2x2_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

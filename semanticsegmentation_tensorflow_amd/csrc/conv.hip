@@ -3,6 +3,7 @@
 // each mapped onto the implicit-GEMM kernels of igemm.hip.
 #include "common.h"
 #include "igemm.h"
+#include <stdio.h>
 
 using seg::NTParams;
 using seg::TNParams;
@@ -183,6 +184,32 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
         case 5: { TNParams p = tconv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
     }
     return 0;
+}
+
+extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, int len, int* splits,
+                                    double* flops) {
+    int st = check_desc(d);
+    if (st) return st;
+    int bm = 0, bn = 0, sp = 1;
+    const char* fam = "igemm_nt";
+    const char* ty = d->dtype == SEG_BF16 ? "bf16" : "f32";
+    const double macs_conv = (double)d->N * d->OH * d->OW * d->R * d->S * d->c_valid * d->k_valid;
+    // conv2d_transpose MACs: every input pixel meets every tap
+    const double macs_t = (double)d->N * d->H * d->W * d->R * d->S * d->c_valid * d->k_valid;
+    double macs = 0;
+    switch (op) {
+        case 0: { NTParams p = conv_fwd_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
+        case 1: { NTParams p = conv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
+        case 2: { TNParams p = conv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_conv; break; }
+        case 3: { NTParams p = tconv_fwd_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 1, &bm, &bn, &sp); macs = macs_t; break; }
+        case 4: { NTParams p = tconv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_t; break; }
+        case 5: { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_t; break; }
+        default: return SEG_EINVAL;
+    }
+    if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
+    if (splits) *splits = sp;
+    if (flops) *flops = 2.0 * macs;
+    return SEG_OK;
 }
 
 extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,

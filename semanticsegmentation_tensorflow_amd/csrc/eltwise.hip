@@ -35,7 +35,7 @@ __host__ __device__ inline RedGeom red_geom(int K, int epc) {
 template <typename T>
 __global__ __launch_bounds__(256) void bias_relu_bwd_k(const T* __restrict__ dy, int ld_dy, const T* __restrict__ y,
                                                        int ld_y, T* __restrict__ dz, int ld_dz, float* __restrict__ part,
-                                                       long P, int K, int relu) {
+                                                       long P, int K, int relu, float scale) {
     constexpr int EPC = dt_traits<T>::EPC;
     extern __shared__ __attribute__((aligned(16))) float red[];
     const RedGeom g = red_geom(K, EPC);
@@ -63,7 +63,11 @@ __global__ __launch_bounds__(256) void bias_relu_bwd_k(const T* __restrict__ dy,
                     float yy[EPC];
                     Chunk<T>::unpack(ldc(y + pix * ld_y + cc * EPC), yy);
 #pragma unroll
-                    for (int e = 0; e < EPC; ++e) d[e] = yy[e] > 0.f ? d[e] : 0.f;
+                    for (int e = 0; e < EPC; ++e) d[e] = yy[e] > 0.f ? d[e] * scale : 0.f;
+                    stc(dz + pix * ld_dz + cc * EPC, Chunk<T>::pack(d));
+                } else if (scale != 1.f) {
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) d[e] *= scale;
                     stc(dz + pix * ld_dz + cc * EPC, Chunk<T>::pack(d));
                 } else if (dz != dy) {
                     stc(dz + pix * ld_dz + cc * EPC, Chunk<T>::pack(d));
@@ -599,8 +603,8 @@ static int red_blocks(long P) {
 }
 
 extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int ld_y, void* dz, int ld_dz, float* dbias,
-                                 long P, int K, int k_valid, int relu, int dtype, void* ws, size_t ws_bytes,
-                                 void* stream) {
+                                 long P, int K, int k_valid, int relu, float scale, int dtype, void* ws,
+                                 size_t ws_bytes, void* stream) {
     if (!dy || !dz || (relu && !y) || (K & 7) || P <= 0) return SEG_EINVAL;
     if (K > 4096) return SEG_EINVAL;
     const int nb = red_blocks(P);
@@ -610,7 +614,7 @@ extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int l
     float* part = (float*)ws;
     if (!ws || ws_bytes < (size_t)nb * K * sizeof(float)) return SEG_EWORKSPACE;
     DISPATCH_T(dtype, hipLaunchKernelGGL(bias_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)dy, ld_dy,
-                                         (const T*)y, ld_y, (T*)dz, ld_dz, part, P, K, relu));
+                                         (const T*)y, ld_y, (T*)dz, ld_dz, part, P, K, relu, scale));
     SEG_CHECK_LAUNCH();
     if (dbias) {
         hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 255) / 256), dim3(256), 0, s, part, nb, K, k_valid, dbias, 0);

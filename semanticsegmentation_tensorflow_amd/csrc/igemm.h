@@ -65,5 +65,7 @@ int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t w
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
 size_t tn_workspace(int M, int N, int P, int dtype);
+void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits);
+void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 
 }  // namespace seg

@@ -547,6 +547,13 @@ static void choose_nt(int M, int N, int K, int bk, int& bm, int& bn, int& splits
     }
 }
 
+void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits) {
+    choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, *bm, *bn, *splits);
+    if (phase) *splits = 1;
+}
+
+void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
+
 size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     if (phase) return 0;
     int bm, bn, splits;
@@ -607,6 +614,10 @@ static void choose_tn(int M, int N, int P, int bkp, int& bm, int& bn, int& split
         splits = std::min(splits, std::max(1, kt / 8));
         splits = std::min(splits, 256);
     }
+}
+
+void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits) {
+    choose_tn(M, N, P, dtype == SEG_BF16 ? 64 : 32, *bm, *bn, *splits);
 }
 
 size_t tn_workspace(int M, int N, int P, int dtype) {

@@ -104,6 +104,16 @@ def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER, OP_TFWD, OP_TBWD_DATA, OP_TBWD_FILTER = range(6)
 
 
+def conv_kernel_info(desc, op):
+    """(kernel name, split-K factor, algorithmic FLOPs) of a conv op launch."""
+    buf = ctypes.create_string_buffer(64)
+    sp = ctypes.c_int(0)
+    fl = ctypes.c_double(0)
+    check(_lib.lib().seg_conv_kernel_info(ctypes.byref(desc), op, buf, 64, ctypes.byref(sp),
+                                          ctypes.byref(fl)), "conv_kernel_info")
+    return buf.value.decode(), sp.value, fl.value
+
+
 def conv_workspace(desc, op):
     return int(_lib.lib().seg_conv_workspace(ctypes.byref(desc), op))
 
@@ -191,7 +201,7 @@ def packed_shape(R, S, A, B, mode):
 # ---------------------------------------------------------------------------
 # HBM-bound ops
 # ---------------------------------------------------------------------------
-def bias_relu_bwd(dy, y, dz, dbias, k_valid, relu=True, ws=None, stream=None):
+def bias_relu_bwd(dy, y, dz, dbias, k_valid, relu=True, ws=None, stream=None, scale=1.0):
     N, H, W, K = dy.shape
     P = N * H * W
     need = int(_lib.lib().seg_bias_grad_workspace(P, K))
@@ -199,7 +209,7 @@ def bias_relu_bwd(dy, y, dz, dbias, k_valid, relu=True, ws=None, stream=None):
     check(_lib.lib().seg_bias_relu_bwd(ptr(dy), pixel_stride(dy), ptr(y),
                                        pixel_stride(y) if y is not None else 0, ptr(dz),
                                        pixel_stride(dz), ptr(dbias), P, K, k_valid,
-                                       1 if relu else 0, seg_dtype(dy), wsp, wss,
+                                       1 if relu else 0, float(scale), seg_dtype(dy), wsp, wss,
                                        stream_ptr(stream)), "bias_relu_bwd")
     return dz
 

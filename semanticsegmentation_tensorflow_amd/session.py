@@ -1,0 +1,716 @@
+"""Session: compiles the symbolic graph into a static launch plan over the HIP
+C-ABI and runs it -- the stand-in for the reference's
+`sess.run(train_step, feed_dict)` (Network/model/FCN.py:395-398).
+
+Compilation (per fetch set and fed shapes):
+  * shape resolution with TF's rules (conv2d_transpose shape check included);
+  * fusion of single-consumer chains into one kernel launch each:
+      Conv2D [+BiasAdd] [+Relu] [+Dropout]      -> conv (fused epilogue)
+      Conv2DTranspose [+BiasAdd] [+Add]         -> tconv (bias + skip fusion)
+      FusedBatchNorm [+Relu]                    -> bn
+      SoftmaxXent + Mean                        -> xent (loss and dlogits)
+  * static device buffers (NHWC, channels padded to 8) for every activation,
+    gradient and workspace -- nothing is allocated while a step runs;
+  * backward in reverse order with gradients written straight into the flat
+    fp32 gradient buffer of the VariableStore; data-parallel buckets are
+    all-reduced (RCCL) as soon as their gradients are complete, overlapping the
+    rest of backward;
+  * TF1 Adam over the flat buffer, then re-packing of the bf16/fp32 filter
+    copies the convolution kernels read.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import graph as G
+from . import ops
+from .ops import round8
+from .variables import VariableStore
+
+_SEED_MIX = 0x9E3779B1
+
+
+class _Node:
+    """One fused kernel in the forward plan."""
+
+    def __init__(self, kind, ops_, inputs, output, **kw):
+        self.kind = kind
+        self.ops = ops_
+        self.inputs = inputs
+        self.output = output
+        self.__dict__.update(kw)
+
+
+class Plan:
+    pass
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        return x
+    return torch.from_numpy(np.ascontiguousarray(x))
+
+
+class Session:
+    def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None):
+        self.graph = graph or G.get_default_graph()
+        if not torch.cuda.is_available():
+            raise RuntimeError("Session needs an MI355X (HIP device); there is no CPU fallback")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.cdt = ops.BF16 if compute_dtype in ("bf16", "bfloat16") else ops.F32
+        self.tdt = ops.torch_dtype(self.cdt)
+        self.seed = seed
+        self.store = None
+        self.plans = {}
+        self.ws = ops.Workspace(self.device)
+        self.dp = data_parallel
+        self.run_count = 0
+        self._packed_version = -1
+        self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
+
+    # ------------------------------------------------------------------ vars
+    def _ensure_store(self):
+        if self.store is None or len(self.store.vars) != len(self.graph.variables):
+            old = self.store
+            self.store = VariableStore(list(self.graph.variables.values()), self.device, self.seed)
+            self.store.initialize()
+            if old is not None:
+                for v in old.vars:
+                    self.store.assign(v.var_name, old.read(v.var_name))
+            self.plans = {}
+        return self.store
+
+    def variable_value(self, name):
+        return self._ensure_store().read(name)
+
+    def assign(self, name, value):
+        self._ensure_store().assign(name, value)
+
+    # ------------------------------------------------------------------- run
+    def run(self, fetches, feed_dict=None, as_numpy=True):
+        feed_dict = feed_dict or {}
+        single = not isinstance(fetches, (list, tuple))
+        flist = [fetches] if single else list(fetches)
+        if any(isinstance(f, G.Op) and f.type == "InitAll" for f in flist):
+            self._ensure_store().initialize()
+            flist = [f for f in flist if not (isinstance(f, G.Op) and f.type == "InitAll")]
+            if not flist:
+                return None
+        self._ensure_store()
+        key = (tuple(id(f) for f in flist),
+               tuple(sorted((id(k), tuple(np.shape(v))) for k, v in feed_dict.items())))
+        plan = self.plans.get(key)
+        if plan is None:
+            plan = self._compile(flist, feed_dict)
+            self.plans[key] = plan
+        out = self._execute(plan, feed_dict)
+        res = []
+        for f in flist:
+            r = out.get(id(f))
+            if as_numpy and isinstance(r, torch.Tensor):
+                r = r.cpu().numpy()
+            res.append(r)
+        return res[0] if single else res
+
+    # --------------------------------------------------------------- compile
+    def _compile(self, fetches, feed_dict):
+        g = self.graph
+        store = self.store
+        p = Plan()
+        p.fetches = fetches
+        train = [f for f in fetches if isinstance(f, G.Op) and f.type == "TrainStep"]
+        p.train = train[0] if train else None
+        roots = [f.inputs[0] if isinstance(f, G.Op) else f for f in fetches]
+
+        # ---- needed ops (ancestors of the fetches), topological = creation order
+        needed = set()
+        stack = [t.op for t in roots]
+        while stack:
+            op = stack.pop()
+            if op.id in needed:
+                continue
+            needed.add(op.id)
+            stack.extend(t.op for t in op.inputs)
+        order = [op for op in g.ops if op.id in needed]
+        consumers = {}
+        for op in order:
+            for t in op.inputs:
+                consumers.setdefault(id(t), []).append(op)
+        fetched = {id(t) for t in roots}
+
+        # ---- concrete shapes
+        shp = {}
+        feeds = {id(k): v for k, v in feed_dict.items()}
+        for op in order:
+            y = op.outputs[0]
+            if op.type == "Placeholder":
+                if id(y) not in feeds:
+                    raise ValueError(f"placeholder {op.name} must be fed")
+                shp[id(y)] = tuple(np.shape(feeds[id(y)]))
+            elif op.type == "VariableV2":
+                shp[id(y)] = tuple(y.shape)
+            else:
+                shp[id(y)] = self._infer(op, shp)
+        p.shapes = shp
+
+        # ---- which tensors need gradients (depend on a trainable variable)
+        needs_grad = set()
+        if p.train:
+            var_ids = {id(v) for v in p.train.attrs["var_list"]}
+            for op in order:
+                if op.type == "VariableV2" and id(op.outputs[0]) in var_ids:
+                    needs_grad.add(id(op.outputs[0]))
+                elif any(id(t) in needs_grad for t in op.inputs):
+                    needs_grad.add(id(op.outputs[0]))
+        p.needs_grad = needs_grad
+
+        # ---- fusion into nodes
+        def single_consumer(t, type_):
+            cs = consumers.get(id(t), [])
+            if len(cs) == 1 and cs[0].type == type_ and id(t) not in fetched:
+                return cs[0]
+            return None
+
+        absorbed = set()
+        nodes = []
+        for op in order:
+            if op.id in absorbed or op.type in ("VariableV2",):
+                continue
+            t = op.type
+            y = op.outputs[0]
+            if t == "Conv2D":
+                x, w = op.inputs
+                chain = [op]
+                bias = relu = None
+                kp = None
+                cur = y
+                nxt = single_consumer(cur, "BiasAdd")
+                if nxt is not None and nxt.inputs[0] is cur:
+                    bias = nxt.inputs[1]
+                    chain.append(nxt)
+                    cur = nxt.outputs[0]
+                nxt = single_consumer(cur, "Relu")
+                if nxt is not None:
+                    relu = True
+                    chain.append(nxt)
+                    cur = nxt.outputs[0]
+                    nxt = single_consumer(cur, "Dropout")
+                    if nxt is not None:
+                        kp = nxt.attrs["keep_prob"]
+                        chain.append(nxt)
+                        cur = nxt.outputs[0]
+                for c in chain[1:]:
+                    absorbed.add(c.id)
+                nodes.append(_Node("conv", chain, [x], cur, w=w, bias=bias, relu=bool(relu), kp=kp,
+                                   stride=op.attrs["stride"], dilation=op.attrs["dilation"],
+                                   padding=op.attrs["padding"]))
+            elif t == "Conv2DTranspose":
+                x, w = op.inputs
+                chain = [op]
+                bias = res = None
+                cur = y
+                nxt = single_consumer(cur, "BiasAdd")
+                if nxt is not None and nxt.inputs[0] is cur:
+                    bias = nxt.inputs[1]
+                    chain.append(nxt)
+                    cur = nxt.outputs[0]
+                nxt = single_consumer(cur, "Add")
+                if nxt is not None:
+                    a, b = nxt.inputs
+                    other = b if a is cur else a
+                    if shp[id(other)] == shp[id(nxt.outputs[0])] and other is not cur:
+                        res = other
+                        chain.append(nxt)
+                        cur = nxt.outputs[0]
+                for c in chain[1:]:
+                    absorbed.add(c.id)
+                nodes.append(_Node("tconv", chain, [x], cur, w=w, bias=bias, residual=res,
+                                   stride=op.attrs["stride"], padding=op.attrs["padding"],
+                                   output_shape=op.attrs["output_shape"]))
+            elif t == "FusedBatchNorm":
+                x, gamma, beta = op.inputs
+                chain = [op]
+                cur = y
+                relu = False
+                nxt = single_consumer(cur, "Relu")
+                if nxt is not None:
+                    relu = True
+                    chain.append(nxt)
+                    cur = nxt.outputs[0]
+                    absorbed.add(nxt.id)
+                nodes.append(_Node("bn", chain, [x], cur, gamma=gamma, beta=beta, relu=relu,
+                                   eps=op.attrs["epsilon"]))
+            elif t == "SoftmaxXent":
+                logits, labels = op.inputs
+                mean = single_consumer(y, "Mean")
+                if mean is None:
+                    raise NotImplementedError("softmax_cross_entropy_with_logits must feed reduce_mean")
+                absorbed.add(mean.id)
+                nodes.append(_Node("xent", [op, mean], [logits], mean.outputs[0], labels=labels,
+                                   valid_hw=op.attrs["valid_hw"]))
+            elif t == "Placeholder":
+                nodes.append(_Node("input", [op], [], y))
+            elif t in ("MaxPool", "AvgPool", "Add", "Relu", "Dropout", "BiasAdd", "ConcatV2",
+                       "ResizeBilinear", "ArgMax", "ExpandDims", "Softmax"):
+                nodes.append(_Node(t, [op], list(op.inputs), y))
+            elif t == "Mean":
+                raise NotImplementedError("reduce_mean is only supported on the xent loss")
+            else:
+                raise NotImplementedError(f"op {t} is not on the hot path")
+        p.nodes = nodes
+        self._allocate(p, consumers, feeds)
+        return p
+
+    def _infer(self, op, shp):
+        t = op.type
+        ins = [shp.get(id(i)) for i in op.inputs]
+        if t == "Conv2D":
+            N, H, W, C = ins[0]
+            R, S, Ci, K = ins[1]
+            if Ci != C:
+                raise ValueError(f"{op.name}: input depth {C} != filter depth {Ci}")
+            d = ops.conv_desc(N, H, W, C, K, R, S, op.attrs["stride"], op.attrs["dilation"],
+                              op.attrs["padding"], self.cdt)
+            return (N, d.OH, d.OW, K)
+        if t == "Conv2DTranspose":
+            N, H, W, C = ins[0]
+            R, S, Co, Ci = ins[1]
+            os_ = G.resolve_shape(op.attrs["output_shape"], lambda tt: shp[id(tt)])
+            if os_[3] != Co or Ci != C:
+                raise ValueError(f"{op.name}: output/filter channel mismatch {os_} {ins[1]}")
+            ops.tconv_desc(N, H, W, C, os_[1], os_[2], Co, R, S, op.attrs["stride"],
+                           op.attrs["padding"], self.cdt)  # raises on TF shape-rule violation
+            return (N, os_[1], os_[2], Co)
+        if t in ("BiasAdd", "Relu", "Dropout", "FusedBatchNorm", "Softmax"):
+            return ins[0]
+        if t == "Add":
+            if ins[0] != ins[1]:
+                raise ValueError(f"{op.name}: incompatible shapes {ins[0]} vs {ins[1]}")
+            return ins[0]
+        if t in ("MaxPool", "AvgPool"):
+            N, H, W, C = ins[0]
+            return (N, H // 2, W // 2, C)
+        if t == "ConcatV2":
+            return tuple(ins[0][:3]) + (sum(s[3] for s in ins),)
+        if t == "ResizeBilinear":
+            N, H, W, C = ins[0]
+            return (N, op.attrs["size"][0], op.attrs["size"][1], C)
+        if t == "SoftmaxXent":
+            return tuple(ins[0][:3])
+        if t == "Mean":
+            return ()
+        if t == "ArgMax":
+            return tuple(ins[0][:3])
+        if t == "ExpandDims":
+            return tuple(ins[0]) + (1,)
+        raise NotImplementedError(t)
+
+    # -------------------------------------------------------------- buffers
+    def _act(self, shape):
+        N, H, W, C = shape
+        return torch.zeros(N, H, W, round8(C), dtype=self.tdt, device=self.device)
+
+    def _allocate(self, p, consumers, feeds):
+        dev = self.device
+        shp = p.shapes
+        buf = {}            # tensor id -> device tensor (padded)
+        p.buf = buf
+        p.feed_slots = {}   # tensor id -> (kind, staging)
+        store = self.store
+        ws_need = 0
+        p.packs = set()
+        for n in p.nodes:
+            y = n.output
+            if n.kind == "input":
+                s = shp[id(y)]
+                dt = n.ops[0].attrs["dtype"]
+                if dt in (G.float32, "float32") and len(s) == 4:
+                    # image placeholder: fp32 feed -> padded compute tensor
+                    stage = torch.zeros(s, dtype=torch.float32, device=dev)
+                    buf[id(y)] = self._act(s)
+                    p.feed_slots[id(y)] = ("image", stage)
+                elif dt in (G.uint8, "uint8"):
+                    stage = torch.zeros(s, dtype=torch.uint8, device=dev)
+                    buf[id(y)] = stage
+                    p.feed_slots[id(y)] = ("raw", stage)
+                elif len(s) == 0:
+                    p.feed_slots[id(y)] = ("scalar", None)
+                else:
+                    stage = torch.zeros(s, dtype=torch.float32, device=dev)
+                    buf[id(y)] = stage
+                    p.feed_slots[id(y)] = ("raw", stage)
+                continue
+            if n.kind == "xent":
+                n.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+                lg = n.inputs[0]
+                n.dlogits = torch.zeros_like(buf[id(lg)])
+                N, H, W = shp[id(lg)][:3]
+                vh, vw = n.valid_hw or (H, W)
+                n.count = N * vh * vw
+                n.num_classes = shp[id(lg)][3]
+                buf[id(y)] = n.loss_sum
+                continue
+            if n.kind in ("ArgMax",):
+                s = shp[id(y)]
+                buf[id(y)] = torch.zeros(s, dtype=torch.int64, device=dev)
+                continue
+            if n.kind == "ExpandDims":
+                src = buf[id(n.inputs[0])]
+                buf[id(y)] = src.unsqueeze(-1)
+                continue
+            s = shp[id(y)]
+            buf[id(y)] = self._act(s)
+            if n.kind == "conv":
+                x = n.inputs[0]
+                N, H, W, C = shp[id(x)]
+                R, S, _, K = n.w.shape
+                n.desc = ops.conv_desc(N, H, W, C, K, R, S, n.stride, n.dilation, n.padding, self.cdt)
+                ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_FWD))
+                p.packs.add((n.w.var_name, ops.PACK_KRSC))
+                if id(x) in p.needs_grad:
+                    p.packs.add((n.w.var_name, ops.PACK_HWIO))
+                if p.train:
+                    ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_BWD_DATA),
+                                  ops.conv_workspace(n.desc, ops.OP_BWD_FILTER),
+                                  4 * 1024 * 2 * round8(K))
+            elif n.kind == "tconv":
+                x = n.inputs[0]
+                N, H, W, C = shp[id(x)]
+                R, S, Co, _ = n.w.shape
+                _, OH, OW, _ = s
+                n.desc = ops.tconv_desc(N, H, W, C, OH, OW, Co, R, S, n.stride, n.padding, self.cdt)
+                p.packs.add((n.w.var_name, ops.PACK_TCONV_FWD))
+                if id(x) in p.needs_grad:
+                    p.packs.add((n.w.var_name, ops.PACK_TCONV_BWD))
+                if p.train:
+                    ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_TBWD_DATA),
+                                  ops.conv_workspace(n.desc, ops.OP_TBWD_FILTER),
+                                  4 * 1024 * 2 * round8(Co))
+            elif n.kind == "bn":
+                ws_need = max(ws_need, 4 * 1024 * 2 * round8(s[3]))
+        ws_need = max(ws_need, 8192)
+        self.ws.get(ws_need)
+        # packed filter copies
+        for name, mode in sorted(p.packs):
+            if (name, mode) not in store.packed:
+                R, S, A, B = store.by_name[name].shape
+                t = torch.zeros(ops.packed_shape(R, S, A, B, mode), dtype=self.tdt, device=dev)
+                store.packed[(name, mode)] = (t, round8(A), round8(B))
+        self._packed_version = -1
+        # gradient buffers / plan for backward
+        if p.train:
+            self._plan_backward(p)
+
+    def _plan_backward(self, p):
+        dev = self.device
+        grad = {}
+        p.grad = grad
+        p.tmp = {}
+        # grads of variables go to the flat buffer; activations get their own
+        covered = set()
+        for n in p.nodes:
+            if n.kind == "conv":
+                covered.add(n.w.var_name)
+                if n.bias is not None:
+                    covered.add(n.bias.var_name)
+            elif n.kind == "tconv":
+                covered.add(n.w.var_name)
+                if n.bias is not None:
+                    covered.add(n.bias.var_name)
+            elif n.kind == "bn":
+                covered.update([n.gamma.var_name, n.beta.var_name])
+            elif n.kind == "BiasAdd":
+                covered.add(n.inputs[1].var_name)
+        p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
+        p.uncovered = [v for v in p.var_names if v not in covered]
+        for v in p.uncovered:            # no gradient path: keep the grad slice at 0
+            self.store.grad(v).zero_()
+        # data parallel bucket schedule (var readiness in backward order)
+        if self.dp is not None:
+            self.dp.prepare(self.store)
+
+    # -------------------------------------------------------------- execute
+    def _repack(self, p):
+        store = self.store
+        if self._packed_version == store.version:
+            return
+        for (name, mode), (t, ap, bp) in store.packed.items():
+            ops.pack_filter(store.param(name), t, ap, bp, mode)
+        self._packed_version = store.version
+
+    def _feed(self, p, feed_dict):
+        feeds = {id(k): v for k, v in feed_dict.items()}
+        # scalars (keep_probability) are read at launch time, not staged
+        scal = {id(k): float(v) for k, v in feed_dict.items() if np.ndim(v) == 0}
+        for tid, (kind, stage) in p.feed_slots.items():
+            v = feeds[tid]
+            if kind == "scalar":
+                scal[tid] = float(v)
+                continue
+            src = _np(v)
+            if src.is_cuda and src.dtype == stage.dtype and src.is_contiguous() and src.shape == stage.shape:
+                src_dev = src                      # resident in HBM: no copy
+            else:
+                stage.copy_(src.to(stage.dtype) if src.dtype != stage.dtype else src, non_blocking=True)
+                src_dev = stage
+            if kind == "image":
+                ops.prepare_input(src_dev, p.buf[tid])
+            else:
+                p.buf[tid] = src_dev
+        return scal
+
+    def _kp(self, kp, scal):
+        if kp is None:
+            return 1.0
+        if isinstance(kp, G.Tensor):
+            return scal[id(kp)]
+        return float(kp)
+
+    def _execute(self, p, feed_dict):
+        self.run_count += 1
+        self._repack(p)
+        scal = self._feed(p, feed_dict)
+        buf = p.buf
+        store = self.store
+        step_seed = (self.seed * 1000003 + self.run_count * 7919) & 0xFFFFFFFF
+        if self.dp is not None:
+            step_seed ^= (self.dp.rank + 1) * _SEED_MIX
+        out = {}
+        # ---------------- forward
+        for i, n in enumerate(p.nodes):
+            k = n.kind
+            if k == "input":
+                continue
+            y = buf[id(n.output)]
+            if k == "conv":
+                x = buf[id(n.inputs[0])]
+                kp = self._kp(n.kp, scal)
+                n.kp_val = kp
+                n.seed_val = (step_seed + i * 131) & 0xFFFFFFFF
+                epi = ops.epilogue(bias=store.param(n.bias.var_name) if n.bias is not None else None,
+                                   relu=n.relu, keep_prob=kp, seed=n.seed_val)
+                self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
+                            store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
+            elif k == "tconv":
+                x = buf[id(n.inputs[0])]
+                res = buf[id(n.residual)] if n.residual is not None else None
+                epi = ops.epilogue(bias=store.param(n.bias.var_name) if n.bias is not None else None,
+                                   residual=res)
+                self._timed(n.desc, ops.OP_TFWD, ops.tconv2d_fwd, n.desc, x,
+                            store.packed[(n.w.var_name, ops.PACK_TCONV_FWD)][0], y, epi, self.ws)
+            elif k == "MaxPool":
+                ops.maxpool2x2_fwd(buf[id(n.inputs[0])], y)
+            elif k == "AvgPool":
+                ops.avgpool2x2_fwd(buf[id(n.inputs[0])], y)
+            elif k == "Add":
+                ops.add(buf[id(n.inputs[0])], buf[id(n.inputs[1])], y)
+            elif k == "bn":
+                C = p.shapes[id(n.inputs[0])][3]
+                ops.bn_relu_fwd(buf[id(n.inputs[0])], y, store.param(n.gamma.var_name),
+                                store.param(n.beta.var_name), C, n.relu, n.eps)
+            elif k == "Relu":
+                self._relu_fwd(buf[id(n.inputs[0])], y)
+            elif k == "Dropout":
+                kp = self._kp(n.ops[0].attrs["keep_prob"], scal)
+                n.kp_val = kp
+                n.seed_val = (step_seed + i * 131) & 0xFFFFFFFF
+                if kp < 1.0:
+                    ops.dropout_fwd(buf[id(n.inputs[0])], y, kp, n.seed_val)
+                else:
+                    ops.copy_channels(buf[id(n.inputs[0])], y)
+            elif k == "xent":
+                lg = buf[id(n.inputs[0])]
+                labels = buf[id(n.labels)]
+                ops.softmax_xent(lg, labels, n.dlogits, n.loss_sum, n.num_classes, n.valid_hw,
+                                 grad_scale=1.0 / n.count, ws=self.ws)
+            elif k == "ArgMax":
+                x = buf[id(n.inputs[0])]
+                C = p.shapes[id(n.inputs[0])][3]
+                ops.argmax(x, y.view(-1), C)
+            elif k == "ExpandDims":
+                pass
+            else:
+                raise NotImplementedError(k)
+        # ---------------- backward + optimizer
+        if p.train:
+            self._backward(p, scal)
+            ts = p.train.attrs
+            opt = ts["optimizer"]
+            gs = ts["grad_scale"]
+            if self.dp is not None:
+                self.dp.finish()
+                gs = gs / self.dp.world
+            store.step += 1
+            ops.adam_tf1_step(store.params, store.grads, store.m, store.v, opt.lr, store.step,
+                              opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs)
+            store.version += 1
+        # ---------------- fetch values
+        for f in p.fetches:
+            if isinstance(f, G.Op):
+                out[id(f)] = None
+                continue
+            t = buf.get(id(f))
+            node = next((n for n in p.nodes if n.output is f), None)
+            if node is not None and node.kind == "xent":
+                out[id(f)] = (t / node.count).reshape(())
+            elif f.dtype == G.int64:
+                out[id(f)] = t
+            else:
+                C = p.shapes[id(f)][3]
+                out[id(f)] = t[..., :C].float()
+        return out
+
+    def _timed(self, desc, op, fn, *args):
+        if self.timer is None:
+            return fn(*args)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn(*args)
+        e.record()
+        self.timer.append((desc, op, s, e))
+
+    def _relu_fwd(self, x, y):
+        C = x.shape[-1]
+        one = torch.ones(C, dtype=torch.float32, device=self.device)
+        zero = torch.zeros(C, dtype=torch.float32, device=self.device)
+        ops.bn_relu_fwd(x, y, one, zero, C, True, eps=0.0)
+
+    # ------------------------------------------------------------- backward
+    def _backward(self, p, scal):
+        buf = p.buf
+        store = self.store
+        grad = {}
+        ws = self.ws
+        ng = p.needs_grad
+
+        def dest(t):
+            """(buffer to write t's gradient into, accumulate-after flag)."""
+            if id(t) not in grad:
+                gbuf = p.tmp.get(("g", id(t)))
+                if gbuf is None:
+                    gbuf = torch.zeros_like(buf[id(t)])
+                    p.tmp[("g", id(t))] = gbuf
+                grad[id(t)] = gbuf
+                return gbuf, None
+            tmp = p.tmp.get(("acc", id(t)))
+            if tmp is None:
+                tmp = torch.zeros_like(buf[id(t)])
+                p.tmp[("acc", id(t))] = tmp
+            return tmp, grad[id(t)]
+
+        def done(dst, acc):
+            if acc is not None:
+                ops.add(acc, dst, acc)
+
+        def contribute_alias(t, g):
+            if id(t) not in ng:
+                return
+            if id(t) not in grad:
+                grad[id(t)] = g
+            else:
+                ops.add(grad[id(t)], g, grad[id(t)])
+
+        for n in reversed(p.nodes):
+            k = n.kind
+            if k == "input" or id(n.output) not in ng:
+                continue
+            if k == "xent":
+                contribute_alias(n.inputs[0], n.dlogits)
+                continue
+            dy = grad.get(id(n.output))
+            if dy is None:
+                continue          # output does not reach the loss
+            if k == "conv":
+                x = n.inputs[0]
+                yb = buf[id(n.output)]
+                dz = dy
+                if n.relu or n.bias is not None:
+                    scale = 1.0 / n.kp_val if (n.kp_val is not None and n.kp_val < 1.0) else 1.0
+                    dz = p.tmp.get(("dz", id(n.output)))
+                    if dz is None:
+                        dz = torch.zeros_like(yb)
+                        p.tmp[("dz", id(n.output))] = dz
+                    db = store.grad(n.bias.var_name) if n.bias is not None else None
+                    K = n.desc.k_valid
+                    self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws)
+                    done(dx, acc)
+                self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
+                            store.grad(n.w.var_name), ws)
+                if self.dp is not None:
+                    self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
+            elif k == "tconv":
+                x = n.inputs[0]
+                if n.bias is not None:
+                    self._bias_relu_bwd(dy, None, dy, store.grad(n.bias.var_name), n.desc.k_valid, False, 1.0)
+                if n.residual is not None:
+                    contribute_alias(n.residual, dy)
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    self._timed(n.desc, ops.OP_TBWD_DATA, ops.tconv2d_bwd_data, n.desc, dy,
+                                store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws)
+                    done(dx, acc)
+                self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
+                            store.grad(n.w.var_name), ws)
+                if self.dp is not None:
+                    self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
+            elif k == "MaxPool":
+                x = n.inputs[0]
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    ops.maxpool2x2_bwd(buf[id(x)], buf[id(n.output)], dy, dx)
+                    done(dx, acc)
+            elif k == "AvgPool":
+                x = n.inputs[0]
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    ops.avgpool2x2_bwd(dy, dx)
+                    done(dx, acc)
+            elif k == "Add":
+                for t in n.inputs:
+                    contribute_alias(t, dy)
+            elif k == "bn":
+                x = n.inputs[0]
+                C = p.shapes[id(x)][3]
+                dx, acc = dest(x)
+                ops.bn_relu_bwd(buf[id(x)], buf[id(n.output)], dy, dx, store.param(n.gamma.var_name),
+                                store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
+                                n.eps, ws)
+                done(dx, acc)
+                if self.dp is not None:
+                    self.dp.ready([n.gamma.var_name, n.beta.var_name])
+            elif k == "Relu":
+                x = n.inputs[0]
+                dx, acc = dest(x)
+                self._bias_relu_bwd(dy, buf[id(n.output)], dx, None, p.shapes[id(x)][3], True, 1.0)
+                done(dx, acc)
+            elif k == "Dropout":
+                x = n.inputs[0]
+                dx, acc = dest(x)
+                if n.kp_val < 1.0:
+                    ops.dropout_fwd(dy, dx, n.kp_val, n.seed_val)
+                else:
+                    ops.copy_channels(dy, dx)
+                done(dx, acc)
+            elif k in ("ArgMax", "ExpandDims"):
+                continue
+            else:
+                raise NotImplementedError(f"backward of {k}")
+
+    def _bias_relu_bwd(self, dy, y, dz, dbias, k_valid, relu, scale):
+        # with TF1 dropout fused after the relu: dz = dy * (y > 0) / keep_prob
+        ops.bias_relu_bwd(dy, y, dz, dbias, k_valid, relu, self.ws, scale=scale)
+
+    def close(self):
+        self.plans = {}
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

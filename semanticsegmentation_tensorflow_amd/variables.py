@@ -1,0 +1,116 @@
+"""Device storage for the graph's variables.
+
+All trainable variables live in ONE flat fp32 buffer (plus flat grad / Adam m
+/ Adam v buffers of the same layout), ordered in *reverse creation order* --
+the order backward produces their gradients -- so that data-parallel
+all-reduce buckets are contiguous slices that become ready one after another.
+Each variable keeps its TF name and TF layout (`conv1_1/weights` HWIO,
+`conv_t1/weights` [kh,kw,out,in]) so checkpoints map 1:1.
+
+Initial values come from a counter-based generator (numpy Philox keyed by
+(seed, crc32(name))), so any host -- including the CPU oracle in the tests --
+can regenerate exactly the same weights.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import torch
+
+from . import graph as G
+
+ALIGN = 4   # floats: every variable starts 16-byte aligned
+
+
+def init_value(var: G.Variable, seed: int = 0) -> np.ndarray:
+    """Deterministic initial value of a variable (float32 numpy)."""
+    ini = var.initializer
+    shape = tuple(var.shape)
+    if isinstance(ini, G.constant_initializer):
+        return np.full(shape, ini.value, dtype=np.float32)
+    if isinstance(ini, G.random_normal_initializer):
+        key = zlib.crc32(var.var_name.encode()) & 0xFFFFFFFF
+        rng = np.random.Generator(np.random.Philox(key=[seed & 0xFFFFFFFFFFFFFFFF, key]))
+        return (rng.standard_normal(shape, dtype=np.float32) * np.float32(ini.stddev)
+                + np.float32(ini.mean)).astype(np.float32)
+    if callable(ini):
+        return np.asarray(ini(shape), dtype=np.float32)
+    raise TypeError(f"unsupported initializer {ini!r}")
+
+
+class VariableStore:
+    def __init__(self, variables, device, seed=0):
+        self.vars = list(variables)
+        self.device = device
+        self.seed = seed
+        order = list(reversed(self.vars))
+        self.offset = {}
+        off = 0
+        for v in order:
+            self.offset[v.var_name] = off
+            n = int(np.prod(v.shape))
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.params = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grads = torch.zeros(off, dtype=torch.float32, device=device)
+        self.m = torch.zeros(off, dtype=torch.float32, device=device)
+        self.v = torch.zeros(off, dtype=torch.float32, device=device)
+        self.by_name = {v.var_name: v for v in self.vars}
+        self.order = order
+        self.step = 0           # Adam t (TF beta powers)
+        self.packed = {}        # (var_name, mode) -> (tensor, a_pad, b_pad)
+        self.version = 0        # bumped on every update -> repack
+
+    def _view(self, buf, name):
+        v = self.by_name[name]
+        n = int(np.prod(v.shape))
+        o = self.offset[name]
+        return buf[o:o + n].view(*v.shape)
+
+    def param(self, name):
+        return self._view(self.params, name)
+
+    def grad(self, name):
+        return self._view(self.grads, name)
+
+    def initialize(self):
+        host = np.zeros(self.numel, dtype=np.float32)
+        for v in self.vars:
+            n = int(np.prod(v.shape))
+            o = self.offset[v.var_name]
+            host[o:o + n] = init_value(v, self.seed).reshape(-1)
+        self.params.copy_(torch.from_numpy(host).to(self.device))
+        self.m.zero_()
+        self.v.zero_()
+        self.step = 0
+        self.version += 1
+
+    def assign(self, name, value):
+        t = torch.as_tensor(np.asarray(value, dtype=np.float32)).to(self.device)
+        self.param(name).copy_(t.view(self.by_name[name].shape))
+        self.version += 1
+
+    def read(self, name):
+        return self.param(name).detach().cpu().numpy().copy()
+
+    def state_dict(self):
+        """TF-Saver-compatible names -> numpy arrays (plus Adam slots)."""
+        out = {}
+        for v in self.vars:
+            out[v.var_name] = self.read(v.var_name)
+            out[v.var_name + "/Adam"] = self._view(self.m, v.var_name).cpu().numpy().copy()
+            out[v.var_name + "/Adam_1"] = self._view(self.v, v.var_name).cpu().numpy().copy()
+        out["beta_step"] = np.array(self.step)
+        return out
+
+    def load_state_dict(self, d):
+        for v in self.vars:
+            if v.var_name in d:
+                self.assign(v.var_name, d[v.var_name])
+            if v.var_name + "/Adam" in d:
+                self._view(self.m, v.var_name).copy_(torch.from_numpy(np.asarray(d[v.var_name + "/Adam"], np.float32)).to(self.device))
+                self._view(self.v, v.var_name).copy_(torch.from_numpy(np.asarray(d[v.var_name + "/Adam_1"], np.float32)).to(self.device))
+        if "beta_step" in d:
+            self.step = int(d["beta_step"])
+        self.version += 1

@@ -1,0 +1,137 @@
+"""FCN model parity: Session (HIP path) vs the CPU oracle restatement of
+Network/model/FCN.py on identical inputs and weights.
+
+Tolerances (stated per the north star): fp32 compute path -- logits/loss
+within 1e-4 relative, every one of the 40 gradients within 2e-3 relative (of
+its max |value|; fp32 accumulation order differs from the fp64 oracle over
+reductions of up to ~10^5 terms).  bf16 path -- logits within 3e-2, gradients
+within 8e-2 relative, loss within 1e-2.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import models as M
+from oracle import tf1_ops as tf_ref
+from semanticsegmentation_tensorflow_amd import graph as G
+from semanticsegmentation_tensorflow_amd import tf
+from semanticsegmentation_tensorflow_amd.fcn import FCN
+
+pytestmark = pytest.mark.gpu
+
+
+def he_weights(shapes, seed):
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, s in shapes.items():
+        if len(s) == 4:
+            R, S_, A, B = s
+            fan = R * S_ * (A if "conv_t" not in name else B)
+            out[name] = (rng.standard_normal(s) * math.sqrt(2.0 / fan)).astype(np.float32)
+            if "conv_t" in name:      # transposed: fan-in ~ in_ch * (k/stride)^2
+                out[name] *= np.float32(R / (4.0 if R == 4 else 16.0))
+        else:
+            out[name] = (0.05 * rng.standard_normal(s)).astype(np.float32)
+    return out
+
+
+def synthetic_batch(N, H, W, seed):
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 256, size=(N, H, W, 3)).astype(np.float32)
+    lab = np.zeros((N, H, W), dtype=np.uint8)
+    lab[:, H // 2:, W // 4: 3 * W // 4] = 1
+    flip = rng.random((N, H, W)) < 0.05
+    lab = np.where(flip, 1 - lab, lab).astype(np.uint8)
+    return img, lab
+
+
+def build_fcn(H, W):
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, shape=[None, H, W, 3], name="input_image")
+    labels = tf.placeholder(tf.uint8, shape=[None, H, W], name="annotation")
+    keep = tf.placeholder(tf.float32, name="keep_probability")
+    fcn = FCN(image, keep, 2)
+    pred, logits = fcn.create()
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    return image, labels, keep, pred, logits, loss, train_step
+
+
+def oracle_step(weights, img, lab):
+    p = {k: torch.from_numpy(v).double().requires_grad_(True) for k, v in weights.items()}
+    x = torch.from_numpy(img).double()
+    pred, logits = M.fcn_forward(p, x)
+    loss = tf_ref.mean_softmax_xent(logits, tf_ref.one_hot(torch.from_numpy(lab), 2))
+    loss.backward()
+    grads = {k: v.grad.numpy() for k, v in p.items()}
+    return pred.numpy(), logits.detach().numpy(), loss.item(), grads
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fcn_logits_grads_adam(dev, dtype):
+    N, H, W = 2, 64, 96
+    image, labels, keep, pred, logits, loss, train_step = build_fcn(H, W)
+    shapes = M.fcn_param_shapes(3, 2)
+    vars_ = {v.var_name: v for v in tf.global_variables()}
+    assert set(vars_) == set(shapes)
+    assert all(tuple(vars_[k].shape) == tuple(s) for k, s in shapes.items())
+    assert sum(int(np.prod(s)) for s in shapes.values()) == 138_873_924
+
+    weights = he_weights(shapes, 1)
+    img, lab = synthetic_batch(N, H, W, 2)
+    if dtype == "bf16":   # the device sees bf16-rounded weights/inputs in its convs
+        weights_ref = {k: (torch.from_numpy(v).bfloat16().float().numpy() if v.ndim == 4 else v)
+                       for k, v in weights.items()}
+    else:
+        weights_ref = weights
+    r_pred, r_logits, r_loss, r_grads = oracle_step(weights_ref, img, lab)
+
+    sess = tf.Session(compute_dtype=dtype)
+    sess.run(tf.global_variables_initializer())
+    for k, v in weights.items():
+        sess.assign(k, v)
+    out_pred, out_logits, out_loss, _ = sess.run(
+        [pred, logits, loss, train_step], feed_dict={image: img, labels: lab, keep: 1.0})
+    torch.cuda.synchronize()
+
+    tl = {"f32": (1e-4, 2e-3, 1e-4), "bf16": (3e-2, 8e-2, 1e-2)}[dtype]
+    e_log = np.abs(out_logits - r_logits).max() / np.abs(r_logits).max()
+    assert e_log < tl[0], f"logits rel err {e_log:.3e}"
+    assert abs(out_loss - r_loss) <= tl[2] * max(1.0, abs(r_loss)), (out_loss, r_loss)
+    if dtype == "f32":
+        agree = (out_pred == r_pred).mean()
+        assert agree > 0.999, agree
+    worst = []
+    for k, gref in r_grads.items():
+        gg = sess.store.grad(k).cpu().numpy()
+        e = np.abs(gg - gref).max() / max(np.abs(gref).max(), 1e-30)
+        worst.append((e, k))
+        assert e < tl[1], f"grad {k} rel err {e:.3e}"
+    # one TF1 Adam step on every variable
+    opt = tf_ref.AdamTF1(lr=1e-4)
+    upd = opt.apply({k: torch.from_numpy(v).double() for k, v in weights.items()},
+                    {k: torch.from_numpy(sess.store.grad(k).cpu().numpy()).double() for k in weights})
+    for k in ["conv1_1/weights", "conv6/weights", "conv_t3/bias", "conv8/biases"]:
+        got = sess.variable_value(k)
+        ref = upd[k].numpy()
+        assert np.abs(got - ref).max() <= 1e-6 + 1e-5 * np.abs(ref).max(), k
+    print("worst grads", sorted(worst)[-3:])
+
+
+def test_fcn_dropout_and_repeat_steps(dev):
+    """keep_prob=0.8 path runs, loss decreases over a few Adam steps (bf16)."""
+    N, H, W = 2, 64, 96
+    image, labels, keep, pred, logits, loss, train_step = build_fcn(H, W)
+    sess = tf.Session(compute_dtype="bf16", seed=3)
+    sess.run(tf.global_variables_initializer())
+    for k, v in he_weights(M.fcn_param_shapes(3, 2), 4).items():
+        sess.assign(k, v)
+    img, lab = synthetic_batch(N, H, W, 5)
+    losses = []
+    for _ in range(8):
+        _, l = sess.run([train_step, loss], feed_dict={image: img, labels: lab, keep: 0.8})
+        losses.append(float(l))
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0], losses

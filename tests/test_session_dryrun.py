@@ -1,0 +1,103 @@
+"""Host-logic test of the Session compiler (no GPU): the C-ABI is replaced by a
+recording stub so plan construction, fusion decisions, buffer allocation and
+launch order can be checked on CPU.  Nothing is computed -- numerics are
+covered by the -m gpu tests."""
+import numpy as np
+import pytest
+import torch
+
+from semanticsegmentation_tensorflow_amd import _lib, ops
+from semanticsegmentation_tensorflow_amd import graph as G
+from semanticsegmentation_tensorflow_amd import session as S
+from semanticsegmentation_tensorflow_amd import tf
+from semanticsegmentation_tensorflow_amd.fcn import FCN
+
+
+class _Rec:
+    def __init__(self, real):
+        self.real = real
+        self.calls = []
+
+    def __getattr__(self, name):
+        real_fn = getattr(self.real, name)
+        host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
+                             "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string")
+
+        def fn(*a):
+            if host_only:
+                return real_fn(*a)
+            self.calls.append(name)
+            return 0
+        return fn
+
+
+@pytest.fixture
+def dry(monkeypatch):
+    real = _lib.load()
+    rec = _Rec(real)
+    monkeypatch.setattr(_lib, "lib", lambda: rec)
+    monkeypatch.setattr(ops, "stream_ptr", lambda s=None: None)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    return rec
+
+
+def test_fcn_train_plan(dry):
+    G.reset_default_graph()
+    H, W = 64, 96
+    image = tf.placeholder(tf.float32, [None, H, W, 3])
+    labels = tf.placeholder(tf.uint8, [None, H, W])
+    keep = tf.placeholder(tf.float32)
+    pred, logits = FCN(image, keep, 2).create()
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="bf16")
+    sess.run(tf.global_variables_initializer())
+    img = np.zeros((2, H, W, 3), np.float32)
+    lab = np.zeros((2, H, W), np.uint8)
+    dry.calls.clear()
+    sess.run([train, loss], feed_dict={image: img, labels: lab, keep: 0.8})
+    c = dry.calls
+    # forward: 17 fused conv launches, 3 tconv, 5 pools, 1 loss
+    assert c.count("seg_conv2d_fwd") == 17
+    assert c.count("seg_tconv2d_fwd") == 3
+    assert c.count("seg_maxpool2x2_fwd") == 5
+    assert c.count("seg_softmax_xent_fwd_bwd") == 1
+    # backward: conv1_1 needs no input gradient (image is a placeholder)
+    assert c.count("seg_conv2d_bwd_data") == 16
+    assert c.count("seg_conv2d_bwd_filter") == 17
+    assert c.count("seg_tconv2d_bwd_data") == 3
+    assert c.count("seg_tconv2d_bwd_filter") == 3
+    assert c.count("seg_maxpool2x2_bwd") == 5
+    assert c.count("seg_adam_tf1_step") == 1
+    # skip fusion: pool3/pool4 gradients = sum of two consumers
+    assert c.count("seg_add") == 2
+    # filter copies are packed once per update (first run) -- KRSC for all 17 convs,
+    # HWIO for the 16 with input grads, 2 layouts x 3 tconvs
+    assert c.count("seg_pack_filter") == 17 + 16 + 6
+    assert c.index("seg_adam_tf1_step") > c.index("seg_conv2d_bwd_filter")
+    dry.calls.clear()
+    sess.run(train, feed_dict={image: img, labels: lab, keep: 1.0})
+    assert dry.calls.count("seg_pack_filter") == 17 + 16 + 6   # repack after the Adam update
+    assert dry.calls.count("seg_conv2d_fwd") == 17
+
+
+def test_inference_plan_has_no_backward(dry):
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, 64, 96, 3])
+    pred, logits = FCN(image, 1.0, 2).create()
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="f32")
+    sess.run(tf.global_variables_initializer())
+    dry.calls.clear()
+    sess.run(pred, feed_dict={image: np.zeros((1, 64, 96, 3), np.float32)})
+    assert "seg_conv2d_bwd_data" not in dry.calls
+    assert dry.calls.count("seg_argmax") == 1
+
+
+def test_tconv_shape_rule_at_375x1242(dry):
+    """The reference cannot run 375x1242 through FCN: same here."""
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, 375, 1242, 3])
+    pred, logits = FCN(image, 1.0, 2).create()
+    sess = S.Session(device=torch.device("cpu"))
+    with pytest.raises(ValueError):
+        sess.run(logits, feed_dict={image: np.zeros((1, 375, 1242, 3), np.float32)})
