@@ -60,30 +60,34 @@ def deconv_layer(x, p, name, out_shape, stride=2):
                        p[f"{name}/biases"])
 
 
-def fcn_forward(p, x, keep_prob=1.0, dropout_u=None, num_classes=2, return_acts=False):
-    """Returns (pred [N,H,W,1] int64, logits [N,H,W,C]) like FCN.create() (FCN.py:114)."""
+def fcn_forward(p, x, keep_prob=1.0, dropout_u=None, num_classes=2, return_acts=False, quant=None):
+    """Returns (pred [N,H,W,1] int64, logits [N,H,W,C]) like FCN.create() (FCN.py:114).
+
+    `quant` (optional) is applied wherever a device implementation stores an
+    activation (each conv/tconv layer output and the logits) -- e.g. rounding
+    to bf16 -- so a reduced-precision device path can be compared at matched
+    rounding points.  Gradients pass through it unchanged."""
+    q = quant or (lambda t: t)
     acts = {}
     h = x
     for name, _, _ in FCN_CONVS[:14]:
-        h = conv_layer(h, p, name)
+        h = q(conv_layer(h, p, name))
         acts[name] = h
         if name in POOL_AFTER:
             h = tf.max_pool2x2(h)
             acts[POOL_AFTER[name]] = h
     du = dropout_u or {}
-    h = conv_layer(h, p, "conv6")
-    h = tf.dropout(h, keep_prob, du.get("dropout6"))
-    h = conv_layer(h, p, "conv7")
-    h = tf.dropout(h, keep_prob, du.get("dropout7"))
-    conv8 = conv_layer(h, p, "conv8")
+    h = q(tf.dropout(conv_layer(h, p, "conv6"), keep_prob, du.get("dropout6")))
+    h = q(tf.dropout(conv_layer(h, p, "conv7"), keep_prob, du.get("dropout7")))
+    conv8 = q(conv_layer(h, p, "conv8"))
     pool4, pool3 = acts["pool4"], acts["pool3"]
     t1 = deconv_layer(conv8, p, "conv_t1", tuple(pool4.shape))
-    fuse1 = tf.add(t1, pool4)
+    fuse1 = q(tf.add(t1, pool4))
     t2 = deconv_layer(fuse1, p, "conv_t2", tuple(pool3.shape))
-    fuse2 = tf.add(t2, pool3)
+    fuse2 = q(tf.add(t2, pool3))
     N, H, W, _ = x.shape
     t3 = tf.conv2d_transpose(fuse2, p["conv_t3/weights"], (N, H, W, num_classes), 8)
-    logits = tf.bias_add(t3, p["conv_t3/bias"])
+    logits = q(tf.bias_add(t3, p["conv_t3/bias"]))
     pred = tf.argmax(logits).unsqueeze(-1)
     if return_acts:
         acts.update(conv8=conv8, fuse_1=fuse1, fuse_2=fuse2)

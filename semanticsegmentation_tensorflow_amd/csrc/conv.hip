@@ -279,26 +279,58 @@ extern "C" int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, con
 // ---------------------------------------------------------------------------
 // filter packing
 // ---------------------------------------------------------------------------
+// dst [RS][ap][bp] <- src [RS][av][bv]: one thread per 8 consecutive b.
 template <typename T>
-__global__ void pack_filter_k(const float* __restrict__ src, T* __restrict__ dst, int R, int S, int av, int bv,
-                              int ap, int bp, int bmajor) {
-    const long total = (long)R * S * ap * bp;
+__global__ void pack_rows_k(const float* __restrict__ src, T* __restrict__ dst, int RS, int av, int bv, int ap,
+                            int bp) {
+    const int b8 = bp / 8;
+    const long total = (long)RS * ap * b8;
+    const bool vec = (bv & 3) == 0;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        int a, b, rs;
-        if (bmajor) {  // dst [bp][R][S][ap]
-            a = (int)(i % ap);
-            long t = i / ap;
-            rs = (int)(t % (R * S));
-            b = (int)(t / (R * S));
-        } else {       // dst [R][S][ap][bp]
-            b = (int)(i % bp);
-            long t = i / bp;
-            a = (int)(t % ap);
-            rs = (int)(t / ap);
+        const int bc = (int)(i % b8);
+        const long ra = i / b8;              // rs * ap + a
+        const int a = (int)(ra % ap);
+        const long rs = ra / ap;
+        float v[8];
+        const int b0 = bc * 8;
+        const float* srow = src + (rs * av + a) * (long)bv;
+        if (a < av && vec && b0 + 8 <= bv) {
+            const float4 x0 = *reinterpret_cast<const float4*>(srow + b0);
+            const float4 x1 = *reinterpret_cast<const float4*>(srow + b0 + 4);
+            v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+            v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (a < av && b0 + e < bv) ? srow[b0 + e] : 0.f;
         }
-        float v = 0.f;
-        if (a < av && b < bv) v = src[((long)rs * av + a) * bv + b];
-        dst[i] = from_f32<T>(v);
+        T* d = dst + ra * bp + b0;
+        if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4*>(d) = Chunk<bf16>::pack(v);
+        } else {
+            *reinterpret_cast<uint4*>(d) = Chunk<float>::pack(v);
+            *reinterpret_cast<uint4*>(d + 4) = Chunk<float>::pack(v + 4);
+        }
+    }
+}
+
+// dst [bp][RS][ap] <- src [RS][av][bv]: 64x64 tiles transposed through LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_transpose_k(const float* __restrict__ src, T* __restrict__ dst, int RS,
+                                                        int av, int bv, int ap, int bp) {
+    __shared__ float tile[64][65];
+    const int tiles_a = (ap + 63) / 64;
+    const int ta = blockIdx.x % tiles_a, tb = blockIdx.x / tiles_a;
+    const long rs = blockIdx.y;
+    const int a0 = ta * 64, b0 = tb * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {          // rows of a, coalesced along b
+        const int a = a0 + r, b = b0 + tx;
+        tile[r][tx] = (a < av && b < bv) ? src[(rs * av + a) * (long)bv + b] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {          // rows of b, coalesced along a
+        const int b = b0 + r, a = a0 + tx;
+        if (b < bp && a < ap) dst[((long)b * RS + rs) * ap + a] = from_f32<T>(tile[tx][r]);
     }
 }
 
@@ -306,16 +338,27 @@ extern "C" int seg_pack_filter(const float* src, void* dst, int R, int S, int a_
                                int b_pad, int mode, int dtype, void* stream) {
     if (!src || !dst || a_pad < a_valid || b_pad < b_valid || mode < 0 || mode > 3) return SEG_EINVAL;
     const int bmajor = (mode == 0 || mode == 3);
-    const long total = (long)R * S * a_pad * b_pad;
-    const int grid = seg_grid_1d(total, 256);
-    if (dtype == SEG_BF16)
-        hipLaunchKernelGGL(pack_filter_k<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst, R,
-                           S, a_valid, b_valid, a_pad, b_pad, bmajor);
-    else if (dtype == SEG_F32)
-        hipLaunchKernelGGL(pack_filter_k<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, (float*)dst, R,
-                           S, a_valid, b_valid, a_pad, b_pad, bmajor);
-    else
-        return SEG_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const int RS = R * S;
+    if ((a_pad & 7) || (b_pad & 7)) return SEG_EALIGN;
+    if (bmajor) {
+        dim3 grid(((a_pad + 63) / 64) * ((b_pad + 63) / 64), RS);
+        if (dtype == SEG_BF16)
+            hipLaunchKernelGGL(pack_transpose_k<bf16>, grid, dim3(256), 0, st, src, (bf16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else if (dtype == SEG_F32)
+            hipLaunchKernelGGL(pack_transpose_k<float>, grid, dim3(256), 0, st, src, (float*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else
+            return SEG_EINVAL;
+    } else {
+        const long total = (long)RS * a_pad * (b_pad / 8);
+        const int grid = seg_grid_1d(total, 256);
+        if (dtype == SEG_BF16)
+            hipLaunchKernelGGL(pack_rows_k<bf16>, dim3(grid), dim3(256), 0, st, src, (bf16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else if (dtype == SEG_F32)
+            hipLaunchKernelGGL(pack_rows_k<float>, dim3(grid), dim3(256), 0, st, src, (float*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else
+            return SEG_EINVAL;
+    }
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

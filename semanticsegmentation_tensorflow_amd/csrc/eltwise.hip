@@ -93,13 +93,19 @@ __global__ __launch_bounds__(256) void bias_relu_bwd_k(const T* __restrict__ dy,
     }
 }
 
-__global__ void reduce_rows_k(const float* __restrict__ part, int nrows, int K, int k_valid, float* __restrict__ out,
-                              int ncols_out_stride) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= k_valid) return;
-    float s = 0.f;
-    for (int r = 0; r < nrows; ++r) s += part[(long)r * K + k];
-    out[k] = s;
+// Column sums of a [nrows][K] fp32 partial matrix: 64 channels per workgroup,
+// four row groups per channel, coalesced 256-byte row segments.
+__global__ __launch_bounds__(256) void reduce_rows_k(const float* __restrict__ part, int nrows, int K, int k_valid,
+                                                     float* __restrict__ out) {
+    __shared__ float s[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int rg = threadIdx.x >> 6;
+    float acc = 0.f;
+    if (c < k_valid)
+        for (int r = rg; r < nrows; r += 4) acc += part[(long)r * K + c];
+    s[rg][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (rg == 0 && c < k_valid) out[c] = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -617,7 +623,7 @@ extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int l
                                          (const T*)y, ld_y, (T*)dz, ld_dz, part, P, K, relu, scale));
     SEG_CHECK_LAUNCH();
     if (dbias) {
-        hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 255) / 256), dim3(256), 0, s, part, nb, K, k_valid, dbias, 0);
+        hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 63) / 64), dim3(256), 0, s, part, nb, K, k_valid, dbias);
         SEG_CHECK_LAUNCH();
     }
     return SEG_OK;
