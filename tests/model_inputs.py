@@ -1,0 +1,50 @@
+"""Deterministic model inputs shared by the golden-vector script and the tests."""
+import math
+
+import numpy as np
+
+from semanticsegmentation_tensorflow_amd import graph as G
+from semanticsegmentation_tensorflow_amd.variables import init_value
+
+
+def he_weights(shapes, seed):
+    """He-scaled init so activations are O(1) (the reference N(0,0.01) init
+    makes them vanish)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, s in shapes.items():
+        if len(s) == 4:
+            R, S_, A, B = s
+            fan = R * S_ * (A if "conv_t" not in name else B)
+            out[name] = (rng.standard_normal(s) * math.sqrt(2.0 / fan)).astype(np.float32)
+            if "conv_t" in name:      # transposed conv: fan-in ~ in_ch * (k/stride)^2
+                out[name] *= np.float32(R / (4.0 if R == 4 else 16.0))
+        else:
+            out[name] = (0.05 * rng.standard_normal(s)).astype(np.float32)
+    # the reference feeds raw 0..255 pixels (FCN.py:395): scale the first layer
+    # so activations / logits stay O(1) and the softmax is not saturated
+    first = [k for k in shapes if len(shapes[k]) == 4][0]
+    out[first] /= np.float32(128.0)
+    return out
+
+
+def reference_init_weights(shapes, seed=0):
+    """The reference's init (N(0, 0.01) weights, zero biases; FCN.py:125-127)
+    drawn by the product's counter-based generator (variables.init_value)."""
+    out = {}
+    for name, s in shapes.items():
+        ini = (G.random_normal_initializer(0.0, 0.01) if len(s) == 4 else G.constant_initializer(0.0))
+        v = G.Variable.__new__(G.Variable)
+        v.var_name, v.shape, v.initializer = name, tuple(s), ini
+        out[name] = init_value(v, seed)
+    return out
+
+
+def synthetic_batch(N, H, W, seed):
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 256, size=(N, H, W, 3)).astype(np.float32)
+    lab = np.zeros((N, H, W), dtype=np.uint8)
+    lab[:, H // 2:, W // 4: 3 * W // 4] = 1
+    flip = rng.random((N, H, W)) < 0.05
+    lab = np.where(flip, 1 - lab, lab).astype(np.uint8)
+    return img, lab

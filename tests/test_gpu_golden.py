@@ -1,0 +1,110 @@
+"""HIP path vs the committed golden vectors (tests/golden/*.npz, made by
+tests/golden/make_golden.py from the CPU oracle).  fp32 compute path.
+
+Tolerances: op outputs 2e-5 relative to max |ref|; FCN logits 1e-4, loss
+1e-5 relative; gradient L2 norms 1e-4 and gradient slices 2e-3 (of max |ref|
+of the slice); one TF1 Adam step within 5e-5 of the step size lr (+1e-6 of |param|)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import models as M
+from semanticsegmentation_tensorflow_amd import ops, tf
+from tests.golden import make_golden as MG
+from tests.gpu_utils import from_dev, to_dev
+from tests.model_inputs import he_weights, synthetic_batch
+from tests.test_gpu_fcn import build_fcn
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    return np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+@pytest.mark.parametrize("which", ["ref", "he"])
+def test_fcn_matches_golden(dev, which):
+    gold = np.load(os.path.join(GOLD, f"fcn_{which}_init.npz"))
+    image, labels, keep, pred, logits, loss, train_step = build_fcn(MG.H, MG.W)
+    sess = tf.Session(compute_dtype="f32", seed=0)
+    sess.run(tf.global_variables_initializer())     # reference init, counter-based seed 0
+    if which == "he":
+        for k, v in he_weights(M.fcn_param_shapes(3, 2), 1).items():
+            sess.assign(k, v)
+    img, lab = synthetic_batch(MG.N, MG.H, MG.W, 2)
+    p_, lg, ls, _ = sess.run([pred, logits, loss, train_step], feed_dict={image: img, labels: lab, keep: 1.0})
+    assert rel(lg, gold["logits"]) < 1e-4
+    assert abs(float(ls) - float(gold["loss"])) <= 1e-5 * abs(float(gold["loss"]))
+    for k in M.fcn_param_shapes(3, 2):
+        g = sess.store.grad(k).cpu().numpy().reshape(-1)
+        gn = float(gold[f"gnorm/{k}"])
+        assert abs(np.linalg.norm(g) - gn) <= 1e-4 * gn, k
+        assert rel(g[:MG.SLICE], gold[f"gslice/{k}"]) < 2e-3, k
+        upd = sess.variable_value(k).reshape(-1)[:MG.SLICE]
+        ref = gold[f"adam1/{k}"]
+        # the step is <= lr (1e-4); its sensitivity to g is O(1) when |g| ~ eps-scale,
+        # so bound it relative to lr: 5e-5 of the step size
+        assert np.abs(upd - ref).max() <= 5e-9 + 1e-6 * np.abs(ref).max(), k
+
+
+def test_ops_match_golden(dev):
+    o = np.load(os.path.join(GOLD, "ops.npz"))
+    f32 = torch.float32
+
+    def conv(xk, wk, stride):
+        x, w = torch.from_numpy(o[xk]), torch.from_numpy(o[wk])
+        N, H, W_, C = x.shape
+        R, S, _, K = w.shape
+        d = ops.conv_desc(N, H, W_, C, K, R, S, stride, 1, "SAME", ops.F32)
+        wk_ = torch.empty(ops.packed_shape(R, S, C, K, ops.PACK_KRSC), device=dev)
+        ops.pack_filter(w.float().to(dev).contiguous(), wk_, ops.round8(C), ops.round8(K), ops.PACK_KRSC)
+        y = torch.empty(N, d.OH, d.OW, d.K, device=dev)
+        ops.conv2d_fwd(d, to_dev(x, f32, dev), wk_, y)
+        return from_dev(y, K).numpy()
+
+    assert rel(conv("conv_even_x", "conv_even_w", 1), o["conv_even_y"]) < 2e-5
+    assert rel(conv("conv_even_x", "conv_even_w", 2), o["conv_s2_y"]) < 2e-5
+
+    def tconv(xk, wk, out_hw, s, ref):
+        x, w = torch.from_numpy(o[xk]), torch.from_numpy(o[wk])
+        N, H, W_, C = x.shape
+        R, S, K, _ = w.shape
+        d = ops.tconv_desc(N, H, W_, C, out_hw[0], out_hw[1], K, R, S, s, "SAME", ops.F32)
+        wp = torch.empty(ops.packed_shape(R, S, K, C, ops.PACK_TCONV_FWD), device=dev)
+        ops.pack_filter(w.float().to(dev).contiguous(), wp, ops.round8(K), ops.round8(C), ops.PACK_TCONV_FWD)
+        y = torch.empty(N, out_hw[0], out_hw[1], d.K, device=dev)
+        ops.tconv2d_fwd(d, to_dev(x, f32, dev), wp, y)
+        assert rel(from_dev(y, K).numpy(), o[ref]) < 2e-5, ref
+
+    tconv("tconv_x", "tconv_w", (6, 8), 2, "tconv_y")
+    tconv("tconv_x", "tconv_w", (5, 7), 2, "tconv_odd_y")
+    tconv("tconv8_x", "tconv8_w", (16, 24), 8, "tconv8_y")
+
+    xp = to_dev(torch.from_numpy(o["pool_x"]), f32, dev)
+    yp = torch.empty(2, 2, 3, 8, device=dev)
+    ops.maxpool2x2_fwd(xp, yp)
+    dx = torch.empty_like(xp)
+    ops.maxpool2x2_bwd(xp, yp, to_dev(torch.from_numpy(o["pool_dy"]), f32, dev), dx)
+    assert np.array_equal(from_dev(yp, 3).numpy(), o["pool_y"].astype(np.float32))
+    assert np.array_equal(from_dev(dx, 3).numpy(), o["pool_dx"].astype(np.float32))
+
+    z = to_dev(torch.from_numpy(o["xent_z"]), f32, dev)
+    dz = torch.empty_like(z)
+    ls = torch.zeros(1, device=dev)
+    ops.softmax_xent(z, torch.from_numpy(o["xent_lab"]).to(torch.uint8).to(dev), dz, ls, 2, grad_scale=1 / 20)
+    assert abs(ls.item() / 20 - float(o["xent_loss"])) < 1e-6
+    assert rel(from_dev(dz, 2).numpy(), o["xent_dz"]) < 1e-5
+
+    p = torch.from_numpy(o["adam_p0"]).float().to(dev)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    for t in range(3):
+        ops.adam_tf1_step(p, torch.from_numpy(o["adam_g"][t]).float().to(dev), m, v, 1e-3, t + 1)
+    assert rel(p.cpu().numpy(), o["adam_p3"]) < 1e-6
+
+    xb = torch.from_numpy(o["bilinear_x"]).float().to(dev).contiguous()
+    yb = torch.empty(1, 5, 7, 2, device=dev)
+    ops.resize_bilinear_fwd(xb, yb)
+    assert rel(yb.cpu().numpy(), o["bilinear_y"]) < 1e-6
