@@ -93,19 +93,23 @@ __global__ __launch_bounds__(256) void bias_relu_bwd_k(const T* __restrict__ dy,
     }
 }
 
-// Column sums of a [nrows][K] fp32 partial matrix: 64 channels per workgroup,
-// four row groups per channel, coalesced 256-byte row segments.
+// Column sums of a [nrows][K] fp32 partial matrix: 8 channels x 32 row groups
+// per workgroup, so even K = 64 spreads 1024 rows over 2048 threads.
 __global__ __launch_bounds__(256) void reduce_rows_k(const float* __restrict__ part, int nrows, int K, int k_valid,
                                                      float* __restrict__ out) {
-    __shared__ float s[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int rg = threadIdx.x >> 6;
+    __shared__ float s[32][9];
+    const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    const int c = blockIdx.x * 8 + cl;
     float acc = 0.f;
     if (c < k_valid)
-        for (int r = rg; r < nrows; r += 4) acc += part[(long)r * K + c];
-    s[rg][threadIdx.x & 63] = acc;
+        for (int r = rg; r < nrows; r += 32) acc += part[(long)r * K + c];
+    s[rg][cl] = acc;
     __syncthreads();
-    if (rg == 0 && c < k_valid) out[c] = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
+    if (threadIdx.x < 8 && c < k_valid) {
+        float t = 0.f;
+        for (int r = 0; r < 32; ++r) t += s[r][cl];
+        out[c] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -623,7 +627,7 @@ extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int l
                                          (const T*)y, ld_y, (T*)dz, ld_dz, part, P, K, relu, scale));
     SEG_CHECK_LAUNCH();
     if (dbias) {
-        hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 63) / 64), dim3(256), 0, s, part, nb, K, k_valid, dbias);
+        hipLaunchKernelGGL(reduce_rows_k, dim3((k_valid + 7) / 8), dim3(256), 0, s, part, nb, K, k_valid, dbias);
         SEG_CHECK_LAUNCH();
     }
     return SEG_OK;
