@@ -120,6 +120,10 @@ size_t seg_conv_workspace(const seg_conv_desc* d, int op);
 int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, int len, int* splits,
                          double* flops);
 
+/* Tuning knobs (host-only): "igemm_nt_variant" = 1 (register-staged
+ * 128-row tiles) or 2 (LDS-DMA 3-stage ring, 256-row tiles; default). */
+int seg_set_option(const char* name, int value);
+
 /* ---- filter packing: fp32 master -> compute copy ----------------------- */
 /* src: fp32 master [R][S][A][B] with A=a_valid, B=b_valid; dst (dtype,
  * channel dims padded to a_pad/b_pad with zeros):

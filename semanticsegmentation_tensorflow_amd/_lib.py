@@ -18,7 +18,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "conv.hip", "eltwise.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "conv.hip", "eltwise.hip"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
@@ -99,6 +99,7 @@ SIGNATURES = {
     "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
     "seg_conv_workspace": (_Z, [_DP, _I]),
+    "seg_set_option": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
                                   ctypes.POINTER(ctypes.c_double)]),
     "seg_pack_filter": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

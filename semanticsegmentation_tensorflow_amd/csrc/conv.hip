@@ -4,6 +4,7 @@
 #include "common.h"
 #include "igemm.h"
 #include <stdio.h>
+#include <string.h>
 
 using seg::NTParams;
 using seg::TNParams;
@@ -206,10 +207,21 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 5: { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_t; break; }
         default: return SEG_EINVAL;
     }
+    if (bm == 256 && fam[6] == 'n') fam = "igemm_nt2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
     if (splits) *splits = sp;
     if (flops) *flops = 2.0 * macs;
     return SEG_OK;
+}
+
+extern "C" int seg_set_option(const char* name, int value) {
+    if (!name) return SEG_EINVAL;
+    if (!strcmp(name, "igemm_nt_variant")) {
+        if (value != 1 && value != 2) return SEG_EINVAL;
+        seg::g_nt_variant = value;
+        return SEG_OK;
+    }
+    return SEG_EINVAL;
 }
 
 extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,

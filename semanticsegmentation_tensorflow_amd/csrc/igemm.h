@@ -67,5 +67,7 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase);
 size_t tn_workspace(int M, int N, int P, int dtype);
 void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits);
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
+void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
+extern int g_nt_variant;
 
 }  // namespace seg

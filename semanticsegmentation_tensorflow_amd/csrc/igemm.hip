@@ -35,35 +35,35 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 
-// NT epilogue for one element; used by the GEMM and by the split-K reducer.
-template <typename T>
-__device__ __forceinline__ void nt_store(const NTParams& p, int row, int col, float v, int Ha,
-                                         int Wa, int ooh, int oow) {
+// NT epilogue, split into a per-row part (one pixel decomposition) and a
+// per-element part; used by the v1 GEMM and by the split-K reducer.
+struct NtRow {
+    long yoff, roff;
+    uint64_t gidx;   // dropout counter base: (img*OH*OW + pix) * n_valid
+};
+
+__device__ __forceinline__ NtRow nt_row(const NTParams& p, int row, int Ha, int Wa, int ooh, int oow) {
     const int hw = Ha * Wa;
     const int img = row / hw;
     const int rem = row - img * hw;
     const int a = rem / Wa;
     const int b = rem - a * Wa;
-    const int oh = a * p.osh + ooh;
-    const int ow = b * p.osw + oow;
-    const long pix = (long)oh * p.OW + ow;
-    const EpiParams& e = p.epi;
-    if (col >= e.n_valid) {
-        v = 0.f;
-    } else {
-        if (e.scale) v *= e.scale[col];
-        if (e.shift) v += e.shift[col];
-        if (e.bias) v += e.bias[col];
-        if (e.relu) v = fmaxf(v, 0.f);
-        if (e.keep_prob < 1.f) {
-            const uint64_t idx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid + col;
-            const float u = seg_uniform(e.seed, idx);
-            v = (v / e.keep_prob) * floorf(e.keep_prob + u);
-        }
-        if (e.residual)
-            v += to_f32(reinterpret_cast<const T*>(e.residual)[img * e.res_img + pix * e.ld_res + col]);
-    }
-    reinterpret_cast<T*>(p.y)[img * p.y_img + pix * p.ldy + col] = from_f32<T>(v);
+    const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
+    NtRow r;
+    r.yoff = img * p.y_img + pix * p.ldy;
+    r.roff = img * p.epi.res_img + pix * p.epi.ld_res;
+    r.gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * p.epi.n_valid;
+    return r;
+}
+
+__device__ __forceinline__ float nt_apply(const EpiParams& e, const NtRow& r, int col, float v, float res) {
+    if (col >= e.n_valid) return 0.f;
+    if (e.scale) v *= e.scale[col];
+    if (e.shift) v += e.shift[col];
+    if (e.bias) v += e.bias[col];
+    if (e.relu) v = fmaxf(v, 0.f);
+    if (e.keep_prob < 1.f) v = (v / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, r.gidx + col));
+    return v + res;
 }
 
 // ---------------------------------------------------------------------------
@@ -261,27 +261,58 @@ __global__ __launch_bounds__(256) void igemm_nt(NTParams p) {
         for (int r = 0; r < 4; ++r) {
             const int row = m0 + wm * WTM + mi * 16 + fg * 4 + r;
             if (row >= M) continue;
+            if (p.partial) {
+                float* prow = p.partial + ((long)blockIdx.z * M + row) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col = n0 + wn * WTN + ni * 16 + fr;
+                    if (col < p.N) prow[col] = acc[mi][ni][r];
+                }
+                continue;
+            }
+            const NtRow rw = nt_row(p, row, Ha, Wa, ooh, oow);
+            T* yrow = reinterpret_cast<T*>(p.y) + rw.yoff;
+            const T* rrow = reinterpret_cast<const T*>(p.epi.residual) + rw.roff;
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const int col = n0 + wn * WTN + ni * 16 + fr;
                 if (col >= p.N) continue;
-                const float v = acc[mi][ni][r];
-                if (p.partial)
-                    p.partial[((long)blockIdx.z * M + row) * p.N + col] = v;
-                else
-                    nt_store<T>(p, row, col, v, Ha, Wa, ooh, oow);
+                const float res = p.epi.residual ? to_f32(rrow[col]) : 0.f;
+                yrow[col] = from_f32<T>(nt_apply(p.epi, rw, col, acc[mi][ni][r], res));
             }
         }
 }
 
+// One thread per (row, 8 columns): sum the split-K slabs, apply the epilogue
+// once per row decomposition, store 16 B (bf16) / 32 B (fp32).
 template <typename T>
 __global__ void splitk_reduce_nt(NTParams p, int splits) {
-    const long total = (long)p.M * p.N;
+    const int c8 = p.N / 8;
+    const long total = (long)p.M * c8;
+    const long slab = (long)p.M * p.N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += p.partial[(long)z * total + i];
-        const int row = (int)(i / p.N), col = (int)(i - (long)(i / p.N) * p.N);
-        nt_store<T>(p, row, col, s, p.Ha, p.Wa, p.ooh, p.oow);
+        const int row = (int)(i / c8);
+        const int col0 = (int)(i - (long)row * c8) * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float* src = p.partial + (long)row * p.N + col0;
+        for (int z = 0; z < splits; ++z) {
+            const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
+            const float4 b = *reinterpret_cast<const float4*>(src + z * slab + 4);
+            v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+            v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+        }
+        const NtRow rw = nt_row(p, row, p.Ha, p.Wa, p.ooh, p.oow);
+        float res[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (p.epi.residual) {
+            const T* rp = reinterpret_cast<const T*>(p.epi.residual) + rw.roff + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), res + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = nt_apply(p.epi, rw, col0 + j, v[j], res[j]);
+        T* yp = reinterpret_cast<T*>(p.y) + rw.yoff + col0;
+        *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
     }
 }
 
@@ -295,10 +326,11 @@ __device__ __forceinline__ int tn_swz(int row, int chunk) {
     else return chunk ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
 }
 
-__device__ __forceinline__ void tn_out(const TNParams& p, int m, int n, float v) {
+__device__ __forceinline__ float* tn_row(const TNParams& p, int m, bool& ok) {
     const int tap = m / p.Cg;
     const int c = m - tap * p.Cg;
-    if (c < p.c_valid && n < p.n_valid) p.out[(long)tap * p.o_tap + (long)c * p.o_c + (long)n * p.o_n] = v;
+    ok = c < p.c_valid;
+    return p.out + (long)tap * p.o_tap + (long)c * p.o_c;
 }
 
 template <typename T, int BM, int BN>
@@ -493,26 +525,46 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + wm * WTM + mi * 16 + fg * 4 + r;
             if (m >= p.M) continue;
+            if (p.partial) {
+                float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int n = n0 + wn * WTN + ni * 16 + fr;
+                    if (n < p.N) prow[n] = acc[mi][ni][r];
+                }
+                continue;
+            }
+            bool ok;
+            float* orow = tn_row(p, m, ok);
+            if (!ok) continue;
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const int n = n0 + wn * WTN + ni * 16 + fr;
-                if (n >= p.N) continue;
-                const float v = acc[mi][ni][r];
-                if (p.partial)
-                    p.partial[((long)blockIdx.z * p.M + m) * p.N + n] = v;
-                else
-                    tn_out(p, m, n, v);
+                if (n < p.n_valid) orow[(long)n * p.o_n] = acc[mi][ni][r];
             }
         }
 }
 
 __global__ void splitk_reduce_tn(TNParams p, int splits) {
-    const long total = (long)p.M * p.N;
+    const int c4 = p.N / 4;
+    const long total = (long)p.M * c4;
+    const long slab = (long)p.M * p.N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += p.partial[(long)z * total + i];
-        const int m = (int)(i / p.N), n = (int)(i - (long)(i / p.N) * p.N);
-        tn_out(p, m, n, s);
+        const int m = (int)(i / c4);
+        const int n0 = (int)(i - (long)m * c4) * 4;
+        float4 s = {0.f, 0.f, 0.f, 0.f};
+        const float* src = p.partial + (long)m * p.N + n0;
+        for (int z = 0; z < splits; ++z) {
+            const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
+            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        }
+        bool ok;
+        float* orow = tn_row(p, m, ok);
+        if (!ok) continue;
+        const float vv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (n0 + j < p.n_valid) orow[(long)(n0 + j) * p.o_n] = vv[j];
     }
 }
 
@@ -531,11 +583,15 @@ static int num_cus() {
     return cus;
 }
 
+// Kernel generation for the NT GEMMs (1 = register-staged 128-row tiles,
+// 2 = LDS-DMA 3-stage ring, 256-row tiles).  Runtime-selectable for tests.
+int g_nt_variant = 2;
+
 // Tile / split selection: fill >= ~2 workgroups per CU; split K only when the
 // (M,N) tiling cannot, and keep >= 8 k tiles per split.
 static void choose_nt(int M, int N, int K, int bk, int& bm, int& bn, int& splits) {
     bn = N <= 64 ? 64 : 128;
-    bm = 128;
+    bm = g_nt_variant == 2 ? 256 : 128;
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const int target = 2 * num_cus();
     const int kt = (K + bk - 1) / bk;
@@ -551,6 +607,8 @@ void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* s
     choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, *bm, *bn, *splits);
     if (phase) *splits = 1;
 }
+
+int nt_variant() { return g_nt_variant; }
 
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 
@@ -584,11 +642,12 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
+    if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
+    else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
     SEG_CHECK_LAUNCH();
     if (p.partial) {
-        const long total = (long)p.M * p.N;
+        const long total = (long)p.M * (p.N / 8);
         hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
         SEG_CHECK_LAUNCH();
         p.partial = nullptr;
@@ -654,7 +713,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     else launch_tn_t<T, 128, 128>(p, gridz, s);
     SEG_CHECK_LAUNCH();
     if (p.partial) {
-        const long total = (long)p.M * p.N;
+        const long total = (long)p.M * (p.N / 4);
         hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
         SEG_CHECK_LAUNCH();
         p.partial = nullptr;

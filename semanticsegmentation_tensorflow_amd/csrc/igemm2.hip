@@ -1,0 +1,330 @@
+// Second-generation implicit-GEMM NT kernel for gfx950.
+//
+// Same contract as igemm_nt (igemm.hip) but staged the CDNA4 way:
+//  * operands go HBM/L2 -> LDS by LDS-DMA (`global_load_lds_dwordx4`, one
+//    1 KiB wave-instruction = 8 rows x 128 B), issued from inline asm so
+//    hipcc does not drain the DMA queue before every ds_read;
+//  * the implicit-GEMM gather lives in the per-lane SOURCE address; zero
+//    padding / tails point the lane at a zero page; the LDS XOR swizzle is
+//    applied on the source side (LDS image stays lane-linear);
+//  * a 3-deep LDS ring: tile t+2 is in flight while tile t is consumed; one
+//    counted `s_waitcnt vmcnt(N)` + raw `s_barrier` per K tile;
+//  * 8 waves (4 x 2), 64x64 (or 64x32) per wave on v_mfma_f32_16x16x32_bf16.
+#include "common.h"
+#include "igemm.h"
+
+namespace seg {
+
+__device__ uint4 g_zero_page[4];
+
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
+    const int xcd = bid & 7;
+    const int q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (bid >> 3);
+}
+
+template <typename T>
+[[maybe_unused]] __device__ __forceinline__ void nt2_store(const NTParams& p, int row, int col, float v, int Ha, int Wa, int ooh,
+                                          int oow) {
+    const int hw = Ha * Wa;
+    const int img = row / hw;
+    const int rem = row - img * hw;
+    const int a = rem / Wa;
+    const int b = rem - a * Wa;
+    const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
+    const EpiParams& e = p.epi;
+    if (col >= e.n_valid) {
+        v = 0.f;
+    } else {
+        if (e.scale) v *= e.scale[col];
+        if (e.shift) v += e.shift[col];
+        if (e.bias) v += e.bias[col];
+        if (e.relu) v = fmaxf(v, 0.f);
+        if (e.keep_prob < 1.f) {
+            const uint64_t idx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid + col;
+            v = (v / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, idx));
+        }
+        if (e.residual)
+            v += to_f32(reinterpret_cast<const T*>(e.residual)[img * e.res_img + pix * e.ld_res + col]);
+    }
+    reinterpret_cast<T*>(p.y)[img * p.y_img + pix * p.ldy + col] = from_f32<T>(v);
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
+    constexpr int NW = WM * WN;
+    constexpr int EPC = dt_traits<T>::EPC;
+    constexpr int BK = 128 / sizeof(T);
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int A_INS = BM / 8 / NW, B_INS = BN / 8 / NW;
+    static_assert(A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+    static_assert(NW % 2 == 0, "swizzle assumes an even wave count");
+    constexpr int NI = A_INS + B_INS;
+    constexpr int STAGE = (BM + BN) * 128;
+    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+
+    int Ha = p.Ha, Wa = p.Wa, ioh = p.ioh, iow = p.iow, ooh = p.ooh, oow = p.oow;
+    int rb = p.rb, sb = p.sb, M = p.M;
+    if (p.phase) {
+        const int ph = blockIdx.z / p.st_w, pw = blockIdx.z - (blockIdx.z / p.st_w) * p.st_w;
+        const int oh0 = ((ph - p.pad_t) % p.st_h + p.st_h) % p.st_h;
+        const int ow0 = ((pw - p.pad_l) % p.st_w + p.st_w) % p.st_w;
+        Ha = (p.OH - oh0 + p.st_h - 1) / p.st_h;
+        Wa = (p.OW - ow0 + p.st_w - 1) / p.st_w;
+        ooh = oh0;
+        oow = ow0;
+        ioh = (oh0 + p.pad_t - ph) / p.st_h;
+        iow = (ow0 + p.pad_l - pw) / p.st_w;
+        rb = ph;
+        sb = pw;
+        M = p.Nimg * Ha * Wa;
+        if (M <= 0) return;
+    }
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int tiles_m = (M + BM - 1) / BM;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int tm = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
+    if (tm >= tiles_m) return;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int KT = (p.K + BK - 1) / BK;
+    int kt_begin = 0, kt_end = KT;
+    if (p.partial) {
+        kt_begin = blockIdx.z * p.kt_per_split;
+        kt_end = min(KT, kt_begin + p.kt_per_split);
+    }
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const int lr = lane >> 3;
+    // global k-chunk this lane stages: physical chunk (lane & 7) of its row,
+    // pre-swizzled; the swizzle of row (i*NW + w)*8 + lr is i-independent.
+    const int c = (lane & 7) ^ ((((w & 1) << 2) + (lr >> 1)) & 7);
+
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const void* zero = (const void*)g_zero_page;
+
+    long a_off[A_INS];
+    int a_ih[A_INS], a_iw[A_INS];
+    bool a_ok[A_INS];
+    const int hw = Ha * Wa;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+        const int m = m0 + (i * NW + w) * 8 + lr;
+        a_ok[i] = m < M;
+        const int mm = a_ok[i] ? m : 0;
+        const int img = mm / hw;
+        const int rem = mm - img * hw;
+        const int a = rem / Wa;
+        const int b = rem - a * Wa;
+        a_off[i] = (long)img * p.x_img;
+        a_ih[i] = a * p.ish + ioh;
+        a_iw[i] = b * p.isw + iow;
+    }
+    long b_off[B_INS];
+    bool b_ok[B_INS];
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+        const int n = n0 + (i * NW + w) * 8 + lr;
+        b_ok[i] = n < p.N;
+        b_off[i] = (long)(b_ok[i] ? n : 0) * p.w_col;
+    }
+    int kg = kt_begin * BK + c * EPC;
+    int tap = kg / p.C;
+    int cc = kg - tap * p.C;
+    int tj = tap / p.taps_w;
+    int ti = tap - tj * p.taps_w;
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+
+    auto load_stage = [&](int stage) {
+        const unsigned sb_ = lds0 + stage * STAGE;
+        const bool kok = kg < p.K;
+        const int dh = tj * p.tsh, dw = ti * p.tsw;
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i) {
+            const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+            const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+            const void* src = ok ? (const void*)(X + a_off[i] + ((long)ih * p.IW + iw) * p.ldx + cc) : zero;
+            glds16(src, sb_ + (i * NW + w) * 1024);
+        }
+        const long wtap = (long)((rb + p.rstep * tj) * p.Sfull + (sb + p.sstep * ti)) * p.w_tap + cc;
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const bool ok = b_ok[i] && kok;
+            const void* src = ok ? (const void*)(Wt + b_off[i] + wtap) : zero;
+            glds16(src, sb_ + BM * 128 + (i * NW + w) * 1024);
+        }
+        kg += BK;
+        cc += BK;
+        while (cc >= p.C) {
+            cc -= p.C;
+            if (++ti == p.taps_w) { ti = 0; ++tj; }
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (kt_begin < kt_end) load_stage(0);
+    if (kt_begin + 1 < kt_end) load_stage(1);
+
+    const int fr = lane & 15, fg = lane >> 4;
+    int stage = 0;
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+        if (kt + 1 < kt_end) wait_vmcnt<NI>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (kt + 2 < kt_end) load_stage(stage == 0 ? 2 : stage - 1);
+        const char* As = smem + stage * STAGE;
+        const char* Bs = As + BM * 128;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            uint4 af[TM], bfr[TN];
+            const int chunk = ks * 4 + fg;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int row = wm * WTM + mi * 16 + fr;
+                af[mi] = *reinterpret_cast<const uint4*>(As + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int row = wn * WTN + ni * 16 + fr;
+                bfr[ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    if constexpr (sizeof(T) == 2) {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]), acc[mi][ni], 0,
+                            0, 0);
+                    } else {
+                        const f32x4 a4 = __builtin_bit_cast(f32x4, af[mi]);
+                        const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[ni]);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t], b4[t], acc[mi][ni], 0, 0, 0);
+                    }
+                }
+        }
+        stage = stage == 2 ? 0 : stage + 1;
+    }
+
+    if (p.partial) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + wm * WTM + mi * 16 + fg * 4 + r;
+                if (row >= M) continue;
+                float* prow = p.partial + ((long)blockIdx.z * M + row) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col = n0 + wn * WTN + ni * 16 + fr;
+                    if (col < p.N) prow[col] = acc[mi][ni][r];
+                }
+            }
+        return;
+    }
+    // ---- epilogue: stage the wave's fp32 tile in LDS, then each lane
+    // finishes 8 consecutive columns of a row (one pixel decomposition per
+    // row, 16-byte bf16 / 32-byte fp32 stores).
+    constexpr int SROW = WTN * 4 + 16;               // padded fp32 row (bytes)
+    static_assert(NW * WTM * SROW <= 3 * STAGE, "epilogue staging must fit the ring");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    char* wbuf = smem + w * WTM * SROW;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) = acc[mi][ni][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own wave's rows only
+    constexpr int CPR = WTN / 8;                      // 8-column chunks per row
+    constexpr int RPP = 64 / CPR;                     // rows per pass of the wave
+    const int cch = lane % CPR, rsub = lane / CPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
+    const EpiParams& e = p.epi;
+    float bias[8], scl[8], shf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        const bool cv = col < e.n_valid;
+        bias[j] = (e.bias && cv) ? e.bias[col] : 0.f;
+        scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
+        shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
+    }
+    const int hw2 = Ha * Wa;
+#pragma unroll 2
+    for (int rr = rsub; rr < WTM; rr += RPP) {
+        const int row = m0 + wm * WTM + rr;
+        if (row >= M || col0 >= p.N) continue;
+        const int img = row / hw2;
+        const int rem = row - img * hw2;
+        const int a = rem / Wa;
+        const int b = rem - a * Wa;
+        const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
+        const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
+        const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        float res[8];
+        if (e.residual) {
+            const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), res + 4);
+        }
+        const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = col0 + j;
+            float x = v[j] * scl[j] + shf[j] + bias[j];
+            if (e.relu) x = fmaxf(x, 0.f);
+            if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+            if (e.residual) x += res[j];
+            v[j] = col < e.n_valid ? x : 0.f;
+        }
+        T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
+        *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
+    }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
+    const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), dim3(tiles, 1, gridz), dim3(WM * WN * 64), 0, s, p);
+}
+
+void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s) {
+    if (dtype == SEG_BF16) {
+        if (bn == 64) launch_nt2_t<bf16, 256, 64, 4, 2>(p, gridz, max_m, s);
+        else launch_nt2_t<bf16, 256, 128, 4, 2>(p, gridz, max_m, s);
+    } else {
+        if (bn == 64) launch_nt2_t<float, 256, 64, 4, 2>(p, gridz, max_m, s);
+        else launch_nt2_t<float, 256, 128, 4, 2>(p, gridz, max_m, s);
+    }
+}
+
+}  // namespace seg

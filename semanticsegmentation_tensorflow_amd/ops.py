@@ -114,6 +114,10 @@ def conv_kernel_info(desc, op):
     return buf.value.decode(), sp.value, fl.value
 
 
+def set_option(name: str, value: int):
+    check(_lib.lib().seg_set_option(name.encode(), int(value)), f"set_option({name})")
+
+
 def conv_workspace(desc, op):
     return int(_lib.lib().seg_conv_workspace(ctypes.byref(desc), op))
 

@@ -15,6 +15,16 @@ from semanticsegmentation_tensorflow_amd import ops
 from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[1, 2], ids=["nt1", "nt2"])
+def ntv(request, dev):
+    """Run NT-GEMM tests on both kernel generations."""
+    ops.set_option("igemm_nt_variant", request.param)
+    yield request.param
+    ops.set_option("igemm_nt_variant", 2)
+
+
 DTYPES = [torch.float32, torch.bfloat16]
 DT = {torch.float32: ops.F32, torch.bfloat16: ops.BF16}
 
@@ -51,7 +61,7 @@ def _pack(w64, mode, dtype, dev):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_fwd_bias_relu(dev, case, dtype):
+def test_conv2d_fwd_bias_relu(dev, ntv, case, dtype):
     N, H, W, C, K, R, S, st, dil, pad = case
     x, w, b = _conv_case(case, 1)
     xr, wr = rnd(x, dtype), rnd(w, dtype)
@@ -70,7 +80,7 @@ def test_conv2d_fwd_bias_relu(dev, case, dtype):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[7] == 1])
-def test_conv2d_bwd_data(dev, case, dtype):
+def test_conv2d_bwd_data(dev, ntv, case, dtype):
     N, H, W, C, K, R, S, st, dil, pad = case
     x, w, _ = _conv_case(case, 2)
     wr = rnd(w, dtype)
@@ -128,7 +138,7 @@ def _tconv_case(case, seed):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", TCONV_CASES)
-def test_tconv2d_fwd_bias_residual(dev, case, dtype):
+def test_tconv2d_fwd_bias_residual(dev, ntv, case, dtype):
     N, IH, IW, Ci, OH, OW, Co, k, s = case
     x, w, b = _tconv_case(case, 4)
     g = torch.Generator().manual_seed(5)
@@ -145,7 +155,7 @@ def test_tconv2d_fwd_bias_residual(dev, case, dtype):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", TCONV_CASES)
-def test_tconv2d_grads(dev, case, dtype):
+def test_tconv2d_grads(dev, ntv, case, dtype):
     N, IH, IW, Ci, OH, OW, Co, k, s = case
     x, w, _ = _tconv_case(case, 6)
     xr = rnd(x, dtype).requires_grad_(True)
