@@ -120,8 +120,9 @@ size_t seg_conv_workspace(const seg_conv_desc* d, int op);
 int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, int len, int* splits,
                          double* flops);
 
-/* Tuning knobs (host-only): "igemm_nt_variant" = 1 (register-staged
- * 128-row tiles) or 2 (LDS-DMA 3-stage ring, 256-row tiles; default). */
+/* Tuning knobs (host-only): "igemm_nt_variant" / "igemm_tn_variant" = 1
+ * (register-staged 128-row tiles) or 2 (LDS-DMA 3-stage ring, 256-wide
+ * tiles, 8 waves; default). */
 int seg_set_option(const char* name, int value);
 
 /* ---- filter packing: fp32 master -> compute copy ----------------------- */

@@ -208,6 +208,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         default: return SEG_EINVAL;
     }
     if (bm == 256 && fam[6] == 'n') fam = "igemm_nt2";
+    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[6] == 't' && (op == 2 ? d->R * d->S * d->C : d->R * d->S * d->K) >= 128)
+        fam = "igemm_tn2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
     if (splits) *splits = sp;
     if (flops) *flops = 2.0 * macs;
@@ -219,6 +221,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "igemm_nt_variant")) {
         if (value != 1 && value != 2) return SEG_EINVAL;
         seg::g_nt_variant = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "igemm_tn_variant")) {
+        if (value != 1 && value != 2) return SEG_EINVAL;
+        seg::g_tn_variant = value;
         return SEG_OK;
     }
     return SEG_EINVAL;

@@ -69,5 +69,7 @@ void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* s
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
 extern int g_nt_variant;
+extern int g_tn_variant;
+void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s);
 
 }  // namespace seg

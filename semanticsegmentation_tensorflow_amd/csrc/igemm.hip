@@ -661,9 +661,23 @@ int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t w
     return SEG_EINVAL;
 }
 
+int g_tn_variant = 2;
+
 static void choose_tn(int M, int N, int P, int bkp, int& bm, int& bn, int& splits) {
-    bm = M <= 64 ? 64 : 128;
-    bn = N <= 64 ? 64 : 128;
+    if (g_tn_variant == 2 && bkp == 64 && M >= 128) {
+        // v2 tiles: minimise padded work / relative tile efficiency
+        static const int cand[5][2] = {{128, 256}, {256, 128}, {128, 128}, {256, 64}, {128, 64}};
+        static const double eff[5] = {1.0, 1.0, 0.85, 0.85, 0.8};
+        double best = 1e30;
+        for (int i = 0; i < 5; ++i) {
+            const double cost = (double)((M + cand[i][0] - 1) / cand[i][0] * cand[i][0]) *
+                                ((N + cand[i][1] - 1) / cand[i][1] * cand[i][1]) / eff[i];
+            if (cost < best * 0.999) { best = cost; bm = cand[i][0]; bn = cand[i][1]; }
+        }
+    } else {
+        bm = M <= 64 ? 64 : 128;
+        bn = N <= 64 ? 64 : 128;
+    }
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const int target = 2 * num_cus();
     const int kt = (P + bkp - 1) / bkp;
@@ -707,7 +721,9 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
+    if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
+        launch_tn2(p, bm, bn, gridz, s);
+    } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
     else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);
     else if (bn == 64) launch_tn_t<T, 128, 64>(p, gridz, s);
     else launch_tn_t<T, 128, 128>(p, gridz, s);

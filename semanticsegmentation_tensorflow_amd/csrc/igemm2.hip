@@ -311,6 +311,208 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// TN v2: filter gradients C[m][n] = sum_p A[p][m] B[p][n] with LDS-DMA staging.
+// LDS image per stage: A [64 px][BM] and B [64 px][BN] bf16 rows, 16-byte
+// chunks XOR-swizzled so the column-wise ds_read_b64_tr_b16 fragment reads
+// are conflict-free.  Grid = splits x tiles flattened so that all tiles of one
+// pixel range (split) are consecutive after the XCD remap -> they share the
+// XCD's L2 for the x / dy rows of that range.
+// ---------------------------------------------------------------------------
+template <int ROWB>
+__device__ __forceinline__ int tn2_swz(int row) {
+    // conflict-free ds_read_b64_tr_b16 images: even XOR values that stay inside
+    // the row's 16-chunk (256 B) half, or inside the row for 128 B rows
+    if constexpr (ROWB >= 256) return ((row & 3) << 1) | (((row >> 3) & 1) << 3);
+    else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m, int tiles_n, int splits) {
+    using T = bf16;
+    constexpr int NW = WM * WN;
+    constexpr int BKP = 64;
+    constexpr int AROWB = BM * 2, BROWB = BN * 2;
+    constexpr int A_RPI = 1024 / AROWB, B_RPI = 1024 / BROWB;     // rows per glds instruction
+    constexpr int A_INS = BKP / A_RPI / NW, B_INS = BKP / B_RPI / NW;
+    static_assert(A_INS * A_RPI * NW == BKP && B_INS * B_RPI * NW == BKP, "rows must split per wave");
+    constexpr int A_CPR = AROWB / 16, B_CPR = BROWB / 16;       // 16-byte chunks per row
+    constexpr int NI = A_INS + B_INS;
+    constexpr int ASZ = BKP * AROWB, STAGE = BKP * (AROWB + BROWB);
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+
+    const int ntile = tiles_m * tiles_n;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int split = wg / ntile;
+    const int tile = wg - split * ntile;
+    if (split >= splits) return;
+    const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int KT = (p.P + BKP - 1) / BKP;
+    int kt_begin = 0, kt_end = KT;
+    if (p.partial) {
+        kt_begin = split * p.kt_per_split;
+        kt_end = min(KT, kt_begin + p.kt_per_split);
+    }
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Bm = reinterpret_cast<const T*>(p.b);
+    const void* zero = (const void*)g_zero_page;
+
+    // ---- A: lane -> (row within instruction, physical chunk) -> global chunk
+    const int a_rsub = lane / A_CPR, a_pc = lane % A_CPR;
+    const int a_row0 = w * A_RPI + a_rsub;                // row of instruction 0
+    const int a_c = (a_pc & ~15) | ((a_pc & 15) ^ tn2_swz<AROWB>(a_row0));   // swizzle i-independent
+    const int am = m0 + a_c * 8;
+    const bool a_mok = am < p.M;
+    const int atap = a_mok ? am / p.Cg : 0;
+    const int ac = a_mok ? am - atap * p.Cg : 0;
+    const int atj = atap / p.taps_w, ati = atap - atj * p.taps_w;
+    const int hoff = atj * p.tsh + p.ioh, woff = ati * p.tsw + p.iow;
+    int pimg[A_INS], pa[A_INS], pb[A_INS], pp[A_INS];
+    const int hw = p.Ha * p.Wa;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+        const int pix = kt_begin * BKP + (i * NW) * A_RPI + a_row0;
+        pp[i] = pix;
+        const int q = pix < p.P ? pix : 0;
+        pimg[i] = q / hw;
+        const int rem = q - pimg[i] * hw;
+        pa[i] = rem / p.Wa;
+        pb[i] = rem - pa[i] * p.Wa;
+    }
+    // ---- B
+    const int b_rsub = lane / B_CPR, b_pc = lane % B_CPR;
+    const int b_row0 = w * B_RPI + b_rsub;
+    const int b_c = (b_pc & ~15) | ((b_pc & 15) ^ tn2_swz<BROWB>(b_row0));
+    const int bn = n0 + b_c * 8;
+    const bool b_nok = bn < p.N;
+    int bpix = kt_begin * BKP + b_row0;
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+    auto load_stage = [&](int stage) {
+        const unsigned sb_ = lds0 + stage * STAGE;
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i) {
+            const int ih = pa[i] * p.ish + hoff, iw = pb[i] * p.isw + woff;
+            const bool ok = a_mok && pp[i] < p.P && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+            const void* src = ok ? (const void*)(X + (long)pimg[i] * p.x_img + ((long)ih * p.IW + iw) * p.ldx + ac) : zero;
+            glds16(src, sb_ + (i * NW + w) * 1024);
+            pp[i] += BKP;
+            pb[i] += BKP;
+            while (pb[i] >= p.Wa) {
+                pb[i] -= p.Wa;
+                if (++pa[i] == p.Ha) { pa[i] = 0; ++pimg[i]; }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const int pix = bpix + (i * NW) * B_RPI;
+            const bool ok = b_nok && pix < p.P;
+            const void* src = ok ? (const void*)(Bm + (long)pix * p.ldb + bn) : zero;
+            glds16(src, sb_ + ASZ + (i * NW + w) * 1024);
+        }
+        bpix += BKP;
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (kt_begin < kt_end) load_stage(0);
+    if (kt_begin + 1 < kt_end) load_stage(1);
+    const int fr = lane & 15, fg = lane >> 4;
+    const int tq = (lane & 15) >> 2, tpp = lane & 3;
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    int stage = 0;
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+        if (kt + 1 < kt_end) wait_vmcnt<NI>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (kt + 2 < kt_end) load_stage(stage == 0 ? 2 : stage - 1);
+        const char* As = smem + stage * STAGE;
+        const char* Bs = As + ASZ;
+#pragma unroll
+        for (int ks = 0; ks < BKP / 32; ++ks) {
+            bf16x8 af[TM], bfr[TN];
+            const int r1 = ks * 32 + 8 * fg + tq;
+            const int s1 = tn2_swz<AROWB>(r1), s2 = tn2_swz<AROWB>(r1 + 4);
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int chk = ((wm * WTM + mi * 16) >> 3) + (tpp >> 1);
+                const int c1 = (chk & ~15) | ((chk & 15) ^ s1), c2 = (chk & ~15) | ((chk & 15) ^ s2);
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(As + r1 * AROWB + 16 * c1 + 8 * (tpp & 1)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(As + (r1 + 4) * AROWB + 16 * c2 + 8 * (tpp & 1)));
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                af[mi] = __builtin_bit_cast(bf16x8, v);
+            }
+            const int t1 = tn2_swz<BROWB>(r1), t2 = tn2_swz<BROWB>(r1 + 4);
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int chk = ((wn * WTN + ni * 16) >> 3) + (tpp >> 1);
+                const int c1 = (chk & ~15) | ((chk & 15) ^ t1), c2 = (chk & ~15) | ((chk & 15) ^ t2);
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Bs + r1 * BROWB + 16 * c1 + 8 * (tpp & 1)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Bs + (r1 + 4) * BROWB + 16 * c2 + 8 * (tpp & 1)));
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bfr[ni] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        }
+        stage = stage == 2 ? 0 : stage + 1;
+    }
+
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WTM + mi * 16 + fg * 4 + r;
+            if (m >= p.M) continue;
+            if (p.partial) {
+                float* prow = p.partial + ((long)split * p.M + m) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int n = n0 + wn * WTN + ni * 16 + fr;
+                    if (n < p.N) prow[n] = acc[mi][ni][r];
+                }
+                continue;
+            }
+            const int tap = m / p.Cg;
+            const int c = m - tap * p.Cg;
+            if (c >= p.c_valid) continue;
+            float* orow = p.out + (long)tap * p.o_tap + (long)c * p.o_c;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int n = n0 + wn * WTN + ni * 16 + fr;
+                if (n < p.n_valid) orow[(long)n * p.o_n] = acc[mi][ni][r];
+            }
+        }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_tn2_t(TNParams& p, int splits, hipStream_t s) {
+    const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
+    hipLaunchKernelGGL((igemm_tn2<BM, BN, WM, WN>), dim3(tm * tn * splits), dim3(WM * WN * 64), 0, s, p, tm, tn,
+                       splits);
+}
+
+void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s) {
+    if (bm == 256 && bn == 128) launch_tn2_t<256, 128, 4, 2>(p, splits, s);
+    else if (bm == 128 && bn == 256) launch_tn2_t<128, 256, 2, 4>(p, splits, s);
+    else if (bm == 256 && bn == 64) launch_tn2_t<256, 64, 4, 2>(p, splits, s);
+    else if (bm == 128 && bn == 64) launch_tn2_t<128, 64, 4, 2>(p, splits, s);
+    else launch_tn2_t<128, 128, 2, 4>(p, splits, s);
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);

@@ -98,9 +98,19 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype):
     assert_close(from_dev(dx, C), xr.grad, dtype, f"conv bwd_data {case}")
 
 
+@pytest.fixture(params=[1, 2], ids=["tn1", "tn2"])
+def tnv(request, dev):
+    """Run TN-GEMM (filter gradient) tests on both kernel generations."""
+    ops.set_option("igemm_tn_variant", request.param)
+    yield request.param
+    ops.set_option("igemm_tn_variant", 2)
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_bwd_filter(dev, case, dtype):
+@pytest.mark.parametrize("case", CONV_CASES + [(2, 24, 20, 64, 64, 3, 3, 1, 1, "SAME"),
+                                               (1, 16, 16, 256, 128, 3, 3, 1, 1, "SAME"),
+                                               (1, 9, 10, 128, 264, 3, 3, 1, 1, "SAME")])
+def test_conv2d_bwd_filter(dev, tnv, case, dtype):
     N, H, W, C, K, R, S, st, dil, pad = case
     x, w, _ = _conv_case(case, 3)
     xr = rnd(x, dtype)
@@ -155,7 +165,7 @@ def test_tconv2d_fwd_bias_residual(dev, ntv, case, dtype):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", TCONV_CASES)
-def test_tconv2d_grads(dev, ntv, case, dtype):
+def test_tconv2d_grads(dev, ntv, tnv, case, dtype):
     N, IH, IW, Ci, OH, OW, Co, k, s = case
     x, w, _ = _tconv_case(case, 6)
     xr = rnd(x, dtype).requires_grad_(True)

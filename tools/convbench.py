@@ -36,6 +36,7 @@ def main():
         flops = ops.conv_kernel_info(d, 0)[2]
         for v in [int(s) for s in a.variants.split(",")]:
             ops.set_option("igemm_nt_variant", v)
+            ops.set_option("igemm_tn_variant", v)
             res = []
             for op, fn in (("fwd", lambda: ops.conv2d_fwd(d, x, wk, y, ops.epilogue(relu=True), ws)),
                            ("dgrad", lambda: ops.conv2d_bwd_data(d, y, wh, dx, ws)),

@@ -16,6 +16,7 @@ _, H, W, C, K, R = L
 dev = torch.device("cuda:0")
 ws = ops.Workspace(dev)
 ops.set_option("igemm_nt_variant", var)
+ops.set_option("igemm_tn_variant", var)
 d = ops.conv_desc(N, H, W, C, K, R, R, dtype=ops.BF16)
 x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
 wk = (torch.randn(K, R, R, C, device=dev) * 0.05).to(torch.bfloat16)
