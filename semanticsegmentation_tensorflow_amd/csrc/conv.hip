@@ -174,13 +174,72 @@ static TNParams tconv_bwd_filter_params(const seg_conv_desc* d) {
     return p;
 }
 
+
+// conv2d_transpose forward for few output channels (FCN conv_t3: 256 -> 2,
+// k16 s8): Z[p_in][(r,s,k)] = sum_c x[p_in][c] * W[r][s][k][c] as one dense
+// GEMM (N = R*S*K, every phase at once), then each output pixel gathers its
+// (R/st)*(S/st) contributions: y[oh][ow][k] = b[k] + res + sum Z[ih][iw][(r,s,k)].
+template <typename T>
+__global__ void tconv_col2im_k(const T* __restrict__ Z, T* __restrict__ y, int N, int H, int W, int OH, int OW,
+                               int Kp, int kv, int R, int S, int st, int pt, int pl, int ldy,
+                               const float* __restrict__ bias, const T* __restrict__ res, int ldr) {
+    const long total = (long)N * OH * OW;
+    const int zrow = R * S * Kp;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int ow = (int)(i % OW);
+        const long t = i / OW;
+        const int oh = (int)(t % OH);
+        const int n = (int)(t / OH);
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        const int rh = (oh + pt) % st, rw = (ow + pl) % st;
+        for (int r = rh; r < R; r += st) {
+            const int ih = (oh + pt - r) / st;
+            if (ih < 0 || ih >= H) continue;
+            for (int s2 = rw; s2 < S; s2 += st) {
+                const int iw = (ow + pl - s2) / st;
+                if (iw < 0 || iw >= W) continue;
+                const T* zp = Z + (((long)n * H + ih) * W + iw) * zrow + (r * S + s2) * Kp;
+                float v[8];
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(zp), v);
+                if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(zp + 4), v + 4);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += v[k];
+            }
+        }
+        float r8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (res) {
+            const T* rp = res + i * ldr;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), r8);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), r8 + 4);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = k < kv ? acc[k] + (bias ? bias[k] : 0.f) + r8[k] : 0.f;
+        T* yp = y + i * ldy;
+        *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(acc);
+        if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(acc + 4);
+    }
+}
+
+static bool tconv_use_gemm(const seg_conv_desc* d) {
+    return d->K == 8 && d->stride_h == d->stride_w && d->stride_h >= 4 && d->R == d->S;
+}
+
+static size_t tconv_gemm_ws(const seg_conv_desc* d) {
+    const size_t esz = d->dtype == SEG_BF16 ? 2 : 4;
+    NTParams z = {};
+    const int M = d->N * d->H * d->W, Nn = d->R * d->S * d->K;
+    return (size_t)M * Nn * esz + seg::nt_workspace(M, Nn, d->C, d->dtype, 0) + 256;
+}
+
 extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
     if (check_desc(d) != SEG_OK) return 0;
     switch (op) {
         case 0: { NTParams p = conv_fwd_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
         case 1: { NTParams p = conv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
         case 2: { TNParams p = conv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
-        case 3: return 0;
+        case 3: return tconv_use_gemm(d) ? tconv_gemm_ws(d) : 0;
         case 4: { NTParams p = tconv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
         case 5: { TNParams p = tconv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
     }
@@ -202,7 +261,16 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 0: { NTParams p = conv_fwd_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
         case 1: { NTParams p = conv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
         case 2: { TNParams p = conv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_conv; break; }
-        case 3: { NTParams p = tconv_fwd_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 1, &bm, &bn, &sp); macs = macs_t; break; }
+        case 3: {
+            if (tconv_use_gemm(d)) {
+                seg::nt_info(d->N * d->H * d->W, d->R * d->S * d->K, d->C, d->dtype, 0, &bm, &bn, &sp);
+            } else {
+                NTParams p = tconv_fwd_params(d);
+                seg::nt_info(p.M, p.N, p.K, d->dtype, 1, &bm, &bn, &sp);
+            }
+            macs = macs_t;
+            break;
+        }
         case 4: { NTParams p = tconv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_t; break; }
         case 5: { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_t; break; }
         default: return SEG_EINVAL;
@@ -269,6 +337,38 @@ extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void
     if (st) return st;
     if (!x || !w || !y) return SEG_EINVAL;
     if (d->R % d->stride_h || d->S % d->stride_w) return SEG_EINVAL;
+    if (tconv_use_gemm(d)) {
+        // dense GEMM over all taps: a 1x1 "conv" with K_gemm = C, N = R*S*Kp,
+        // filter rows = the packed [R][S][Kp][Cp] image as is
+        const size_t esz = d->dtype == SEG_BF16 ? 2 : 4;
+        const int M = d->N * d->H * d->W, Nn = d->R * d->S * d->K;
+        const size_t zbytes = ((size_t)M * Nn * esz + 255) & ~(size_t)255;
+        if (!ws || ws_bytes < tconv_gemm_ws(d)) return SEG_EWORKSPACE;
+        NTParams g = {};
+        g.M = M; g.N = Nn; g.K = d->C;
+        g.x = x; g.x_img = (long)d->H * d->W * d->ldx; g.IH = d->H; g.IW = d->W; g.C = d->C; g.ldx = d->ldx;
+        g.Ha = d->H; g.Wa = d->W; g.ish = 1; g.isw = 1; g.ioh = 0; g.iow = 0; g.tsh = 1; g.tsw = 1; g.taps_w = 1;
+        g.w = w; g.w_col = d->C; g.w_tap = d->C; g.rstep = 1; g.sstep = 1; g.Sfull = 1;
+        g.y = ws; g.y_img = (long)d->H * d->W * Nn; g.OH = d->H; g.OW = d->W; g.ldy = Nn; g.osh = 1; g.osw = 1;
+        g.epi.n_valid = Nn; g.epi.keep_prob = 1.f;
+        int st2 = seg::launch_nt(g, d->dtype, 1, g.M, (char*)ws + zbytes, ws_bytes - zbytes, (hipStream_t)stream);
+        if (st2) return st2;
+        const long total = (long)d->N * d->OH * d->OW;
+        const int grid = seg_grid_1d(total, 256);
+        const float* bias = epi ? epi->bias : nullptr;
+        const void* res = epi ? epi->residual : nullptr;
+        const int ldr = epi ? epi->ld_residual : 0;
+        if (d->dtype == SEG_BF16)
+            hipLaunchKernelGGL(tconv_col2im_k<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)ws,
+                               (bf16*)y, d->N, d->H, d->W, d->OH, d->OW, d->K, d->k_valid, d->R, d->S, d->stride_h,
+                               d->pad_top, d->pad_left, d->ldy, bias, (const bf16*)res, ldr);
+        else
+            hipLaunchKernelGGL(tconv_col2im_k<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)ws,
+                               (float*)y, d->N, d->H, d->W, d->OH, d->OW, d->K, d->k_valid, d->R, d->S, d->stride_h,
+                               d->pad_top, d->pad_left, d->ldy, bias, (const float*)res, ldr);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     NTParams p = tconv_fwd_params(d);
     p.x = x; p.w = w; p.y = y;
     p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));

@@ -380,6 +380,7 @@ class Session:
                 R, S, Co, _ = n.w.shape
                 _, OH, OW, _ = s
                 n.desc = ops.tconv_desc(N, H, W, C, OH, OW, Co, R, S, n.stride, n.padding, self.cdt)
+                ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_TFWD))
                 p.packs.add((n.w.var_name, ops.PACK_TCONV_FWD))
                 if id(x) in p.needs_grad:
                     p.packs.add((n.w.var_name, ops.PACK_TCONV_BWD))
