@@ -258,8 +258,17 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
     const double macs_t = (double)d->N * d->H * d->W * d->R * d->S * d->c_valid * d->k_valid;
     double macs = 0;
     switch (op) {
-        case 0: { NTParams p = conv_fwd_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
-        case 1: { NTParams p = conv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_conv; break; }
+        case 0:
+        case 1: {
+            NTParams p = op == 0 ? conv_fwd_params(d) : conv_bwd_data_params(d);
+            seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp);
+            seg::HaloPlan hp;
+            if (seg::g_nt_variant == 2 && seg::halo_plan(p, d->dtype, sp, seg::device_cus(), &hp)) {
+                fam = "conv_halo"; bn = hp.bn; sp = hp.splits;
+            }
+            macs = macs_conv;
+            break;
+        }
         case 2: { TNParams p = conv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_conv; break; }
         case 3: {
             if (tconv_use_gemm(d)) {
@@ -275,7 +284,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 5: { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_t; break; }
         default: return SEG_EINVAL;
     }
-    if (bm == 256 && fam[6] == 'n') fam = "igemm_nt2";
+    if (bm == 256 && fam[0] == 'i' && fam[6] == 'n') fam = "igemm_nt2";
     if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[6] == 't' && (op == 2 ? d->R * d->S * d->C : d->R * d->S * d->K) >= 128)
         fam = "igemm_tn2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
@@ -289,6 +298,31 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "igemm_nt_variant")) {
         if (value != 1 && value != 2) return SEG_EINVAL;
         seg::g_nt_variant = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "nt_halo")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_nt_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "halo_phases")) {
+        if (value != 2 && value != 4) return SEG_EINVAL;
+        seg::g_halo_phases = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "halo_stagger")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_halo_stagger = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "halo_wide")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_halo_wide = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
+        if (value < 0 || value > 3) return SEG_EINVAL;
+        seg::g_nt2_ablate = value;
         return SEG_OK;
     }
     if (!strcmp(name, "igemm_tn_variant")) {

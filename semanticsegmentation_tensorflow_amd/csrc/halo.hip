@@ -1,0 +1,711 @@
+// Halo-tiled direct convolution for stride-1 convs (bf16, gfx950).
+//
+// The implicit-GEMM NT kernel (igemm2.hip) re-gathers every input pixel once
+// per filter tap: for a 3x3 conv each activation byte crosses L2 -> LDS nine
+// times, and ablation shows that DMA stream (not the MFMA) bounds it.  Here a
+// block owns a BH x BW tile of output pixels (256 px) x BN output channels and,
+// per 64-channel chunk, stages the tile's input HALO
+// ((BH + (taps_h-1)|tsh|) x (BW + (taps_w-1)|tsw|) pixels x 128 B) in LDS once;
+// all taps of that chunk read their A fragments from the halo at a per-tap row
+// offset.  Only the filter slice (BN x 128 B) is streamed per tap.
+//
+//  * k order: channel chunk outer, tap inner (iteration = (chunk, tap)).
+//  * filter slices: 3-deep LDS ring, slice it+2 in flight while it is consumed.
+//  * halos: double buffered; halo chunk c+1 is staged one 8-row-per-wave piece
+//    per tap iteration of chunk c (pieces h < HI, HI <= taps-1), so every
+//    iteration issues at most B_INS + 1 DMA instructions per wave and one
+//    counted `s_waitcnt vmcnt` + barrier per iteration suffices.
+//  * A fragment = 16 consecutive output px of one tile row = 16 consecutive
+//    halo rows: the (row>>1)&7 chunk XOR stays conflict-free for any offset.
+//  * output: same LDS-staged 16-byte epilogue as igemm_nt2 (bias / BN-affine /
+//    ReLU / dropout / residual), or fp32 split-K slabs over channel chunks.
+//
+// Covers Conv2D fwd and Conv2DBackpropInput of stride-1 convs (dilation any)
+// with C % 64 == 0 -- conv1_2 ... conv5_3 of FCN (Network/model/FCN.py:55-99)
+// and the FC-DenseNet 3x3 layers.
+#include "common.h"
+#include "igemm.h"
+#include "ldsdma.h"
+
+namespace seg {
+
+static __device__ uint4 halo_zero_page[4];
+
+int g_nt_halo = 1;
+int g_halo_wide = 1;
+int g_halo_stagger = 1;
+int g_halo_phases = 2;
+
+struct HaloGeom {
+    int taps_h, tiles_x, tiles_y, nimg;
+    int hwd, hrows, hy0, hx0;   // halo width, rows, origin offset vs tap (0,0)
+    int nchunks, kc_per_split;
+};
+
+template <int BW, int HI, int BN>
+__global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
+    using T = bf16;
+    constexpr int NW = 8, WM = 4, WN = 2, BM = 256, BH = BM / BW;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int B_INS = BN / 8 / NW;
+    constexpr int HBUF = HI * NW * 1024;
+    constexpr int BSTAGE = BN * 128;
+    constexpr int SMEM = 2 * HBUF + 3 * BSTAGE;
+    static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
+    static_assert(B_INS >= 1 && B_INS <= 2, "wait counts below assume B_INS + 1 <= 3");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int tsp = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
+    const int tpi = g.tiles_x * g.tiles_y;
+    const int img = tsp / tpi;
+    if (img >= g.nimg) return;
+    const int trem = tsp - img * tpi;
+    const int ty = trem / g.tiles_x, tx = trem - (trem / g.tiles_x) * g.tiles_x;
+    const int oy0 = ty * BH, ox0 = tx * BW, n0 = tn * BN;
+    int kc_begin = 0, kc_end = g.nchunks;
+    if (p.partial) {
+        kc_begin = blockIdx.z * g.kc_per_split;
+        kc_end = min(g.nchunks, kc_begin + g.kc_per_split);
+    }
+    const int ntaps = g.taps_h * p.taps_w;
+    const int iters = (kc_end - kc_begin) * ntaps;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const int lr = lane >> 3;
+    // physical 16-byte chunk (lane & 7) of LDS row (q*8 + lr) holds global
+    // chunk c; with NW even the swizzle (row>>1)&7 depends on w, lr only.
+    const int c = (lane & 7) ^ ((((w & 1) << 2) + (lr >> 1)) & 7);
+
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const void* zero = (const void*)halo_zero_page;
+
+    // ---- halo rows this lane stages: row (h*NW + w)*8 + lr, h < h_n
+    long h_off[HI];
+    const long xbase = (long)img * p.x_img + c * 8;
+#pragma unroll
+    for (int h = 0; h < HI; ++h) {
+        const int hr = (h * NW + w) * 8 + lr;
+        const int hy = hr / g.hwd, hx = hr - (hr / g.hwd) * g.hwd;
+        const int ih = oy0 + p.ioh + g.hy0 + hy, iw = ox0 + p.iow + g.hx0 + hx;
+        const bool ok = hr < g.hrows && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        h_off[h] = ok ? xbase + ((long)ih * p.IW + iw) * p.ldx : -1;
+    }
+    // wave-uniform: instructions whose 8 rows start below hrows
+    const int h_n = g.hrows > w * 8 ? min(HI, (g.hrows - w * 8 + NW * 8 - 1) / (NW * 8)) : 0;
+
+    long b_off[B_INS];
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+        const int n = n0 + (i * NW + w) * 8 + lr;
+        b_off[i] = n < p.N ? (long)n * p.w_col + c * 8 : -1;
+    }
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+    const unsigned ldsB = lds0 + 2 * HBUF;
+
+    auto load_halo = [&](int h, int kc, int buf) {
+        const void* src = h_off[h] >= 0 ? (const void*)(X + h_off[h] + kc * 64) : zero;
+        glds16(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
+    };
+    // B issue cursor (chunk, tap j/i)
+    int b_kc = kc_begin, b_j = 0, b_i = 0;
+    auto issue_b = [&](int stage) {
+        const long wtap = (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const void* src = b_off[i] >= 0 ? (const void*)(Wt + b_off[i] + wtap) : zero;
+            glds16(src, ldsB + stage * BSTAGE + (i * NW + w) * 1024);
+        }
+        if (++b_i == p.taps_w) {
+            b_i = 0;
+            if (++b_j == g.taps_h) { b_j = 0; ++b_kc; }
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (iters > 0) {
+        for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
+        issue_b(0);
+    }
+    if (iters > 1) issue_b(1);
+    int last = iters > 1 ? B_INS : 0;   // DMA instructions of the newest batch
+
+    const int fr = lane & 15, fg = lane >> 4;
+    int rowbase[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+        const int ml = wm * WTM + mi * 16;
+        rowbase[mi] = (ml / BW) * g.hwd + (ml % BW) + fr;
+    }
+    int t_j = 0, t_i = 0, kc = kc_begin, stage = 0, hbuf = 0, tap = 0;
+    for (int it = 0; it < iters; ++it) {
+        // everything but the newest batch (slice it+1, next-halo piece) landed
+        if (last == 0) wait_vmcnt<0>();
+        else if (last == 1) wait_vmcnt<1>();
+        else if (last == 2) wait_vmcnt<2>();
+        else wait_vmcnt<3>();
+        lds_barrier();
+        int issued = 0;
+        if (it + 2 < iters) {
+            issue_b(stage == 0 ? 2 : stage - 1);
+            issued = B_INS;
+        }
+        if (tap < h_n && kc + 1 < kc_end) {
+            load_halo(tap, kc + 1, hbuf ^ 1);
+            ++issued;
+        }
+        last = issued;
+
+        const char* Hs = smem + hbuf * HBUF;
+        const char* Bs = smem + 2 * HBUF + stage * BSTAGE;
+        const int toff = (t_j * p.tsh - g.hy0) * g.hwd + t_i * p.tsw - g.hx0;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            uint4 af[TM], bfr[TN];
+            const int chunk = ks * 4 + fg;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int row = rowbase[mi] + toff;
+                af[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int row = wn * WTN + ni * 16 + fr;
+                bfr[ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]), acc[mi][ni], 0, 0, 0);
+        }
+        stage = stage == 2 ? 0 : stage + 1;
+        ++tap;
+        if (++t_i == p.taps_w) {
+            t_i = 0;
+            if (++t_j == g.taps_h) {
+                t_j = 0;
+                tap = 0;
+                ++kc;
+                hbuf ^= 1;
+            }
+        }
+    }
+
+    if (p.partial) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ml = wm * WTM + mi * 16 + fg * 4 + r;
+                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+                if (oy >= p.OH || ox >= p.OW) continue;
+                const long m = ((long)img * p.OH + oy) * p.OW + ox;
+                float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col = n0 + wn * WTN + ni * 16 + fr;
+                    if (col < p.N) prow[col] = acc[mi][ni][r];
+                }
+            }
+        return;
+    }
+    // ---- epilogue: wave tile -> LDS (fp32), then 8 columns x one row per lane
+    constexpr int SROW = WTN * 4 + 16;
+    static_assert(NW * WTM * SROW <= SMEM, "epilogue staging must fit");
+    lds_barrier();
+    char* wbuf = smem + w * WTM * SROW;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) = acc[mi][ni][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int CPR = WTN / 8;
+    constexpr int RPP = 64 / CPR;
+    const int cch = lane % CPR, rsub = lane / CPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
+    const EpiParams& e = p.epi;
+    float bias[8], scl[8], shf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        const bool cv = col < e.n_valid;
+        bias[j] = (e.bias && cv) ? e.bias[col] : 0.f;
+        scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
+        shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
+    }
+#pragma unroll 2
+    for (int rr = rsub; rr < WTM; rr += RPP) {
+        const int ml = wm * WTM + rr;
+        const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+        if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
+        const long pix = (long)oy * p.OW + ox;
+        const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
+        const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        float res[8];
+        if (e.residual) {
+            const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
+        }
+        const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = col0 + j;
+            float x = v[j] * scl[j] + shf[j] + bias[j];
+            if (e.relu) x = fmaxf(x, 0.f);
+            if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+            if (e.residual) x += res[j];
+            v[j] = col < e.n_valid ? x : 0.f;
+        }
+        T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
+        *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// 256 x 256 variant (N > 128): 8 waves as 2 (M) x 4 (N), 128 x 64 per wave,
+// each (chunk, tap) iteration split into 4 phases, one C quadrant
+// (64 px x 32 ch x K=64 = 16 MFMAs) per phase:
+//   reads for the phase -> DMA issue -> [wait] -> barrier -> lgkmcnt(0) ->
+//   setprio(1) MFMA x16 setprio(0) -> barrier
+// Quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0): A halves re-read twice,
+// B halves once per iteration.  LDS: 2 halo buffers + 2 filter slices.
+//   q0 issues filter slice it+1 (4 DMA / wave) into the other slice buffer;
+//   q1 issues one halo piece of chunk+1 (taps < h_n);
+//   q3 waits for slice it+1 (vmcnt(1) if a halo piece is still young), so
+//   the next iteration's q0 reads it after q3's barriers.
+// WAR: a slice / halo buffer is restaged >= 2 phases after its last reads,
+// which every wave retired with lgkmcnt(0) before a barrier.
+// ---------------------------------------------------------------------------
+// STAG: the upper M wave group runs one barrier behind, so on every SIMD one
+// wave's MFMA cluster overlaps the other's LDS reads (waves w and w+4 share a
+// SIMD).  Every DMA wait precedes a barrier that the other group passes before
+// its reads of that data; the extra barrier is paid back after the loop.
+// ABL (diagnostic builds, garbage results): 1 = no DMA in the loop, 2 = no
+// MFMA, 3 = no LDS fragment reads.
+// PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
+// both B halves read in the first).
+template <int BW, bool STAG, int ABL = 0, int PH = 4>
+__global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
+    using T = bf16;
+    constexpr int NW = 8, BM = 256, BN = 256, BH = BM / BW, HI = 6;
+    constexpr int HBUF = HI * NW * 1024;
+    constexpr int BBUF = BN * 128;
+    constexpr int SMEM = 2 * HBUF + 2 * BBUF;
+    constexpr int B_INS = BN / 8 / NW;   // 4
+    static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int tsp = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
+    const int tpi = g.tiles_x * g.tiles_y;
+    const int img = tsp / tpi;
+    if (img >= g.nimg) return;
+    const int trem = tsp - img * tpi;
+    const int ty = trem / g.tiles_x, tx = trem - (trem / g.tiles_x) * g.tiles_x;
+    const int oy0 = ty * BH, ox0 = tx * BW, n0 = tn * BN;
+    int kc_begin = 0, kc_end = g.nchunks;
+    if (p.partial) {
+        kc_begin = blockIdx.z * g.kc_per_split;
+        kc_end = min(g.nchunks, kc_begin + g.kc_per_split);
+    }
+    const int ntaps = g.taps_h * p.taps_w;
+    const int iters = (kc_end - kc_begin) * ntaps;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 2, wn = w & 3;
+    const int lr = lane >> 3;
+    const int c = (lane & 7) ^ ((((w & 1) << 2) + (lr >> 1)) & 7);
+
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const void* zero = (const void*)halo_zero_page;
+
+    long h_off[HI];
+    const long xbase = (long)img * p.x_img + c * 8;
+#pragma unroll
+    for (int h = 0; h < HI; ++h) {
+        const int hr = (h * NW + w) * 8 + lr;
+        const int hy = hr / g.hwd, hx = hr - (hr / g.hwd) * g.hwd;
+        const int ih = oy0 + p.ioh + g.hy0 + hy, iw = ox0 + p.iow + g.hx0 + hx;
+        const bool ok = hr < g.hrows && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        h_off[h] = ok ? xbase + ((long)ih * p.IW + iw) * p.ldx : -1;
+    }
+    const int h_n = g.hrows > w * 8 ? min(HI, (g.hrows - w * 8 + NW * 8 - 1) / (NW * 8)) : 0;
+    long b_off[B_INS];
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+        const int n = n0 + (i * NW + w) * 8 + lr;
+        b_off[i] = n < p.N ? (long)n * p.w_col + c * 8 : -1;
+    }
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+    const unsigned ldsB = lds0 + 2 * HBUF;
+
+    auto load_halo = [&](int h, int kc, int buf) {
+        const void* src = h_off[h] >= 0 ? (const void*)(X + h_off[h] + kc * 64) : zero;
+        glds16(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
+    };
+    int b_kc = kc_begin, b_j = 0, b_i = 0;
+    auto issue_b = [&](int buf) {
+        const long wtap = (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const void* src = b_off[i] >= 0 ? (const void*)(Wt + b_off[i] + wtap) : zero;
+            glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
+        }
+        if (++b_i == p.taps_w) {
+            b_i = 0;
+            if (++b_j == g.taps_h) { b_j = 0; ++b_kc; }
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (iters > 0) {
+        for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
+        issue_b(0);
+    }
+    wait_vmcnt<0>();
+    lds_barrier();
+    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
+
+    const int fr = lane & 15, fg = lane >> 4;
+    int rowbase[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+        const int ml = wm * 128 + mi * 16;
+        rowbase[mi] = (ml / BW) * g.hwd + (ml % BW) + fr;
+    }
+    int t_j = 0, t_i = 0, kc = kc_begin, hbuf = 0, tap = 0, bbuf = 0;
+    for (int it = 0; it < iters; ++it) {
+        const char* Hs = smem + hbuf * HBUF;
+        const char* Bs = smem + 2 * HBUF + bbuf * BBUF;
+        const int toff = (t_j * p.tsh - g.hy0) * g.hwd + t_i * p.tsw - g.hx0;
+        uint4 af[2][4], bq[2][2][2];   // A half [ks][mi]; B [nh][ks][ni]
+        auto read_a = [&](int mh) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const int row = rowbase[mh * 4 + mi] + toff;
+                    if constexpr (ABL == 3) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
+                    else af[ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                }
+        };
+        auto read_b = [&](int nh) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int row = wn * 64 + nh * 32 + ni * 16 + fr;
+                    if constexpr (ABL == 3) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
+                    else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                }
+        };
+        auto mma = [&](int mh, int nh) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        if constexpr (ABL == 2) {
+                            asm volatile("" ::"v"(af[ks][mi].x), "v"(af[ks][mi].w), "v"(bq[nh][ks][ni].x), "v"(bq[nh][ks][ni].w));
+                        } else {
+                            acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[nh][ks][ni]),
+                                acc[mh * 4 + mi][nh * 2 + ni], 0, 0, 0);
+                        }
+                    }
+            __builtin_amdgcn_s_setprio(0);
+        };
+        if constexpr (PH == 4) {
+            // q0
+            read_a(0);
+            read_b(0);
+            if (ABL != 1 && it + 1 < iters) issue_b(bbuf ^ 1);
+            __builtin_amdgcn_s_barrier();
+            mma(0, 0);
+            __builtin_amdgcn_s_barrier();
+            // q1
+            read_b(1);
+            const bool hp = ABL != 1 && tap < h_n && kc + 1 < kc_end;
+            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
+            __builtin_amdgcn_s_barrier();
+            mma(0, 1);
+            __builtin_amdgcn_s_barrier();
+            // q2
+            read_a(1);
+            __builtin_amdgcn_s_barrier();
+            mma(1, 1);
+            __builtin_amdgcn_s_barrier();
+            // q3: slice it+1 (and every older DMA) must land before the next q0
+            if (hp) wait_vmcnt<1>();
+            else wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+            mma(1, 0);
+            __builtin_amdgcn_s_barrier();
+        } else {
+            // h0: A0 + whole B slice, 32 MFMAs
+            read_a(0);
+            read_b(0);
+            read_b(1);
+            if (ABL != 1 && it + 1 < iters) issue_b(bbuf ^ 1);
+            __builtin_amdgcn_s_barrier();
+            mma(0, 0);
+            mma(0, 1);
+            __builtin_amdgcn_s_barrier();
+            // h1: A1, halo piece; slice it+1 must land before the next h0
+            read_a(1);
+            const bool hp = ABL != 1 && tap < h_n && kc + 1 < kc_end;
+            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
+            if (hp) wait_vmcnt<1>();
+            else wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+            mma(1, 1);
+            mma(1, 0);
+            __builtin_amdgcn_s_barrier();
+        }
+        bbuf ^= 1;
+        ++tap;
+        if (++t_i == p.taps_w) {
+            t_i = 0;
+            if (++t_j == g.taps_h) {
+                t_j = 0;
+                tap = 0;
+                ++kc;
+                hbuf ^= 1;
+            }
+        }
+    }
+    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
+
+    if (p.partial) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ml = wm * 128 + mi * 16 + fg * 4 + r;
+                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+                if (oy >= p.OH || ox >= p.OW) continue;
+                const long m = ((long)img * p.OH + oy) * p.OW + ox;
+                float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const int col = n0 + wn * 64 + ni * 16 + fr;
+                    if (col < p.N) prow[col] = acc[mi][ni][r];
+                }
+            }
+        return;
+    }
+    // ---- epilogue in two 64-row halves per wave (LDS holds 8 x 64 x 64 fp32)
+    constexpr int SROW = 64 * 4 + 16;
+    static_assert(NW * 64 * SROW <= SMEM, "epilogue staging must fit");
+    const int cch = lane & 7, rsub = lane >> 3;
+    const int col0 = n0 + wn * 64 + cch * 8;
+    const EpiParams& e = p.epi;
+    float bias[8], scl[8], shf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        const bool cv = col < e.n_valid;
+        bias[j] = (e.bias && cv) ? e.bias[col] : 0.f;
+        scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
+        shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
+    }
+    char* wbuf = smem + w * 64 * SROW;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+        lds_barrier();
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                        acc[mh * 4 + mi][ni][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 2
+        for (int rr = rsub; rr < 64; rr += 8) {
+            const int ml = wm * 128 + mh * 64 + rr;
+            const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
+            const long pix = (long)oy * p.OW + ox;
+            const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
+            const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
+            float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            float res[8];
+            if (e.residual) {
+                const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
+            }
+            const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int col = col0 + j;
+                float x = v[j] * scl[j] + shf[j] + bias[j];
+                if (e.relu) x = fmaxf(x, 0.f);
+                if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+                if (e.residual) x += res[j];
+                v[j] = col < e.n_valid ? x : 0.f;
+            }
+            T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
+            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static constexpr int kHaloBW[3] = {16, 32, 64};
+
+bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp) {
+    if (!g_nt_halo || dtype != SEG_BF16) return false;
+    if (p.phase || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1 || p.ooh != 0 || p.oow != 0) return false;
+    if (p.Ha != p.OH || p.Wa != p.OW || p.rb != 0 || p.sb != 0) return false;
+    if (p.C % 64 != 0 || p.K % p.C != 0 || p.taps_w <= 0) return false;
+    const int ntaps = p.K / p.C;
+    if (ntaps % p.taps_w) return false;
+    const int taps_h = ntaps / p.taps_w;
+    if (p.OH <= 0 || p.OW <= 0 || p.M % (p.OH * p.OW)) return false;
+    const int nimg = p.M / (p.OH * p.OW);
+    long best = -1;
+    for (int k = 0; k < 3; ++k) {
+        const int bw = kHaloBW[k], bh = 256 / bw;
+        const int hwd = bw + (p.taps_w - 1) * std::abs(p.tsw);
+        const int hht = bh + (taps_h - 1) * std::abs(p.tsh);
+        const int hrows = hwd * hht;
+        const int hi = (hrows + 63) / 64;
+        if (hi > 7 || hi > ntaps - 1) continue;
+        const int tx = (p.OW + bw - 1) / bw, ty = (p.OH + bh - 1) / bh;
+        // padded output work + halo staging (~1/9 of the per-tap filter stream)
+        const long cost = (long)tx * ty * (256 * 16 + hrows);
+        if (best < 0 || cost < best) {
+            best = cost;
+            hp->bw = bw;
+            hp->hi = hi <= 6 ? 6 : 7;
+            hp->geom[0] = taps_h; hp->geom[1] = tx; hp->geom[2] = ty; hp->geom[3] = nimg;
+            hp->geom[4] = hwd; hp->geom[5] = hrows;
+            hp->geom[6] = std::min(0, (taps_h - 1) * p.tsh);
+            hp->geom[7] = std::min(0, (p.taps_w - 1) * p.tsw);
+        }
+    }
+    if (best < 0) return false;
+    hp->bn = p.N <= 64 ? 64 : 128;
+    if (p.N > 128 && g_halo_wide) {
+        // 256 x 256 four-phase kernel: halo must fit 6 pieces (384 rows)
+        long best2 = -1;
+        for (int k = 0; k < 2; ++k) {
+            const int bw = kHaloBW[k], bh = 256 / bw;
+            const int hwd = bw + (p.taps_w - 1) * std::abs(p.tsw);
+            const int hht = bh + (taps_h - 1) * std::abs(p.tsh);
+            if (hwd * hht > 384 || 6 > ntaps - 1) continue;
+            const int tx = (p.OW + bw - 1) / bw, ty = (p.OH + bh - 1) / bh;
+            const long cost = (long)tx * ty * (256 * 16 + hwd * hht);
+            if (best2 < 0 || cost < best2) {
+                best2 = cost;
+                hp->bw = bw;
+                hp->hi = 6;
+                hp->geom[1] = tx; hp->geom[2] = ty;
+                hp->geom[4] = hwd; hp->geom[5] = hwd * hht;
+            }
+        }
+        if (best2 >= 0) hp->bn = 256;
+    }
+    const int nchunks = p.C / 64;
+    const long tiles = (long)hp->geom[1] * hp->geom[2] * nimg * ((p.N + hp->bn - 1) / hp->bn);
+    // split-K over channel chunks: minimise (block rounds x chunks per split),
+    // +4% per extra split for the fp32 slab round trip and reduce
+    const int cap = std::min(nchunks, std::max(1, max_splits));
+    int kps = nchunks;
+    double best_t = 1e30;
+    for (int sp = 1; sp <= cap; ++sp) {
+        const int k = (nchunks + sp - 1) / sp;
+        const int s2 = (nchunks + k - 1) / k;
+        const long rounds = (tiles * s2 + cus - 1) / cus;
+        const double t = (double)rounds * k * (1.0 + 0.04 * (s2 - 1));
+        if (t < best_t * 0.999) { best_t = t; kps = k; }
+    }
+    hp->splits = (nchunks + kps - 1) / kps;
+    hp->geom[8] = nchunks;
+    hp->geom[9] = kps;
+    hp->tiles = tiles;
+    return true;
+}
+
+template <int BW, int HI, int BN>
+static void launch_halo_t(NTParams& p, const HaloGeom& g, long tiles, int gridz, hipStream_t s) {
+    hipLaunchKernelGGL((conv_halo<BW, HI, BN>), dim3((unsigned)tiles, 1, gridz), dim3(512), 0, s, p, g);
+}
+
+template <int BW, int HI>
+static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s) {
+    if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s);
+    else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s);
+}
+
+void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {
+    HaloGeom g;
+    g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
+    g.hwd = hp.geom[4]; g.hrows = hp.geom[5]; g.hy0 = hp.geom[6]; g.hx0 = hp.geom[7];
+    g.nchunks = hp.geom[8]; g.kc_per_split = hp.geom[9];
+    if (hp.bn == 256) {
+        const dim3 grid((unsigned)hp.tiles, 1, gridz);
+        if (g_nt2_ablate && hp.bw == 16) {
+            if (g_nt2_ablate == 1) hipLaunchKernelGGL((conv_halo2<16, true, 1>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 2) hipLaunchKernelGGL((conv_halo2<16, true, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 3) hipLaunchKernelGGL((conv_halo2<16, true, 3>), grid, dim3(512), 0, s, p, g);
+            return;
+        }
+        if (g_halo_phases == 2) {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2>), grid, dim3(512), 0, s, p, g);
+            return;
+        }
+        if (g_halo_stagger) {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32, true>), grid, dim3(512), 0, s, p, g);
+        } else {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32, false>), grid, dim3(512), 0, s, p, g);
+        }
+        return;
+    }
+    const int key = hp.bw * 10 + hp.hi;
+    switch (key) {
+        case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
+    }
+}
+
+}  // namespace seg

@@ -70,6 +70,21 @@ void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
 extern int g_nt_variant;
 extern int g_tn_variant;
+extern int g_nt2_ablate;
 void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s);
+
+// halo-tiled direct conv (halo.hip) for stride-1 NT problems
+struct HaloPlan {
+    int bw, hi, bn, splits;
+    long tiles;
+    int geom[10];
+};
+extern int g_nt_halo;
+extern int g_halo_wide;
+extern int g_halo_stagger;
+extern int g_halo_phases;
+int device_cus();
+bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
+void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s);
 
 }  // namespace seg

@@ -583,6 +583,8 @@ static int num_cus() {
     return cus;
 }
 
+int device_cus() { return num_cus(); }
+
 // Kernel generation for the NT GEMMs (1 = register-staged 128-row tiles,
 // 2 = LDS-DMA 3-stage ring, 256-row tiles).  Runtime-selectable for tests.
 int g_nt_variant = 2;
@@ -632,6 +634,23 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
     if (nphases > 1) splits = 1;
     p.partial = nullptr;
+    HaloPlan hp;
+    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, splits, num_cus(), &hp)) {
+        if (hp.splits > 1) {
+            const size_t need = (size_t)hp.splits * p.M * p.N * sizeof(float);
+            if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
+            p.partial = reinterpret_cast<float*>(ws);
+        }
+        launch_halo(p, hp, hp.splits, s);
+        SEG_CHECK_LAUNCH();
+        if (p.partial) {
+            const long total = (long)p.M * (p.N / 8);
+            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, hp.splits);
+            SEG_CHECK_LAUNCH();
+            p.partial = nullptr;
+        }
+        return SEG_OK;
+    }
     int gridz = nphases;
     if (splits > 1) {
         const int kt = (p.K + BK - 1) / BK;

@@ -12,30 +12,11 @@
 //  * 8 waves (4 x 2), 64x64 (or 64x32) per wave on v_mfma_f32_16x16x32_bf16.
 #include "common.h"
 #include "igemm.h"
+#include "ldsdma.h"
 
 namespace seg {
 
 __device__ uint4 g_zero_page[4];
-
-__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
-                 : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
-    const int xcd = bid & 7;
-    const int q = nwg >> 3, r = nwg & 7;
-    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    return base + (bid >> 3);
-}
 
 template <typename T>
 [[maybe_unused]] __device__ __forceinline__ void nt2_store(const NTParams& p, int row, int col, float v, int Ha, int Wa, int ooh,
@@ -64,7 +45,9 @@ template <typename T>
     reinterpret_cast<T*>(p.y)[img * p.y_img + pix * p.ldy + col] = from_f32<T>(v);
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+// ABL (diagnostic builds only, results are garbage): 1 = no LDS-DMA in the
+// main loop, 2 = no MFMA, 3 = trivial (row-constant) source addresses.
+template <typename T, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
     constexpr int NW = WM * WN;
     constexpr int EPC = dt_traits<T>::EPC;
@@ -161,15 +144,17 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
         for (int i = 0; i < A_INS; ++i) {
             const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
             const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-            const void* src = ok ? (const void*)(X + a_off[i] + ((long)ih * p.IW + iw) * p.ldx + cc) : zero;
-            glds16(src, sb_ + (i * NW + w) * 1024);
+            const void* src;
+            if constexpr (ABL == 3) src = (const void*)(X + a_off[i] + (long)(a_ih[i] & 7) * p.ldx + cc);
+            else src = ok ? (const void*)(X + a_off[i] + ((long)ih * p.IW + iw) * p.ldx + cc) : zero;
+            if constexpr (ABL != 1) glds16(src, sb_ + (i * NW + w) * 1024);
         }
         const long wtap = (long)((rb + p.rstep * tj) * p.Sfull + (sb + p.sstep * ti)) * p.w_tap + cc;
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {
             const bool ok = b_ok[i] && kok;
             const void* src = ok ? (const void*)(Wt + b_off[i] + wtap) : zero;
-            glds16(src, sb_ + BM * 128 + (i * NW + w) * 1024);
+            if constexpr (ABL != 1) glds16(src, sb_ + BM * 128 + (i * NW + w) * 1024);
         }
         kg += BK;
         cc += BK;
@@ -215,7 +200,9 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
             for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
-                    if constexpr (sizeof(T) == 2) {
+                    if constexpr (ABL == 2) {
+                        asm volatile("" ::"v"(af[mi].x), "v"(af[mi].w), "v"(bfr[ni].x), "v"(bfr[ni].w));
+                    } else if constexpr (sizeof(T) == 2) {
                         acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]), acc[mi][ni], 0,
                             0, 0);
@@ -513,10 +500,20 @@ void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s) {
     else launch_tn2_t<128, 128, 2, 4>(p, splits, s);
 }
 
+int g_nt2_ablate = 0;
+
 template <typename T, int BM, int BN, int WM, int WN>
 void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), dim3(tiles, 1, gridz), dim3(WM * WN * 64), 0, s, p);
+    const dim3 g(tiles, 1, gridz), b(WM * WN * 64);
+    if constexpr (sizeof(T) == 2 && BN == 128) {
+        switch (g_nt2_ablate) {
+            case 1: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 1>), g, b, 0, s, p); return;
+            case 2: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 2>), g, b, 0, s, p); return;
+            case 3: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 3>), g, b, 0, s, p); return;
+        }
+    }
+    hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), g, b, 0, s, p);
 }
 
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s) {

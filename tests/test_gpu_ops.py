@@ -17,12 +17,25 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2], ids=["nt1", "nt2"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph"])
 def ntv(request, dev):
-    """Run NT-GEMM tests on both kernel generations."""
-    ops.set_option("igemm_nt_variant", request.param)
-    yield request.param
+    """Run NT tests on every kernel generation: 1 = register-staged GEMM,
+    2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
+    (bf16, stride 1, C % 64 == 0; 256x256 four-phase tiles for N > 128),
+    4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
+    stagger (two-phase schedule), 6 = 3 with four phases per iteration."""
+    v = request.param
+    ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
+    ops.set_option("nt_halo", 1 if v >= 3 else 0)
+    ops.set_option("halo_wide", 0 if v == 4 else 1)
+    ops.set_option("halo_stagger", 0 if v == 5 else 1)
+    ops.set_option("halo_phases", 4 if v == 6 else 2)
+    yield v
     ops.set_option("igemm_nt_variant", 2)
+    ops.set_option("nt_halo", 1)
+    ops.set_option("halo_wide", 1)
+    ops.set_option("halo_stagger", 1)
+    ops.set_option("halo_phases", 2)
 
 
 DTYPES = [torch.float32, torch.bfloat16]
@@ -40,6 +53,12 @@ CONV_CASES = [
     (1, 12, 12, 8, 16, 3, 3, 1, 2, "SAME"),     # atrous (dilation 2)
     (1, 10, 10, 16, 8, 3, 3, 1, 1, "VALID"),
     (3, 20, 20, 128, 256, 3, 3, 1, 1, "SAME"),  # multi-tile M and N, uniform-tap path
+    # halo-tiled direct conv: ragged tiles in x and y, BN=64, dilation, split-K
+    (2, 37, 70, 64, 64, 3, 3, 1, 1, "SAME"),
+    (1, 30, 41, 64, 128, 3, 3, 1, 2, "SAME"),   # atrous halo (hi = 7)
+    (1, 9, 21, 512, 128, 3, 3, 1, 1, "SAME"),   # few tiles -> channel-chunk split-K
+    (1, 18, 19, 128, 72, 3, 3, 1, 1, "VALID"),
+    (2, 33, 45, 64, 328, 3, 3, 1, 1, "SAME"),   # 256-wide halo tiles: 2 N tiles + tail
 ]
 
 
