@@ -238,7 +238,14 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
     switch (op) {
         case 0: { NTParams p = conv_fwd_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
         case 1: { NTParams p = conv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
-        case 2: { TNParams p = conv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
+        case 2: {
+            TNParams p = conv_bwd_filter_params(d);
+            size_t need = seg::tn_workspace(p.M, p.N, p.P, d->dtype);
+            seg::WgradPlan wp;
+            if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp))
+                need = std::max(need, seg::wgrad_workspace(wp, p));
+            return need;
+        }
         case 3: return tconv_use_gemm(d) ? tconv_gemm_ws(d) : 0;
         case 4: { NTParams p = tconv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
         case 5: { TNParams p = tconv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
@@ -269,7 +276,17 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             macs = macs_conv;
             break;
         }
-        case 2: { TNParams p = conv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_conv; break; }
+        case 2: {
+            TNParams p = conv_bwd_filter_params(d);
+            seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp);
+            fam = "igemm_tn";
+            seg::WgradPlan wp;
+            if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
+                fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
+            }
+            macs = macs_conv;
+            break;
+        }
         case 3: {
             if (tconv_use_gemm(d)) {
                 seg::nt_info(d->N * d->H * d->W, d->R * d->S * d->K, d->C, d->dtype, 0, &bm, &bn, &sp);
@@ -285,7 +302,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         default: return SEG_EINVAL;
     }
     if (bm == 256 && fam[0] == 'i' && fam[6] == 'n') fam = "igemm_nt2";
-    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[6] == 't' && (op == 2 ? d->R * d->S * d->C : d->R * d->S * d->K) >= 128)
+    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[0] == 'i' && fam[6] == 't' && (op == 2 ? d->R * d->S * d->C : d->R * d->S * d->K) >= 128)
         fam = "igemm_tn2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
     if (splits) *splits = sp;
@@ -303,6 +320,16 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt_halo")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wgrad_halo")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_wgrad_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wgrad_nt")) {
+        if (value != 64 && value != 128) return SEG_EINVAL;
+        seg::g_wgrad_nt = value;
         return SEG_OK;
     }
     if (!strcmp(name, "halo_phases")) {

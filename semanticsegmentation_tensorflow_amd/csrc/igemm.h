@@ -87,4 +87,16 @@ int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
 void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s);
 
+// halo-tiled filter gradient (wgrad.hip) for stride-1 3x3 TN problems
+struct WgradPlan {
+    int bw, nt, splits;
+    long blocks;
+    int g[10];
+};
+extern int g_wgrad_halo;
+extern int g_wgrad_nt;
+bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
+size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
+void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s);
+
 }  // namespace seg

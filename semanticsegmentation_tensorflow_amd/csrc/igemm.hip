@@ -727,9 +727,25 @@ static void launch_tn_t(TNParams& p, int gridz, hipStream_t s) {
 template <typename T>
 static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
+    p.partial = nullptr;
+    WgradPlan wp;
+    if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
+        if (wp.splits > 1) {
+            if (!ws || ws_bytes < wgrad_workspace(wp, p)) return SEG_EWORKSPACE;
+            p.partial = reinterpret_cast<float*>(ws);
+        }
+        launch_wgrad(p, wp, s);
+        SEG_CHECK_LAUNCH();
+        if (p.partial) {
+            const long total = (long)p.M * (p.N / 4);
+            hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, wp.splits);
+            SEG_CHECK_LAUNCH();
+            p.partial = nullptr;
+        }
+        return SEG_OK;
+    }
     int bm, bn, splits;
     choose_tn(p.M, p.N, p.P, BKP, bm, bn, splits);
-    p.partial = nullptr;
     int gridz = 1;
     if (splits > 1) {
         const int kt = (p.P + BKP - 1) / BKP;

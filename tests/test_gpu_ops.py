@@ -117,12 +117,19 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype):
     assert_close(from_dev(dx, C), xr.grad, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2], ids=["tn1", "tn2"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128"])
 def tnv(request, dev):
-    """Run TN-GEMM (filter gradient) tests on both kernel generations."""
-    ops.set_option("igemm_tn_variant", request.param)
-    yield request.param
+    """Run filter-gradient tests on every kernel generation: 1 = register-staged
+    TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
+    where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles."""
+    v = request.param
+    ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
+    ops.set_option("wgrad_halo", 1 if v >= 3 else 0)
+    ops.set_option("wgrad_nt", 128 if v == 4 else 64)
+    yield v
     ops.set_option("igemm_tn_variant", 2)
+    ops.set_option("wgrad_halo", 1)
+    ops.set_option("wgrad_nt", 64)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

@@ -65,3 +65,23 @@ for (name, H, W, C, K) in LAYERS:
     info = ops.conv_kernel_info(d, 0)[0], ops.conv_kernel_info(d, 1)[0]
     print(name, info, "  ".join(f"{m}/{k}={min(v)*1e3:.1f}us({flops/min(v)/1e9:.0f}TF)" for (m, k), v in res.items()),
           flush=True)
+
+# ---- filter gradients: igemm_tn2 vs halo (NT 64 / 128)
+WMODES = [("tn2", 0, 64), ("wgh64", 1, 64), ("wgh128", 1, 128)]
+for (name, H, W, C, K) in LAYERS:
+    N = 4
+    d = ops.conv_desc(N, H, W, C, K, 3, 3, dtype=ops.BF16)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, K, device=dev).to(torch.bfloat16)
+    dw = torch.empty(3, 3, C, K, device=dev, dtype=torch.float32)
+    flops = ops.conv_kernel_info(d, 2)[2]
+    res = {}
+    for rnd in range(4):
+        for (m, on, nt) in WMODES:
+            ops.set_option("wgrad_halo", on)
+            ops.set_option("wgrad_nt", nt)
+            res.setdefault(m, []).append(timeit(lambda: ops.conv2d_bwd_filter(d, x, dy, dw, ws)))
+    ops.set_option("wgrad_halo", 1)
+    ops.set_option("wgrad_nt", 64)
+    print(name, ops.conv_kernel_info(d, 2)[:2],
+          "  ".join(f"{m}={min(v)*1e3:.1f}us({flops/min(v)/1e9:.0f}TF)" for m, v in res.items()), flush=True)
