@@ -220,6 +220,30 @@ int seg_confusion(const int64_t* pred, const uint8_t* labels, int N, int H, int 
 int seg_adam_tf1_step(float* p, const float* g, float* m, float* v, long n, float lr,
                       float beta1, float beta2, float eps, int t, float grad_scale, void* stream);
 
+/* Multi-tensor Adam fused with the packed compute copies (one launch per step).
+ * Each segment is one variable of the flat buffers viewed as [rs][a][b]
+ * (conv HWIO: rs=R*S, a=C, b=K; tconv [kh,kw,out,in]: a=out, b=in; biases:
+ * rs=a=1).  After the update the new values are also written to the optional
+ * copies (element type = dtype; padding entries are left untouched):
+ *   rows_dst[(rs*rows_ap + a)*rows_bp + b]   (seg_pack_filter modes 1, 2)
+ *   tr_dst  [(b*RS + rs)*tr_ap + a]          (seg_pack_filter modes 0, 3)
+ * replaces seg_adam_tf1_step + seg_pack_filter per step.                     */
+typedef struct seg_adam_segment {
+    long long offset;       /* element offset into p / g / m / v */
+    int rs, a, b;
+    int tile_begin;         /* filled by seg_adam_segments_plan */
+    void* rows_dst;
+    int rows_ap, rows_bp;
+    void* tr_dst;
+    int tr_ap, tr_bp;
+} seg_adam_segment;
+/* Host-side: fills tile_begin; returns the total tile count (< 0 on error). */
+int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs);
+/* dev_segs: the planned table copied to device memory. */
+int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_adam_segment* dev_segs,
+                      int nsegs, int total_tiles, float lr, float beta1, float beta2, float eps, int t,
+                      float grad_scale, int dtype, void* stream);
+
 /* ---- misc ---------------------------------------------------------------- */
 int seg_fill(void* y, long n, float value, int dtype, void* stream);
 int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);

@@ -18,7 +18,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
@@ -53,7 +53,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise SegKernelError(f"hipcc failed for {src}:\n{r.stderr}")
         return o
 
-    with ThreadPoolExecutor(max_workers=min(6, len(SOURCES))) as ex:
+    with ThreadPoolExecutor(max_workers=min(7, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     if force or not os.path.exists(LIB_PATH) or any(
             os.path.getmtime(o) > os.path.getmtime(LIB_PATH) for o in objs):
@@ -127,6 +127,8 @@ SIGNATURES = {
     "seg_argmax": (_I, [_P, _I, _I, _L, _P, _I, _P]),
     "seg_confusion": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "seg_adam_tf1_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _I, _F, _P]),
+    "seg_adam_segments_plan": (_I, [_P, _I]),
+    "seg_adam_tf1_pack": (_I, [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _I, _F, _I, _P]),
     "seg_fill": (_I, [_P, _L, _F, _I, _P]),
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
     "seg_status_string": (ctypes.c_char_p, [_I]),

@@ -360,6 +360,48 @@ def adam_tf1_step(p, g, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scal
                                        float(grad_scale), stream_ptr(stream)), "adam")
 
 
+class AdamSegment(ctypes.Structure):
+    """seg_adam_segment (include/segkern.h)."""
+    _fields_ = [("offset", ctypes.c_longlong), ("rs", ctypes.c_int), ("a", ctypes.c_int), ("b", ctypes.c_int),
+                ("tile_begin", ctypes.c_int), ("rows_dst", ctypes.c_void_p), ("rows_ap", ctypes.c_int),
+                ("rows_bp", ctypes.c_int), ("tr_dst", ctypes.c_void_p), ("tr_ap", ctypes.c_int),
+                ("tr_bp", ctypes.c_int)]
+
+
+class AdamPlan:
+    """Device-resident segment table for adam_tf1_pack.  `segments` is a list of
+    (offset, rs, a, b, rows, tr) with rows / tr = (tensor, a_pad, b_pad) or None;
+    the tensors are kept alive by the plan."""
+
+    def __init__(self, segments, device):
+        arr = (AdamSegment * len(segments))()
+        self.keep = []
+        for i, (off, rs, a, b, rows, tr) in enumerate(segments):
+            e = arr[i]
+            e.offset, e.rs, e.a, e.b = off, rs, a, b
+            if rows is not None:
+                e.rows_dst, e.rows_ap, e.rows_bp = ptr(rows[0]), rows[1], rows[2]
+                self.keep.append(rows[0])
+            if tr is not None:
+                e.tr_dst, e.tr_ap, e.tr_bp = ptr(tr[0]), tr[1], tr[2]
+                self.keep.append(tr[0])
+        total = _lib.lib().seg_adam_segments_plan(ctypes.byref(arr), len(segments))
+        if total <= 0:
+            raise ValueError(f"adam segment plan failed ({total})")
+        self.total_tiles = total
+        self.nsegs = len(segments)
+        raw = bytes(memoryview(arr).cast("B"))
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+
+def adam_tf1_pack(p, g, m, v, plan, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0,
+                  dtype=BF16, stream=None):
+    """TF1 Adam over every planned variable + packed compute copies (one launch)."""
+    check(_lib.lib().seg_adam_tf1_pack(ptr(p), ptr(g), ptr(m), ptr(v), ptr(plan.table), plan.nsegs,
+                                       plan.total_tiles, float(lr), float(beta1), float(beta2), float(eps),
+                                       int(t), float(grad_scale), int(dtype), stream_ptr(stream)), "adam_pack")
+
+
 def fill(y, value, stream=None):
     check(_lib.lib().seg_fill(ptr(y), y.numel(), float(value), seg_dtype(y), stream_ptr(stream)),
           "fill")

@@ -67,6 +67,8 @@ class Session:
         self.dp = data_parallel
         self.run_count = 0
         self._packed_version = -1
+        self._adam_key = None
+        self._adam = None
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
 
     # ------------------------------------------------------------------ vars
@@ -398,7 +400,7 @@ class Session:
                 R, S, A, B = store.by_name[name].shape
                 t = torch.zeros(ops.packed_shape(R, S, A, B, mode), dtype=self.tdt, device=dev)
                 store.packed[(name, mode)] = (t, round8(A), round8(B))
-        self._packed_version = -1
+                self._packed_version = -1          # new copies must be filled
         # gradient buffers / plan for backward
         if p.train:
             self._plan_backward(p)
@@ -439,6 +441,35 @@ class Session:
         for (name, mode), (t, ap, bp) in store.packed.items():
             ops.pack_filter(store.param(name), t, ap, bp, mode)
         self._packed_version = store.version
+
+    def _adam_plan(self):
+        """Segment table of the fused Adam + pack launch: every variable of the
+        store, with the packed copies that exist (rebuilt when packs are added)."""
+        store = self.store
+        key = (len(store.packed), store.numel)
+        if self._adam_key == key:
+            return self._adam
+        segs = []
+        for v in store.order:
+            shape = tuple(v.shape)
+            n = int(np.prod(shape))
+            if len(shape) == 4:
+                rs, a, b = shape[0] * shape[1], shape[2], shape[3]
+            else:
+                rs, a, b = 1, 1, n
+            rows = tr = None
+            for mode in (ops.PACK_KRSC, ops.PACK_HWIO, ops.PACK_TCONV_FWD, ops.PACK_TCONV_BWD):
+                e = store.packed.get((v.var_name, mode))
+                if e is None:
+                    continue
+                if mode in (ops.PACK_HWIO, ops.PACK_TCONV_FWD):
+                    rows = e
+                else:
+                    tr = e
+            segs.append((store.offset[v.var_name], rs, a, b, rows, tr))
+        self._adam = ops.AdamPlan(segs, self.device)
+        self._adam_key = key
+        return self._adam
 
     def _feed(self, p, feed_dict):
         feeds = {id(k): v for k, v in feed_dict.items()}
@@ -543,9 +574,13 @@ class Session:
                 self.dp.finish()
                 gs = gs / self.dp.world
             store.step += 1
-            ops.adam_tf1_step(store.params, store.grads, store.m, store.v, opt.lr, store.step,
-                              opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs)
+            fresh = self._packed_version == store.version
+            ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(), opt.lr,
+                              store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
+                              dtype=ops.BF16 if self.tdt == torch.bfloat16 else ops.F32)
             store.version += 1
+            if fresh:           # the fused update rewrote every packed copy
+                self._packed_version = store.version
         # ---------------- fetch values
         for f in p.fetches:
             if isinstance(f, G.Op):

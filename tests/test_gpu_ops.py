@@ -401,3 +401,58 @@ def test_resize_bilinear(dev):
     torch.cuda.synchronize()
     assert_close(yd.double().cpu(), y.detach(), torch.float32, "resize fwd", 1e-5)
     assert_close(dxd.double().cpu(), x.grad, torch.float32, "resize bwd", 1e-5)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_adam_tf1_pack_matches_step_plus_pack(dev, dtype):
+    """Fused multi-tensor Adam + packed copies == adam_tf1_step then pack_filter.
+    params / m / v: same TF1 expression, FMA contraction may differ between the
+    two kernels -> 2e-6 relative; packed copies: bitwise equal to pack_filter
+    of the fused kernel's own params (incl. untouched zero padding)."""
+    g = torch.Generator().manual_seed(11)
+    # (shape, modes): conv1_1-like padded C, ragged 64-tiles, tconv, biases
+    spec = [((3, 3, 3, 64), (ops.PACK_KRSC,)),
+            ((3, 3, 72, 136), (ops.PACK_KRSC, ops.PACK_HWIO)),
+            ((4, 4, 2, 64), (ops.PACK_TCONV_FWD, ops.PACK_TCONV_BWD)),
+            ((64,), ()), ((2,), ()), ((1, 1, 40, 2), (ops.PACK_KRSC, ops.PACK_HWIO))]
+    offs, off = [], 0
+    for shape, _ in spec:
+        offs.append(off)
+        off += (int(np.prod(shape)) + 3) // 4 * 4
+    P = (torch.randn(off, generator=g) * 0.1).to(dev)
+    Gr = (torch.randn(off, generator=g) * 0.01).to(dev)
+    M = (torch.randn(off, generator=g) * 0.001).to(dev)
+    V = (torch.rand(off, generator=g) * 1e-4).to(dev)
+    ref = [t.clone() for t in (P, Gr, M, V)]
+    copies, ref_copies, segs = [], [], []
+    for (shape, modes), o in zip(spec, offs):
+        rows = tr = None
+        if len(shape) == 4:
+            R, S, A, B = shape
+            for mode in modes:
+                t = torch.zeros(ops.packed_shape(R, S, A, B, mode), dtype=dtype, device=dev)
+                e = (t, ops.round8(A), ops.round8(B))
+                if mode in (ops.PACK_HWIO, ops.PACK_TCONV_FWD):
+                    rows = e
+                else:
+                    tr = e
+                copies.append((t, shape, o, mode))
+            rs, a, b = R * S, A, B
+        else:
+            rs, a, b = 1, 1, int(np.prod(shape))
+        segs.append((o, rs, a, b, rows, tr))
+    plan = ops.AdamPlan(segs, dev)
+    kw = dict(beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=9.0)
+    for step in (1, 2):
+        ops.adam_tf1_pack(P, Gr, M, V, plan, 1e-3, step, dtype=DT[dtype], **kw)
+        ops.adam_tf1_step(*ref, 1e-3, step, **kw)
+    torch.cuda.synchronize()
+    for a_, b_ in zip((P, M, V), (ref[0], ref[2], ref[3])):
+        torch.testing.assert_close(a_, b_, rtol=2e-6, atol=1e-12)
+    for t, shape, o, mode in copies:
+        R, S, A, B = shape
+        src = P[o:o + R * S * A * B].view(R, S, A, B).contiguous()
+        want = torch.zeros_like(t)
+        ops.pack_filter(src, want, ops.round8(A), ops.round8(B), mode)
+        torch.cuda.synchronize()
+        assert torch.equal(t, want), f"copy mode {mode} of {shape}"

@@ -21,7 +21,8 @@ class _Rec:
     def __getattr__(self, name):
         real_fn = getattr(self.real, name)
         host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
-                             "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string")
+                             "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
+                             "seg_adam_segments_plan")
 
         def fn(*a):
             if host_only:
@@ -68,17 +69,37 @@ def test_fcn_train_plan(dry):
     assert c.count("seg_tconv2d_bwd_data") == 3
     assert c.count("seg_tconv2d_bwd_filter") == 3
     assert c.count("seg_maxpool2x2_bwd") == 5
-    assert c.count("seg_adam_tf1_step") == 1
+    assert c.count("seg_adam_tf1_pack") == 1          # one fused multi-tensor launch
     # skip fusion: pool3/pool4 gradients = sum of two consumers
     assert c.count("seg_add") == 2
     # filter copies are packed once per update (first run) -- KRSC for all 17 convs,
     # HWIO for the 16 with input grads, 2 layouts x 3 tconvs
     assert c.count("seg_pack_filter") == 17 + 16 + 6
-    assert c.index("seg_adam_tf1_step") > c.index("seg_conv2d_bwd_filter")
+    assert c.index("seg_adam_tf1_pack") > c.index("seg_conv2d_bwd_filter")
     dry.calls.clear()
     sess.run(train, feed_dict={image: img, labels: lab, keep: 1.0})
-    assert dry.calls.count("seg_pack_filter") == 17 + 16 + 6   # repack after the Adam update
+    # the fused Adam launch rewrote every packed copy: no repack pass
+    assert dry.calls.count("seg_pack_filter") == 0
+    assert dry.calls.count("seg_adam_tf1_pack") == 1
+    # the segment table covers every variable once, with both copies of each conv
+    plan = sess._adam
+    assert plan.nsegs == len(sess.store.vars)
     assert dry.calls.count("seg_conv2d_fwd") == 17
+
+
+def test_adam_segment_plan_host():
+    """seg_adam_segments_plan: tile prefix over 64x64 [a][b] tiles per rs slice."""
+    lib = _lib.load()
+    arr = (ops.AdamSegment * 3)()
+    for e, (rs, a, b) in zip(arr, [(9, 3, 64), (1, 1, 130), (49, 512, 4096)]):
+        e.rs, e.a, e.b = rs, a, b
+    import ctypes
+    total = lib.seg_adam_segments_plan(ctypes.byref(arr), 3)
+    assert [e.tile_begin for e in arr] == [0, 9, 9 + 3]
+    assert total == 9 + 3 + 49 * 8 * 64
+    assert ctypes.sizeof(ops.AdamSegment) == 56
+    bad = (ops.AdamSegment * 1)()
+    assert lib.seg_adam_segments_plan(ctypes.byref(bad), 1) < 0      # rs = 0
 
 
 def test_inference_plan_has_no_backward(dry):
