@@ -61,7 +61,12 @@ typedef struct seg_conv_desc {
 /* Epilogue fused into a convolution's output write:
  *   v = acc * scale[k] + shift[k] (+ bias[k]);  v = relu(v) if relu;
  *   v = v / keep_prob * floor(keep_prob + U) if keep_prob < 1 (TF1 dropout);
- *   v += residual[pixel, k]  (tf.add skip fusion)                          */
+ *   v += residual[pixel, k]  (tf.add skip fusion);
+ *   v = relu_mask[pixel, k] > 0 ? v * mask_scale : 0   (if relu_mask)
+ * The last step is ReluGrad (x dropout's 1/keep_prob) of the layer that
+ * produced this op's input, fused into Conv2DBackpropInput / the tconv input
+ * gradient: relu_mask is that layer's (post-ReLU/dropout) output, laid out
+ * like the gradient being written (ld_relu_mask 0 = same stride).           */
 typedef struct seg_epilogue {
     const float* bias;
     const float* scale;
@@ -71,6 +76,9 @@ typedef struct seg_epilogue {
     int relu;
     float keep_prob;
     uint64_t seed;
+    const void* relu_mask;
+    int ld_relu_mask;
+    float mask_scale;
 } seg_epilogue;
 
 /* ---- descriptor helpers ------------------------------------------------ */
@@ -91,11 +99,13 @@ int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_krsc,
 /* Conv2DBackpropInput.  w_hwio: packed filter [R][S][C][K] in `dtype`
  * (seg_pack_filter mode 1).  dx may be a channel-slice view (ldx). */
 int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,
-                        void* dx, void* ws, size_t ws_bytes, void* stream);
+                        const seg_epilogue* epi, void* dx, void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropFilter: dw_f32 is the fp32 master-gradient layout
- * [R][S][c_valid][k_valid]; written (not accumulated). */
+ * [R][S][c_valid][k_valid]; written (not accumulated).  dbias (optional):
+ * BiasAddGrad of the same dy, dbias[k] = sum over pixels of dy[p][k]
+ * (k < k_valid) -- summed inside the filter-gradient kernel when it can. */
 int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
-                          float* dw_f32, void* ws, size_t ws_bytes, void* stream);
+                          float* dw_f32, float* dbias, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- conv2d_transpose (Network/model/FCN.py:155, :106; utils.py:272) ---- */
 /* w_rskc: packed filter [R][S][K][C] in `dtype` (TF layout, seg_pack_filter mode 2). */
@@ -104,10 +114,10 @@ int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_rskc,
 /* Gradient w.r.t. the tconv input = strided Conv2D of dy.  w_crsk: packed
  * [C][R][S][K] (seg_pack_filter mode 3). */
 int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_crsk,
-                         void* dx, void* ws, size_t ws_bytes, void* stream);
-/* Filter gradient in TF layout [R][S][k_valid][c_valid], fp32. */
+                         const seg_epilogue* epi, void* dx, void* ws, size_t ws_bytes, void* stream);
+/* Filter gradient in TF layout [R][S][k_valid][c_valid], fp32; dbias as above. */
 int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
-                           float* dw_f32, void* ws, size_t ws_bytes, void* stream);
+                           float* dw_f32, float* dbias, void* ws, size_t ws_bytes, void* stream);
 
 /* Workspace bytes for op: 0 fwd, 1 bwd_data, 2 bwd_filter, 3 tconv fwd,
  * 4 tconv bwd_data, 5 tconv bwd_filter. */
@@ -150,9 +160,11 @@ size_t seg_bias_grad_workspace(long P, int K);
 int seg_maxpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy,
                        int dtype, void* stream);
 /* dx (dense [N,H,W,C], ldx) is fully written; routes dy to the first max
- * in row-major window order (TF CPU MaxPoolGrad tie rule). */
+ * in row-major window order (TF CPU MaxPoolGrad tie rule).  relu_mask != 0
+ * also applies ReluGrad of the (post-ReLU) pool input x: the routed value is
+ * kept only where that max is > 0. */
 int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H,
-                       int W, int C, int ldx, int ldy, int dtype, void* stream);
+                       int W, int C, int ldx, int ldy, int relu_mask, int dtype, void* stream);
 int seg_avgpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy,
                        int dtype, void* stream);
 int seg_avgpool2x2_bwd(const void* dy, void* dx, int N, int H, int W, int C, int ldx, int ldy,

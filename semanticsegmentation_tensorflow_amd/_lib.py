@@ -77,7 +77,8 @@ class SegConvDesc(ctypes.Structure):
 class SegEpilogue(ctypes.Structure):
     _fields_ = [("bias", ctypes.c_void_p), ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
                 ("residual", ctypes.c_void_p), ("ld_residual", ctypes.c_int), ("relu", ctypes.c_int),
-                ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64)]
+                ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64), ("relu_mask", ctypes.c_void_p),
+                ("ld_relu_mask", ctypes.c_int), ("mask_scale", ctypes.c_float)]
 
 
 _P = ctypes.c_void_p
@@ -93,11 +94,11 @@ SIGNATURES = {
     "seg_conv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "seg_tconv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "seg_conv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
-    "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
-    "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
-    "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
-    "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _Z, _P]),
+    "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_conv_workspace": (_Z, [_DP, _I]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
@@ -106,7 +107,7 @@ SIGNATURES = {
     "seg_bias_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _F, _I, _P, _Z, _P]),
     "seg_bias_grad_workspace": (_Z, [_L, _I]),
     "seg_maxpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "seg_maxpool2x2_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_maxpool2x2_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_avgpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_avgpool2x2_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_add": (_I, [_P, _P, _P, _L, _I, _P]),

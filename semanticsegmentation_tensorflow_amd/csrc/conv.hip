@@ -86,14 +86,21 @@ extern "C" int seg_tconv_desc_init(seg_conv_desc* d, int N, int H, int W, int C,
     return SEG_OK;
 }
 
-static seg::EpiParams make_epi(const seg_epilogue* e, int n_valid, long res_img) {
+static seg::EpiParams make_epi(const seg_epilogue* e, int n_valid, long res_img, long pix_per_img = 0, int ld_out = 0) {
     seg::EpiParams r = {};
     r.n_valid = n_valid;
     r.keep_prob = 1.f;
+    r.mask_scale = 1.f;
     if (e) {
         r.bias = e->bias; r.scale = e->scale; r.shift = e->shift;
         r.residual = e->residual; r.ld_res = e->ld_residual; r.res_img = res_img;
         r.relu = e->relu; r.keep_prob = e->keep_prob > 0.f ? e->keep_prob : 1.f; r.seed = e->seed;
+        if (e->relu_mask) {
+            r.mask = e->relu_mask;
+            r.ld_mask = e->ld_relu_mask > 0 ? e->ld_relu_mask : ld_out;
+            r.mask_img = pix_per_img * r.ld_mask;
+            r.mask_scale = e->mask_scale != 0.f ? e->mask_scale : 1.f;
+        }
     }
     return r;
 }
@@ -244,11 +251,15 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
             seg::WgradPlan wp;
             if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp))
                 need = std::max(need, seg::wgrad_workspace(wp, p));
-            return need;
+            return std::max(need, seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
         }
         case 3: return tconv_use_gemm(d) ? tconv_gemm_ws(d) : 0;
         case 4: { NTParams p = tconv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
-        case 5: { TNParams p = tconv_bwd_filter_params(d); return seg::tn_workspace(p.M, p.N, p.P, d->dtype); }
+        case 5: {
+            TNParams p = tconv_bwd_filter_params(d);
+            return std::max(seg::tn_workspace(p.M, p.N, p.P, d->dtype),
+                            seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
+        }
     }
     return 0;
 }
@@ -371,25 +382,39 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, void* dx, void* ws,
-                                   size_t ws_bytes, void* stream) {
+extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, const seg_epilogue* epi,
+                                   void* dx, void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);
     if (st) return st;
     if (!dy || !w || !dx) return SEG_EINVAL;
     if (d->stride_h != 1 || d->stride_w != 1) return SEG_EINVAL;  // FCN / FC-DenseNet convs are stride 1
     NTParams p = conv_bwd_data_params(d);
     p.x = dy; p.w = w; p.y = dx;
+    if (epi) {
+        const int ldr = epi->ld_residual ? epi->ld_residual : d->ldx;
+        p.epi = make_epi(epi, d->C, (long)d->H * d->W * ldr, (long)d->H * d->W, d->ldx);
+        if (epi->residual && epi->ld_residual == 0) p.epi.ld_res = d->ldx;
+    }
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
-                                     size_t ws_bytes, void* stream) {
+// BiasAddGrad of dy [N*OH*OW][K] when the filter-gradient kernel did not fuse it.
+static int bias_grad_fallback(const seg_conv_desc* d, const void* dy, float* dbias, void* ws, size_t ws_bytes,
+                              void* stream) {
+    return seg_bias_relu_bwd(dy, d->ldy, nullptr, 0, const_cast<void*>(dy), d->ldy, dbias,
+                             (long)d->N * d->OH * d->OW, d->K, d->k_valid, 0, 1.f, d->dtype, ws, ws_bytes, stream);
+}
+
+extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias,
+                                     void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);
     if (st) return st;
     if (!x || !dy || !dw) return SEG_EINVAL;
     TNParams p = conv_bwd_filter_params(d);
-    p.x = x; p.b = dy; p.out = dw;
-    return seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+    p.x = x; p.b = dy; p.out = dw; p.dbias = dbias;
+    st = seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+    if (st || !p.dbias) return st;
+    return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
 }
 
 extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
@@ -436,24 +461,31 @@ extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void
     return seg::launch_nt(p, d->dtype, d->stride_h * d->stride_w, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, void* dx, void* ws,
-                                    size_t ws_bytes, void* stream) {
+extern "C" int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, const seg_epilogue* epi,
+                                    void* dx, void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);
     if (st) return st;
     if (!dy || !w || !dx) return SEG_EINVAL;
     NTParams p = tconv_bwd_data_params(d);
     p.x = dy; p.w = w; p.y = dx;
+    if (epi) {
+        const int ldr = epi->ld_residual ? epi->ld_residual : d->ldx;
+        p.epi = make_epi(epi, d->C, (long)d->H * d->W * ldr, (long)d->H * d->W, d->ldx);
+        if (epi->residual && epi->ld_residual == 0) p.epi.ld_res = d->ldx;
+    }
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
-                                      size_t ws_bytes, void* stream) {
+extern "C" int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw,
+                                      float* dbias, void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);
     if (st) return st;
     if (!x || !dy || !dw) return SEG_EINVAL;
     TNParams p = tconv_bwd_filter_params(d);
-    p.x = dy; p.b = x; p.out = dw;
-    return seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+    p.x = dy; p.b = x; p.out = dw;          // dy is the gathered operand here: bias via the fallback
+    st = seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+    if (st || !dbias) return st;
+    return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
 }
 
 // ---------------------------------------------------------------------------

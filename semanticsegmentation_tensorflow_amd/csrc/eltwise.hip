@@ -149,7 +149,7 @@ __global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N,
 // (odd H / W) receive zero gradient.
 template <typename T>
 __global__ void maxpool_bwd_k(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, int N, int H,
-                              int W, int C, int ldx, int ldy) {
+                              int W, int C, int ldx, int ldy, int relu) {
     constexpr int EPC = dt_traits<T>::EPC;
     const int OH = H / 2, OW = W / 2, BH = (H + 1) / 2, BW = (W + 1) / 2, CK = C / EPC;
     const long total = (long)N * BH * BW * CK;
@@ -180,8 +180,10 @@ __global__ void maxpool_bwd_k(const T* __restrict__ x, const T* __restrict__ dy,
                 if (v[1][e] > m) { m = v[1][e]; a = 1; }
                 if (v[2][e] > m) { m = v[2][e]; a = 2; }
                 if (v[3][e] > m) { m = v[3][e]; a = 3; }
+                // relu: ReluGrad of the post-ReLU input -> nothing flows where the max is 0
+                const float g = (relu && !(m > 0.f)) ? 0.f : d[e];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q][e] = (q == a) ? d[e] : 0.f;
+                for (int q = 0; q < 4; ++q) o[q][e] = (q == a) ? g : 0.f;
             }
         }
         const bool h1 = 2 * bh + 1 < H, w1 = 2 * bw + 1 < W;
@@ -644,12 +646,13 @@ extern "C" int seg_maxpool2x2_fwd(const void* x, void* y, int N, int H, int W, i
 }
 
 extern "C" int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H, int W, int C,
-                                  int ldx, int ldy, int dtype, void* stream) {
+                                  int ldx, int ldy, int relu_mask, int dtype, void* stream) {
     (void)y;
     if (!x || !dy || !dx || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2) return SEG_EINVAL;
     const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / epc_of(dtype));
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
-                                         (hipStream_t)stream, (const T*)x, (const T*)dy, (T*)dx, N, H, W, C, ldx, ldy));
+                                         (hipStream_t)stream, (const T*)x, (const T*)dy, (T*)dx, N, H, W, C, ldx, ldy,
+                                         relu_mask));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

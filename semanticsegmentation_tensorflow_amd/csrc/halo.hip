@@ -257,7 +257,12 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
         const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        float res[8];
+        float res[8], mk[8];
+        if (e.mask) {
+            const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
+        }
         if (e.residual) {
             const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
@@ -270,6 +275,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             if (e.relu) x = fmaxf(x, 0.f);
             if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
             if (e.residual) x += res[j];
+            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = col < e.n_valid ? x : 0.f;
         }
         T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
@@ -559,7 +565,11 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
             const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
             float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-            float res[8];
+            float res[8], mk[8];
+            if (e.mask) {
+                const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
+            }
             if (e.residual) {
                 const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
@@ -572,6 +582,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 if (e.relu) x = fmaxf(x, 0.f);
                 if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
                 if (e.residual) x += res[j];
+            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
             }
             T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;

@@ -15,6 +15,12 @@ struct EpiParams {
     float keep_prob;
     uint64_t seed;
     int n_valid;      // columns >= n_valid are written as 0 (padding channels)
+    // ReluGrad of the layer that produced this op's input (gradient kernels):
+    // v = mask[pixel, col] > 0 ? v * mask_scale : 0
+    const void* mask;
+    long mask_img;
+    int ld_mask;
+    float mask_scale;
 };
 
 // C[m][n] = sum_k A[m][k] B[n][k].  Row m -> (img, a, b) on an Ha x Wa grid;
@@ -59,6 +65,11 @@ struct TNParams {
     int c_valid, n_valid;
     float* partial;
     int kt_per_split;
+    // BiasAddGrad fused into the filter gradient: dbias[n] = sum_p b[p][n]
+    // (kernels that support it clear the pointer after launching); split-K
+    // slabs then carry it as an extra row M, so slabs hold Mp = M + 1 rows.
+    float* dbias;
+    int Mp;
 };
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);

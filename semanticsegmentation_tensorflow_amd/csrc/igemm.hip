@@ -38,7 +38,7 @@ __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<
 // NT epilogue, split into a per-row part (one pixel decomposition) and a
 // per-element part; used by the v1 GEMM and by the split-K reducer.
 struct NtRow {
-    long yoff, roff;
+    long yoff, roff, moff;
     uint64_t gidx;   // dropout counter base: (img*OH*OW + pix) * n_valid
 };
 
@@ -52,18 +52,23 @@ __device__ __forceinline__ NtRow nt_row(const NTParams& p, int row, int Ha, int 
     NtRow r;
     r.yoff = img * p.y_img + pix * p.ldy;
     r.roff = img * p.epi.res_img + pix * p.epi.ld_res;
+    r.moff = img * p.epi.mask_img + pix * p.epi.ld_mask;
     r.gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * p.epi.n_valid;
     return r;
 }
 
-__device__ __forceinline__ float nt_apply(const EpiParams& e, const NtRow& r, int col, float v, float res) {
+// mk: the ReLU-mask value (e.mask) at (pixel, col), 1 when unused
+__device__ __forceinline__ float nt_apply(const EpiParams& e, const NtRow& r, int col, float v, float res,
+                                          float mk = 1.f) {
     if (col >= e.n_valid) return 0.f;
     if (e.scale) v *= e.scale[col];
     if (e.shift) v += e.shift[col];
     if (e.bias) v += e.bias[col];
     if (e.relu) v = fmaxf(v, 0.f);
     if (e.keep_prob < 1.f) v = (v / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, r.gidx + col));
-    return v + res;
+    v += res;
+    if (e.mask) v = mk > 0.f ? v * e.mask_scale : 0.f;
+    return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -273,12 +278,14 @@ __global__ __launch_bounds__(256) void igemm_nt(NTParams p) {
             const NtRow rw = nt_row(p, row, Ha, Wa, ooh, oow);
             T* yrow = reinterpret_cast<T*>(p.y) + rw.yoff;
             const T* rrow = reinterpret_cast<const T*>(p.epi.residual) + rw.roff;
+            const T* mrow = reinterpret_cast<const T*>(p.epi.mask) + rw.moff;
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const int col = n0 + wn * WTN + ni * 16 + fr;
                 if (col >= p.N) continue;
                 const float res = p.epi.residual ? to_f32(rrow[col]) : 0.f;
-                yrow[col] = from_f32<T>(nt_apply(p.epi, rw, col, acc[mi][ni][r], res));
+                const float mk = p.epi.mask ? to_f32(mrow[col]) : 1.f;
+                yrow[col] = from_f32<T>(nt_apply(p.epi, rw, col, acc[mi][ni][r], res, mk));
             }
         }
 }
@@ -303,13 +310,19 @@ __global__ void splitk_reduce_nt(NTParams p, int splits) {
         }
         const NtRow rw = nt_row(p, row, p.Ha, p.Wa, p.ooh, p.oow);
         float res[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
         if (p.epi.residual) {
             const T* rp = reinterpret_cast<const T*>(p.epi.residual) + rw.roff + col0;
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), res + 4);
         }
+        if (p.epi.mask) {
+            const T* mp = reinterpret_cast<const T*>(p.epi.mask) + rw.moff + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = nt_apply(p.epi, rw, col0 + j, v[j], res[j]);
+        for (int j = 0; j < 8; ++j) v[j] = nt_apply(p.epi, rw, col0 + j, v[j], res[j], mk[j]);
         T* yp = reinterpret_cast<T*>(p.y) + rw.yoff + col0;
         *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
         if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
@@ -526,7 +539,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
             const int m = m0 + wm * WTM + mi * 16 + fg * 4 + r;
             if (m >= p.M) continue;
             if (p.partial) {
-                float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
+                float* prow = p.partial + ((long)blockIdx.z * p.Mp + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
                     const int n = n0 + wn * WTN + ni * 16 + fr;
@@ -547,21 +560,38 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
 
 __global__ void splitk_reduce_tn(TNParams p, int splits) {
     const int c4 = p.N / 4;
-    const long total = (long)p.M * c4;
-    const long slab = (long)p.M * p.N;
+    const long total = (long)p.Mp * c4;
+    const long slab = (long)p.Mp * p.N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int m = (int)(i / c4);
         const int n0 = (int)(i - (long)m * c4) * 4;
         float4 s = {0.f, 0.f, 0.f, 0.f};
         const float* src = p.partial + (long)m * p.N + n0;
-        for (int z = 0; z < splits; ++z) {
+        int z = 0;
+        for (; z + 4 <= splits; z += 4) {   // 4 independent slab loads in flight
+            const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
+            const float4 b = *reinterpret_cast<const float4*>(src + (z + 1) * slab);
+            const float4 c = *reinterpret_cast<const float4*>(src + (z + 2) * slab);
+            const float4 d = *reinterpret_cast<const float4*>(src + (z + 3) * slab);
+            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+            s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+            s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+            s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+        }
+        for (; z < splits; ++z) {
             const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
             s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        }
+        const float vv[4] = {s.x, s.y, s.z, s.w};
+        if (m == p.M) {               // fused BiasAddGrad row
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (n0 + j < p.n_valid) p.dbias[n0 + j] = vv[j];
+            continue;
         }
         bool ok;
         float* orow = tn_row(p, m, ok);
         if (!ok) continue;
-        const float vv[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (n0 + j < p.n_valid) orow[(long)(n0 + j) * p.o_n] = vv[j];
@@ -728,8 +758,10 @@ template <typename T>
 static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
     p.partial = nullptr;
+    p.Mp = p.M;
     WgradPlan wp;
     if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
+        if (p.dbias) p.Mp = p.M + 1;          // wgrad_halo sums dy columns too
         if (wp.splits > 1) {
             if (!ws || ws_bytes < wgrad_workspace(wp, p)) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
@@ -737,11 +769,12 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         launch_wgrad(p, wp, s);
         SEG_CHECK_LAUNCH();
         if (p.partial) {
-            const long total = (long)p.M * (p.N / 4);
+            const long total = (long)p.Mp * (p.N / 4);
             hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, wp.splits);
             SEG_CHECK_LAUNCH();
             p.partial = nullptr;
         }
+        p.dbias = nullptr;                    // done
         return SEG_OK;
     }
     int bm, bn, splits;

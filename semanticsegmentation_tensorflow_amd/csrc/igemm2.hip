@@ -276,7 +276,12 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
         const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
         const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        float res[8];
+        float res[8], mk[8];
+        if (e.mask) {
+            const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
+        }
         if (e.residual) {
             const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
@@ -290,6 +295,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
             if (e.relu) x = fmaxf(x, 0.f);
             if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
             if (e.residual) x += res[j];
+            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = col < e.n_valid ? x : 0.f;
         }
         T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
@@ -465,7 +471,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
             const int m = m0 + wm * WTM + mi * 16 + fg * 4 + r;
             if (m >= p.M) continue;
             if (p.partial) {
-                float* prow = p.partial + ((long)split * p.M + m) * p.N;
+                float* prow = p.partial + ((long)split * p.Mp + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
                     const int n = n0 + wn * WTN + ni * 16 + fr;

@@ -128,6 +128,12 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fused BiasAddGrad: the first channel chunk's cf == 0 waves sum their dy
+    // fragments (8 pixels x column fr per lane and substep)
+    const bool do_bias = p.dbias != nullptr && ct == 0 && cf == 0;
+    float dsum[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) dsum[j] = 0.f;
 
     const int fg = lane >> 4, tq = (lane & 15) >> 2, tpp = lane & 3;
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -176,6 +182,11 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 bfr[ni] = __builtin_bit_cast(bf16x8, v);
+                if (do_bias) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                }
             }
             const int hbase = py * g.hwd + px;
             const int achk = cf * 2 + (tpp >> 1);
@@ -198,6 +209,24 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     }
 
     const int fr = lane & 15;
+    if (do_bias) {
+#pragma unroll
+        for (int ni = 0; ni < NF; ++ni) {
+            dsum[ni] += __shfl_xor(dsum[ni], 16);
+            dsum[ni] += __shfl_xor(dsum[ni], 32);
+        }
+        if (fg == 0) {
+#pragma unroll
+            for (int ni = 0; ni < NF; ++ni) {
+                const int n = n0 + nh * (NT / 2) + ni * 16 + fr;
+                if (p.partial) {
+                    if (n < p.N) p.partial[((long)split * p.Mp + p.M) * p.N + n] = dsum[ni];
+                } else if (n < p.n_valid) {
+                    p.dbias[n] = dsum[ni];
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
@@ -205,7 +234,7 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             const int c = c0 + cf * 16 + fg * 4 + j;
             const int m = tap * p.Cg + c;
             if (p.partial) {
-                float* prow = p.partial + ((long)split * p.M + m) * p.N;
+                float* prow = p.partial + ((long)split * p.Mp + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     const int n = n0 + nh * (NT / 2) + ni * 16 + fr;
@@ -261,7 +290,8 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
 }
 
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p) {
-    return wp.splits > 1 ? (size_t)wp.splits * p.M * p.N * sizeof(float) : 0;
+    // +1 slab row for the fused BiasAddGrad
+    return wp.splits > 1 ? (size_t)wp.splits * (p.M + 1) * p.N * sizeof(float) : 0;
 }
 
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s) {

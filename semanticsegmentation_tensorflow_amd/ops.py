@@ -88,7 +88,10 @@ def tconv_desc(N, H, W, C, OH, OW, K, R, S, stride, padding="SAME", dtype=BF16):
     return d
 
 
-def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_prob=1.0, seed=0):
+def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_prob=1.0, seed=0,
+             relu_mask=None, mask_scale=1.0):
+    """seg_epilogue.  relu_mask (gradient kernels): the post-ReLU output of the
+    layer whose input gradient is being written; v = mask > 0 ? v*mask_scale : 0."""
     e = SegEpilogue()
     e.bias = None if bias is None else bias.data_ptr()
     e.scale = None if scale is None else scale.data_ptr()
@@ -98,6 +101,9 @@ def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_
     e.relu = 1 if relu else 0
     e.keep_prob = float(keep_prob)
     e.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    e.relu_mask = None if relu_mask is None else relu_mask.data_ptr()
+    e.ld_relu_mask = 0 if relu_mask is None else pixel_stride(relu_mask)
+    e.mask_scale = float(mask_scale)
     return e
 
 
@@ -143,18 +149,23 @@ def conv2d_fwd(desc, x, w_krsc, y, epi=None, ws=None, stream=None):
     return y
 
 
-def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None):
+def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None, epi=None):
+    """Conv2DBackpropInput; epi (e.g. epilogue(relu_mask=y_prev)) fuses the
+    ReluGrad of the layer that produced this conv's input."""
     d = _with_ld(desc, dx, dy)
     wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_BWD_DATA))
-    check(_lib.lib().seg_conv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_hwio), ptr(dx), wsp, wss,
+    check(_lib.lib().seg_conv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_hwio),
+                                         None if epi is None else ctypes.byref(epi), ptr(dx), wsp, wss,
                                          stream_ptr(stream)), "conv2d_backprop_input")
     return dx
 
 
-def conv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None):
+def conv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None, dbias=None):
+    """Conv2DBackpropFilter (+ BiasAddGrad of dy into dbias when given)."""
     d = _with_ld(desc, x, dy)
     wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_BWD_FILTER))
-    check(_lib.lib().seg_conv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw), wsp, wss,
+    check(_lib.lib().seg_conv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw),
+                                           None if dbias is None else ptr(dbias), wsp, wss,
                                            stream_ptr(stream)), "conv2d_backprop_filter")
     return dw
 
@@ -168,18 +179,20 @@ def tconv2d_fwd(desc, x, w_rskc, y, epi=None, ws=None, stream=None):
     return y
 
 
-def tconv2d_bwd_data(desc, dy, w_crsk, dx, ws=None, stream=None):
+def tconv2d_bwd_data(desc, dy, w_crsk, dx, ws=None, stream=None, epi=None):
     d = _with_ld(desc, dx, dy)
     wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_TBWD_DATA))
-    check(_lib.lib().seg_tconv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_crsk), ptr(dx), wsp, wss,
+    check(_lib.lib().seg_tconv2d_bwd_data(ctypes.byref(d), ptr(dy), ptr(w_crsk),
+                                          None if epi is None else ctypes.byref(epi), ptr(dx), wsp, wss,
                                           stream_ptr(stream)), "conv2d_transpose_grad_input")
     return dx
 
 
-def tconv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None):
+def tconv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None, dbias=None):
     d = _with_ld(desc, x, dy)
     wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_TBWD_FILTER))
-    check(_lib.lib().seg_tconv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw), wsp, wss,
+    check(_lib.lib().seg_tconv2d_bwd_filter(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw),
+                                            None if dbias is None else ptr(dbias), wsp, wss,
                                             stream_ptr(stream)), "conv2d_transpose_grad_filter")
     return dw
 
@@ -226,11 +239,12 @@ def maxpool2x2_fwd(x, y, stream=None):
     return y
 
 
-def maxpool2x2_bwd(x, y, dy, dx, stream=None):
+def maxpool2x2_bwd(x, y, dy, dx, stream=None, relu_mask=False):
+    """MaxPoolGrad; relu_mask=True also applies ReluGrad of the post-ReLU input x."""
     N, H, W, C = x.shape
     check(_lib.lib().seg_maxpool2x2_bwd(ptr(x), ptr(y), ptr(dy), ptr(dx), N, H, W, C,
-                                        pixel_stride(dx), pixel_stride(dy), seg_dtype(x),
-                                        stream_ptr(stream)), "max_pool_grad")
+                                        pixel_stride(dx), pixel_stride(dy), 1 if relu_mask else 0,
+                                        seg_dtype(x), stream_ptr(stream)), "max_pool_grad")
     return dx
 
 

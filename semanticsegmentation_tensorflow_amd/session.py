@@ -425,6 +425,27 @@ class Session:
                 covered.update([n.gamma.var_name, n.beta.var_name])
             elif n.kind == "BiasAdd":
                 covered.add(n.inputs[1].var_name)
+        # ReluGrad fusion: a ReLU conv whose output has exactly one consumer that
+        # is a conv / tconv (input gradient via the NT epilogue mask) or a
+        # dropout-free max-pool (MaxPoolGrad relu flag) gets its gradient
+        # already masked; it then only needs the bias column sum.
+        p.producer = {id(n.output): n for n in p.nodes}
+        consumers = {}
+        for n in p.nodes:
+            ins = list(n.inputs) + ([n.residual] if getattr(n, "residual", None) is not None else []) \
+                + ([n.labels] if getattr(n, "labels", None) is not None else [])
+            for t in ins:
+                consumers.setdefault(id(t), []).append(n)
+        p.mask_fuse = set()
+        for n in p.nodes:
+            if n.kind != "conv" or not n.relu or id(n.output) not in p.needs_grad:
+                continue
+            cs = consumers.get(id(n.output), [])
+            if len(cs) != 1 or cs[0].inputs[0] is not n.output:
+                continue
+            c = cs[0]
+            if c.kind in ("conv", "tconv") or (c.kind == "MaxPool" and n.kp is None):
+                p.mask_fuse.add(id(n))
         p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
         p.uncovered = [v for v in p.var_names if v not in covered]
         for v in p.uncovered:            # no gradient path: keep the grad slice at 0
@@ -613,6 +634,16 @@ class Session:
         zero = torch.zeros(C, dtype=torch.float32, device=self.device)
         ops.bn_relu_fwd(x, y, one, zero, C, True, eps=0.0)
 
+    def _mask_epi(self, p, x):
+        """Epilogue fusing the ReluGrad (x 1/keep_prob) of x's producer into the
+        input-gradient kernel of x's (only) consumer, or None."""
+        prod = p.producer.get(id(x))
+        if prod is None or id(prod) not in p.mask_fuse:
+            return None
+        kp = prod.kp_val
+        scale = 1.0 / kp if (kp is not None and kp < 1.0) else 1.0
+        return ops.epilogue(relu_mask=p.buf[id(x)], mask_scale=scale)
+
     # ------------------------------------------------------------- backward
     def _backward(self, p, scal):
         buf = p.buf
@@ -662,7 +693,13 @@ class Session:
                 x = n.inputs[0]
                 yb = buf[id(n.output)]
                 dz = dy
-                if n.relu or n.bias is not None:
+                fused_db = None
+                if id(n) in p.mask_fuse or (n.bias is not None and not n.relu):
+                    # gradient arrives masked (or there is no ReLU): BiasAddGrad is
+                    # summed by the filter-gradient launch below
+                    if n.bias is not None:
+                        fused_db = store.grad(n.bias.var_name)
+                elif n.relu or n.bias is not None:
                     scale = 1.0 / n.kp_val if (n.kp_val is not None and n.kp_val < 1.0) else 1.0
                     dz = p.tmp.get(("dz", id(n.output)))
                     if dz is None:
@@ -674,32 +711,35 @@ class Session:
                 if id(x) in ng:
                     dx, acc = dest(x)
                     self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
-                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws)
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
+                                self._mask_epi(p, x))
                     done(dx, acc)
                 self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
-                            store.grad(n.w.var_name), ws)
+                            store.grad(n.w.var_name), ws, None, fused_db)
                 if self.dp is not None:
                     self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "tconv":
                 x = n.inputs[0]
-                if n.bias is not None:
-                    self._bias_relu_bwd(dy, None, dy, store.grad(n.bias.var_name), n.desc.k_valid, False, 1.0)
                 if n.residual is not None:
                     contribute_alias(n.residual, dy)
                 if id(x) in ng:
                     dx, acc = dest(x)
                     self._timed(n.desc, ops.OP_TBWD_DATA, ops.tconv2d_bwd_data, n.desc, dy,
-                                store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws)
+                                store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws, None,
+                                self._mask_epi(p, x))
                     done(dx, acc)
                 self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
-                            store.grad(n.w.var_name), ws)
+                            store.grad(n.w.var_name), ws, None,
+                            store.grad(n.bias.var_name) if n.bias is not None else None)
                 if self.dp is not None:
                     self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
                 if id(x) in ng:
                     dx, acc = dest(x)
-                    ops.maxpool2x2_bwd(buf[id(x)], buf[id(n.output)], dy, dx)
+                    prod = p.producer.get(id(x))
+                    ops.maxpool2x2_bwd(buf[id(x)], buf[id(n.output)], dy, dx,
+                                       relu_mask=prod is not None and id(prod) in p.mask_fuse)
                     done(dx, acc)
             elif k == "AvgPool":
                 x = n.inputs[0]

@@ -97,9 +97,12 @@ def test_conv2d_fwd_bias_relu(dev, ntv, case, dtype):
         assert y[..., K:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("masked", [False, True], ids=["plain", "relu_mask"])
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[7] == 1])
-def test_conv2d_bwd_data(dev, ntv, case, dtype):
+def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
+    """Conv2DBackpropInput; relu_mask: the fused ReluGrad x 1/keep_prob of the
+    layer that produced x (epilogue mask = that layer's post-ReLU output)."""
     N, H, W, C, K, R, S, st, dil, pad = case
     x, w, _ = _conv_case(case, 2)
     wr = rnd(w, dtype)
@@ -112,9 +115,16 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype):
     dyd = to_dev(dy, dtype, dev)
     wh = _pack(w, ops.PACK_HWIO, dtype, dev)
     dx = torch.full((N, H, W, d.C), float("nan"), dtype=dtype, device=dev)
-    ops.conv2d_bwd_data(d, dyd, wh, dx)
+    want = xr.grad
+    epi = None
+    if masked:
+        prev = torch.relu(torch.randn(N, H, W, C, generator=g, dtype=torch.float64))   # ~half zeros
+        prev_d = to_dev(prev, dtype, dev)     # epilogue keeps only the pointer: hold the tensor
+        epi = ops.epilogue(relu_mask=prev_d, mask_scale=1.25)
+        want = torch.where(prev > 0, want * 1.25, torch.zeros_like(want))
+    ops.conv2d_bwd_data(d, dyd, wh, dx, epi=epi)
     torch.cuda.synchronize()
-    assert_close(from_dev(dx, C), xr.grad, dtype, f"conv bwd_data {case}")
+    assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
 @pytest.fixture(params=[1, 2, 3, 4], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128"])
@@ -147,10 +157,13 @@ def test_conv2d_bwd_filter(dev, tnv, case, dtype):
     (y * dy).sum().backward()
     d = ops.conv_desc(N, H, W, C, K, R, S, st, dil, pad, DT[dtype])
     dw = torch.full((R, S, C, K), float("nan"), dtype=torch.float32, device=dev)
-    ops.conv2d_bwd_filter(d, to_dev(x, dtype, dev), to_dev(dy, dtype, dev), dw)
+    db = torch.full((K,), float("nan"), dtype=torch.float32, device=dev)
+    ops.conv2d_bwd_filter(d, to_dev(x, dtype, dev), to_dev(dy, dtype, dev), dw, dbias=db)
     torch.cuda.synchronize()
     tol = 2e-5 if dtype == torch.float32 else 2e-3   # fp32 accumulation of bf16 products
     assert_close(dw.double().cpu(), wr.grad, dtype, f"conv bwd_filter {case}", tol)
+    # BiasAddGrad of the same dy (fused into the halo filter gradient)
+    assert_close(db.double().cpu(), dy.sum(dim=(0, 1, 2)), dtype, f"bias grad {case}", 2e-5)
 
 
 # (N, IH, IW, C_in, OH, OW, C_out, k, stride)
@@ -206,11 +219,13 @@ def test_tconv2d_grads(dev, ntv, tnv, case, dtype):
     dx = torch.full((N, IH, IW, d.C), float("nan"), dtype=dtype, device=dev)
     ops.tconv2d_bwd_data(d, dyd, wb, dx)
     dw = torch.full((k, k, Co, Ci), float("nan"), dtype=torch.float32, device=dev)
-    ops.tconv2d_bwd_filter(d, to_dev(x, dtype, dev), dyd, dw)
+    db = torch.full((Co,), float("nan"), dtype=torch.float32, device=dev)
+    ops.tconv2d_bwd_filter(d, to_dev(x, dtype, dev), dyd, dw, dbias=db)
     torch.cuda.synchronize()
     assert_close(from_dev(dx, Ci), xr.grad, dtype, f"tconv bwd_data {case}")
     tol = 2e-5 if dtype == torch.float32 else 2e-3
     assert_close(dw.double().cpu(), wr.grad, dtype, f"tconv bwd_filter {case}", tol)
+    assert_close(db.double().cpu(), dy.sum(dim=(0, 1, 2)), dtype, f"tconv bias grad {case}", 2e-5)
 
 
 def test_tconv_shape_rule_rejects_375(dev):
@@ -238,6 +253,16 @@ def test_maxpool_fwd_bwd(dev, shape, dtype):
     torch.cuda.synchronize()
     assert torch.equal(from_dev(yd, C), y.detach())
     assert torch.equal(from_dev(dxd, C), x.grad)
+    # fused ReluGrad of a post-ReLU input: relu(x) -> pool; d/dx through both
+    xr = torch.relu(x.detach()).requires_grad_(True)
+    (tf.max_pool2x2(xr) * dy).sum().backward()
+    want = torch.where(xr.detach() > 0, xr.grad, torch.zeros_like(xr.grad))
+    xrd = to_dev(xr.detach(), dtype, dev)
+    ops.maxpool2x2_fwd(xrd, yd)
+    dxd.fill_(float("nan"))
+    ops.maxpool2x2_bwd(xrd, yd, to_dev(dy, dtype, dev), dxd, relu_mask=True)
+    torch.cuda.synchronize()
+    assert torch.equal(from_dev(dxd, C), want)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -423,6 +448,12 @@ def test_adam_tf1_pack_matches_step_plus_pack(dev, dtype):
     Gr = (torch.randn(off, generator=g) * 0.01).to(dev)
     M = (torch.randn(off, generator=g) * 0.001).to(dev)
     V = (torch.rand(off, generator=g) * 1e-4).to(dev)
+    # alignment padding between variables holds zeros in the store (grad / m / v)
+    pad = torch.ones(off, dtype=torch.bool)
+    for (shape, _), o in zip(spec, offs):
+        pad[o:o + int(np.prod(shape))] = False
+    for t in (Gr, M, V):
+        t[pad.to(dev)] = 0
     ref = [t.clone() for t in (P, Gr, M, V)]
     copies, ref_copies, segs = [], [], []
     for (shape, modes), o in zip(spec, offs):
@@ -448,7 +479,7 @@ def test_adam_tf1_pack_matches_step_plus_pack(dev, dtype):
         ops.adam_tf1_step(*ref, 1e-3, step, **kw)
     torch.cuda.synchronize()
     for a_, b_ in zip((P, M, V), (ref[0], ref[2], ref[3])):
-        torch.testing.assert_close(a_, b_, rtol=2e-6, atol=1e-12)
+        torch.testing.assert_close(a_, b_, rtol=2e-6, atol=1e-9)
     for t, shape, o, mode in copies:
         R, S, A, B = shape
         src = P[o:o + R * S * A * B].view(R, S, A, B).contiguous()
