@@ -18,7 +18,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
@@ -53,7 +53,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise SegKernelError(f"hipcc failed for {src}:\n{r.stderr}")
         return o
 
-    with ThreadPoolExecutor(max_workers=min(7, len(SOURCES))) as ex:
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     if force or not os.path.exists(LIB_PATH) or any(
             os.path.getmtime(o) > os.path.getmtime(LIB_PATH) for o in objs):

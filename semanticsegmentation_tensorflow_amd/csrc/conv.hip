@@ -251,6 +251,9 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
             seg::WgradPlan wp;
             if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp))
                 need = std::max(need, seg::wgrad_workspace(wp, p));
+            if (seg::smallc_wgrad_ok(p, d->dtype))
+                need = std::max(need, (size_t)seg::smallc_wgrad_splits(p, seg::device_cus()) * (p.M + 1) * p.N *
+                                          sizeof(float));
             return std::max(need, seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
         }
         case 3: return tconv_use_gemm(d) ? tconv_gemm_ws(d) : 0;
@@ -280,6 +283,11 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 1: {
             NTParams p = op == 0 ? conv_fwd_params(d) : conv_bwd_data_params(d);
             seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp);
+            p.epi.keep_prob = 1.f;
+            if (op == 0 && d->dil_w == d->dil_h && seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) {
+                fam = "conv_c8"; bm = 512; bn = d->K; sp = 1; macs = macs_conv;
+                break;
+            }
             seg::HaloPlan hp;
             if (seg::g_nt_variant == 2 && seg::halo_plan(p, d->dtype, sp, seg::device_cus(), &hp)) {
                 fam = "conv_halo"; bn = hp.bn; sp = hp.splits;
@@ -292,7 +300,9 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp);
             fam = "igemm_tn";
             seg::WgradPlan wp;
-            if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
+            if (seg::smallc_wgrad_ok(p, d->dtype)) {
+                fam = "wgrad_c8"; bm = 72; bn = p.N; sp = seg::smallc_wgrad_splits(p, seg::device_cus());
+            } else if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
             }
             macs = macs_conv;
@@ -331,6 +341,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt_halo")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "smallc")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_smallc = value;
         return SEG_OK;
     }
     if (!strcmp(name, "wgrad_halo")) {
@@ -379,6 +394,11 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     NTParams p = conv_fwd_params(d);
     p.x = x; p.w = w; p.y = y;
     p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    if (d->dil_w == d->dil_h && seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) {
+        seg::launch_smallc_fwd(p, (hipStream_t)stream);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 

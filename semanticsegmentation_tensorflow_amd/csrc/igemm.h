@@ -98,6 +98,14 @@ int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
 void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s);
 
+// 8-input-channel first layer (smallc.hip)
+extern int g_smallc;
+bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil);
+void launch_smallc_fwd(NTParams& p, hipStream_t s);
+bool smallc_wgrad_ok(const TNParams& p, int dtype);
+int smallc_wgrad_splits(const TNParams& p, int cus);
+void launch_smallc_wgrad(TNParams& p, int splits, hipStream_t s);
+
 // halo-tiled filter gradient (wgrad.hip) for stride-1 3x3 TN problems
 struct WgradPlan {
     int bw, nt, splits;

@@ -759,6 +759,24 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
     p.partial = nullptr;
     p.Mp = p.M;
+    if (smallc_wgrad_ok(p, sizeof(T) == 2 ? SEG_BF16 : SEG_F32)) {
+        const int splits = smallc_wgrad_splits(p, num_cus());
+        if (p.dbias) p.Mp = p.M + 1;
+        if (splits > 1) {
+            if (!ws || ws_bytes < (size_t)splits * p.Mp * p.N * sizeof(float)) return SEG_EWORKSPACE;
+            p.partial = reinterpret_cast<float*>(ws);
+        }
+        launch_smallc_wgrad(p, splits, s);
+        SEG_CHECK_LAUNCH();
+        if (p.partial) {
+            const long total = (long)p.Mp * (p.N / 4);
+            hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+            SEG_CHECK_LAUNCH();
+            p.partial = nullptr;
+        }
+        p.dbias = nullptr;
+        return SEG_OK;
+    }
     WgradPlan wp;
     if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
         if (p.dbias) p.Mp = p.M + 1;          // wgrad_halo sums dy columns too

@@ -81,7 +81,18 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
     const int tiles_n = (p.N + BN - 1) / BN;
     const int tiles_m = (M + BM - 1) / BM;
     const int wg = xcd_remap2(blockIdx.x, gridDim.x);
-    const int tm = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
+    // Few M tiles x many N tiles (conv6/7: B = 100+ MB of filter): walk M fastest
+    // so all M tiles of one B panel run back to back on one XCD and share its
+    // L2; otherwise N fastest (A panel shared).
+    const int tiles_mg = gridDim.x / tiles_n;        // grid M tiles (max over phases)
+    int tm, tn;
+    if (tiles_mg <= 16 && tiles_n > tiles_mg) {
+        tn = wg / tiles_mg;
+        tm = wg - tn * tiles_mg;
+    } else {
+        tm = wg / tiles_n;
+        tn = wg - tm * tiles_n;
+    }
     if (tm >= tiles_m) return;
     const int m0 = tm * BM, n0 = tn * BN;
     const int KT = (p.K + BK - 1) / BK;

@@ -1,0 +1,351 @@
+// First-layer convolution with 8 (padded) input channels: conv1_1 of FCN
+// (Network/model/FCN.py:55, 3 -> 64, 3x3 SAME) and the FC-DenseNet stem.
+//
+// K = 9 taps x 8 channels = 72 is far too shallow for the implicit-GEMM
+// kernels (a whole block lives for ~2 k-tiles), and the layer is bound by its
+// output write (4 x 384 x 1248 x 64 x 2 B = 123 MB).  Direct form:
+//  * v_mfma_f32_16x16x32_bf16 with k = 4 taps x 8 channels: lane group g of an
+//    A fragment is ONE tap's 8 channels of one pixel = one 16-byte ds_read_b128
+//    from the LDS input halo (taps 9..11 read a zero slot);
+//  * the filter (3 k-steps x K/16 fragments) stays in VGPRs for the block;
+//  * block = 8 x 64 output pixels, 4 waves x 2 rows, one 16-pixel fragment
+//    at a time; bias + ReLU, staged through LDS into 16-byte row stores.
+#include "common.h"
+#include "igemm.h"
+
+namespace seg {
+
+namespace {
+
+constexpr int SC_BH = 8, SC_BW = 64;
+constexpr int SC_HW = SC_BW + 2;                       // halo width (3x3, dilation 1)
+constexpr int SC_HROWS = (SC_BH + 2) * SC_HW;          // 660 halo pixels
+
+template <int NF>
+__global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int tiles_y) {
+    using T = bf16;
+    constexpr int KN = NF * 16;
+    constexpr int SROW = KN + 8;                       // staged bf16 row (pad vs bank conflicts)
+    __shared__ __attribute__((aligned(16))) uint4 halo[SC_HROWS + 1];    // + zero slot
+    __shared__ __attribute__((aligned(16))) T stage[4][16 * SROW];
+
+    const int tpi = tiles_x * tiles_y;
+    const int img = blockIdx.x / tpi;
+    const int rem = blockIdx.x - img * tpi;
+    const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+    const int oy0 = ty * SC_BH, ox0 = tx * SC_BW;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+
+    // ---- halo: pixel (hy, hx) <- x[oy0 + ioh + hy, ox0 + iow + hx, 0..7]
+    for (int i = tid; i < SC_HROWS + 1; i += 256) {
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (i < SC_HROWS) {
+            const int hy = i / SC_HW, hx = i - (i / SC_HW) * SC_HW;
+            const int ih = oy0 + p.ioh + hy, iw = ox0 + p.iow + hx;
+            if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW)
+                v = *reinterpret_cast<const uint4*>(X + (long)img * p.x_img + ((long)ih * p.IW + iw) * p.ldx);
+        }
+        halo[i] = v;
+    }
+    // ---- filter fragments: lane -> n = nf*16 + (lane&15), tap = ks*4 + (lane>>4)
+    const int fr = lane & 15, fg = lane >> 4;
+    uint4 bw[3][NF];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+        const int t = ks * 4 + fg;
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+            const int n = nf * 16 + fr;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (t < 9 && n < p.N) v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col + t * 8);
+            bw[ks][nf] = v;
+        }
+    }
+    const EpiParams& e = p.epi;
+    __syncthreads();
+
+    // A address of this lane for k-step ks: tap (r, s) of pixel (py, px)
+    int toff[3];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+        const int t = ks * 4 + fg;
+        toff[ks] = t < 9 ? (t / 3) * SC_HW + (t % 3) : -1;
+    }
+    T* st = stage[w];
+#pragma unroll 1
+    for (int f = 0; f < 2 * SC_BW / 16; ++f) {         // 8 fragments of 16 px per wave
+        const int py = w * 2 + f / (SC_BW / 16);
+        const int px0 = (f % (SC_BW / 16)) * 16;
+        f32x4 acc[NF];
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            const int hr = toff[ks] < 0 ? SC_HROWS : py * SC_HW + px0 + fr + toff[ks];
+            const uint4 a = halo[hr];
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf)
+                acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                                  __builtin_bit_cast(bf16x8, bw[ks][nf]), acc[nf],
+                                                                  0, 0, 0);
+        }
+        // D: lane holds rows (pixels) 4*fg + j, column n = nf*16 + fr
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+            const int n = nf * 16 + fr;
+            const float b = (e.bias && n < e.n_valid) ? e.bias[n] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v = acc[nf][j] + b;
+                if (e.relu) v = fmaxf(v, 0.f);
+                st[(4 * fg + j) * SROW + n] = (T)(n < e.n_valid ? v : 0.f);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own wave's stage writes
+        // 16 px x KN/8 chunks of 16 B
+        const int oy = oy0 + py;
+#pragma unroll
+        for (int q = lane; q < 16 * (KN / 8); q += 64) {
+            const int px = q / (KN / 8), ch = q - (q / (KN / 8)) * (KN / 8);
+            const int ox = ox0 + px0 + px;
+            if (oy < p.OH && ox < p.OW) {
+                const uint4 v = *reinterpret_cast<const uint4*>(st + px * SROW + ch * 8);
+                *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + (long)img * p.y_img +
+                                          ((long)oy * p.OW + ox) * p.ldy + ch * 8) = v;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next writes
+    }
+}
+
+}  // namespace
+
+int g_smallc = 1;
+
+bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil) {
+    return g_smallc && dtype == SEG_BF16 && p.C == 8 && p.K == 72 && R == 3 && S == 3 && dil == 1 && p.ish == 1 &&
+           p.isw == 1 && !p.phase && p.N % 16 == 0 && p.N <= 64 && p.N >= 16 && p.ldx == 8 &&
+           p.ldy % 8 == 0 && !p.epi.residual && !p.epi.mask && !p.epi.scale && !p.epi.shift &&
+           p.epi.keep_prob >= 1.f;
+}
+
+void launch_smallc_fwd(NTParams& p, hipStream_t s) {
+    const int tx = (p.OW + SC_BW - 1) / SC_BW, ty = (p.OH + SC_BH - 1) / SC_BH;
+    const int nimg = p.M / (p.OH * p.OW);
+    const dim3 grid(nimg * tx * ty), block(256);
+    switch (p.N / 16) {
+        case 1: hipLaunchKernelGGL(conv_c8_fwd<1>, grid, block, 0, s, p, tx, ty); break;
+        case 2: hipLaunchKernelGGL(conv_c8_fwd<2>, grid, block, 0, s, p, tx, ty); break;
+        case 3: hipLaunchKernelGGL(conv_c8_fwd<3>, grid, block, 0, s, p, tx, ty); break;
+        default: hipLaunchKernelGGL(conv_c8_fwd<4>, grid, block, 0, s, p, tx, ty); break;
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Filter gradient of the same layer: dW[r][s][c][n] = sum_p x[p + (r,s)][c] dz[p][n]
+// computed as D[n][j] = sum_p dz[p][n] * X2[p][j] with k = pixels, where a
+// 16-column B fragment j = (s_off, c) of tap pair (r, s0..s0+1) is 32
+// contiguous bytes of the [px][8] halo starting at pixel (py + r, px + s0):
+// taps are paired horizontally, the s0+1 == 3 half is computed and dropped.
+// Both operands come from LDS with ds_read_b64_tr_b16 (k = pixels).
+//  * tile = 4 x 64 output pixels; halo (4+2) x (64+2) px x 16 B; dz tile
+//    256 px x N x 2 B; both staged by LDS-DMA, double buffered.
+//  * 4 waves = (N half) x (tap-pair half): 2 n-fragments x 3 pair fragments.
+//  * split-K over tile ranges -> fp32 slabs (+ BiasAddGrad row) -> reducer.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int WC_BH = 4, WC_BW = 64, WC_TP = WC_BH * WC_BW;      // 256 px per tile
+constexpr int WC_HW = WC_BW + 2;
+constexpr int WC_HROWS = (WC_BH + 2) * WC_HW;                     // 396
+constexpr int WC_HPAD = 448;                                      // 7 x 64 DMA rows (>= 396 + 1)
+
+struct WCGeom {
+    int tiles_x, tiles_y, ptiles, tps, splits;
+};
+
+__device__ __forceinline__ void wc_glds16(const void* gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+__device__ uint4 wc_zero_page[4];
+
+// N = 64 (4 n fragments); 6 tap-pair fragments: (r, 0..1), (r, 2..3*) for r = 0..2
+__global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
+    using T = bf16;
+    constexpr int DROWB = 128;                          // 64 dz channels
+    constexpr int HBUF = WC_HPAD * 16, DBUF = WC_TP * DROWB, STAGE = HBUF + DBUF;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int split = blockIdx.x;
+    const int t_begin = split * g.tps, t_end = min(g.ptiles, t_begin + g.tps);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nh = w & 1, mh = w >> 1;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Dz = reinterpret_cast<const T*>(p.b);
+    const void* zero = (const void*)wc_zero_page;
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+
+    // DMA: halo 7 instructions per block (1.75 per wave -> waves 0..2 take 2, 3 takes 1),
+    // dz: 256 rows x 128 B = 32 instructions (8 per wave), lane -> (row lane>>3, chunk lane&7)
+    auto stage_tile = [&](int t, int buf) {
+        const int tpi = g.tiles_x * g.tiles_y;
+        const int img = t / tpi;
+        const int rem = t - img * tpi;
+        const int ty = rem / g.tiles_x, tx = rem - (rem / g.tiles_x) * g.tiles_x;
+        const int oy0 = ty * WC_BH, ox0 = tx * WC_BW;
+        const unsigned sb = lds0 + buf * STAGE;
+        for (int q = w; q < WC_HPAD / 64; q += 4) {
+            const int hr = q * 64 + lane;
+            const int hy = hr / WC_HW, hx = hr - (hr / WC_HW) * WC_HW;
+            const int ih = oy0 + p.ioh + hy, iw = ox0 + p.iow + hx;
+            const bool ok = hr < WC_HROWS && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+            const void* src = ok ? (const void*)(X + (long)img * p.x_img + ((long)ih * p.IW + iw) * p.ldx) : zero;
+            wc_glds16(src, sb + q * 1024);
+        }
+        const int lr = lane >> 3, pc = lane & 7;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = (i * 4 + w) * 8 + lr;                 // dz tile row (pixel)
+            const int ch = pc ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2));
+            const int oy = oy0 + r / WC_BW, ox = ox0 + r % WC_BW;
+            const bool ok = oy < p.Ha && ox < p.Wa;
+            const void* src = ok ? (const void*)(Dz + (((long)img * p.Ha + oy) * p.Wa + ox) * p.ldb + ch * 8) : zero;
+            wc_glds16(src, sb + HBUF + (i * 4 + w) * 1024);
+        }
+    };
+
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = p.dbias != nullptr && mh == 0;
+    float dsum[2] = {0.f, 0.f};
+    const int fg = lane >> 4, tq = (lane & 15) >> 2, tpp = lane & 3;
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    // tap-pair fragments of this wave: mf = mh*3 + i -> (r = mf / 2, s0 = (mf % 2) * 2)
+    int poff[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int mf = mh * 3 + i;
+        poff[i] = (mf >> 1) * WC_HW + (mf & 1) * 2;
+    }
+
+    if (t_begin < t_end) stage_tile(t_begin, 0);
+    int buf = 0;
+    for (int t = t_begin; t < t_end; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t + 1 < t_end) stage_tile(t + 1, buf ^ 1);
+        const char* Hs = smem + buf * STAGE;
+        const char* Ds = Hs + HBUF;
+#pragma unroll 2
+        for (int ks = 0; ks < WC_TP / 32; ++ks) {
+            const int kk = ks * 32 + 8 * fg + tq;                  // pixel of this lane's lo row
+            const int py = kk / WC_BW, px = kk - (kk / WC_BW) * WC_BW;
+            bf16x8 af[2], bfr[3];
+            const int d1 = (((kk >> 1) & 1) << 1) | (((kk >> 3) & 1) << 2);
+            const int d2 = ((((kk + 4) >> 1) & 1) << 1) | ((((kk + 4) >> 3) & 1) << 2);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int chk = nh * 4 + ni * 2 + (tpp >> 1);
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * (chk ^ d1) + 8 * (tpp & 1)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * (chk ^ d2) + 8 * (tpp & 1)));
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                af[ni] = __builtin_bit_cast(bf16x8, v);
+                if (do_bias) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                }
+            }
+            const int hb = py * WC_HW + px;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int h1 = hb + poff[i];
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + h1 * 16 + 8 * tpp));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (h1 + 4) * 16 + 8 * tpp));
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bfr[i] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    acc[ni][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bfr[i], acc[ni][i], 0, 0, 0);
+        }
+        buf ^= 1;
+    }
+
+    // D[n][j]: lane holds n = nfrag*16 + 4*fg + jj, j = lane & 15 -> (s_off = j >> 3, c = j & 7)
+    const int j = lane & 15, soff = j >> 3, c = j & 7;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int mf = mh * 3 + i, r = mf >> 1, s = (mf & 1) * 2 + soff;
+        if (s >= 3) continue;
+        const int m = (r * 3 + s) * p.Cg + c;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int n = nh * 32 + ni * 16 + 4 * fg + jj;
+                const float v = acc[ni][i][jj];
+                if (p.partial) {
+                    if (n < p.N) p.partial[((long)split * p.Mp + m) * p.N + n] = v;
+                } else if (c < p.c_valid && n < p.n_valid) {
+                    p.out[(long)(r * 3 + s) * p.o_tap + (long)c * p.o_c + (long)n * p.o_n] = v;
+                }
+            }
+    }
+    if (do_bias) {
+        const int fr = lane & 15;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+            dsum[ni] += __shfl_xor(dsum[ni], 16);
+            dsum[ni] += __shfl_xor(dsum[ni], 32);
+            const int n = nh * 32 + ni * 16 + fr;
+            if (fg == 0) {
+                if (p.partial) {
+                    if (n < p.N) p.partial[((long)split * p.Mp + p.M) * p.N + n] = dsum[ni];
+                } else if (n < p.n_valid) {
+                    p.dbias[n] = dsum[ni];
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+bool smallc_wgrad_ok(const TNParams& p, int dtype) {
+    return g_smallc && dtype == SEG_BF16 && p.Cg == 8 && p.M == 72 && p.taps_w == 3 && p.ish == 1 && p.isw == 1 &&
+           p.tsh == 1 && p.tsw == 1 && p.N == 64 && p.ldx == 8 && p.ldb == 64 && p.Ha > 0 && p.Wa > 0 &&
+           p.P % (p.Ha * p.Wa) == 0;
+}
+
+int smallc_wgrad_splits(const TNParams& p, int cus) {
+    const int nimg = p.P / (p.Ha * p.Wa);
+    const int ptiles = nimg * ((p.Wa + WC_BW - 1) / WC_BW) * ((p.Ha + WC_BH - 1) / WC_BH);
+    const int want = std::min(ptiles, 2 * cus);
+    const int tps = (ptiles + want - 1) / want;
+    return (ptiles + tps - 1) / tps;
+}
+
+void launch_smallc_wgrad(TNParams& p, int splits, hipStream_t s) {
+    WCGeom g;
+    g.tiles_x = (p.Wa + WC_BW - 1) / WC_BW;
+    g.tiles_y = (p.Ha + WC_BH - 1) / WC_BH;
+    g.ptiles = (p.P / (p.Ha * p.Wa)) * g.tiles_x * g.tiles_y;
+    g.tps = (g.ptiles + splits - 1) / splits;
+    g.splits = splits;
+    hipLaunchKernelGGL(wgrad_c8, dim3(splits), dim3(256), 0, s, p, g);
+}
+
+}  // namespace seg
