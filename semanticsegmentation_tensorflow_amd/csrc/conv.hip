@@ -289,7 +289,9 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
                 break;
             }
             seg::HaloPlan hp;
-            if (seg::g_nt_variant == 2 && seg::halo_plan(p, d->dtype, sp, seg::device_cus(), &hp)) {
+            if (seg::g_nt_variant == 2 && seg::res64_ok(p, d->dtype)) {
+                fam = "conv_res64"; bn = 64; sp = 1;
+            } else if (seg::g_nt_variant == 2 && seg::halo_plan(p, d->dtype, sp, seg::device_cus(), &hp)) {
                 fam = "conv_halo"; bn = hp.bn; sp = hp.splits;
             }
             macs = macs_conv;
@@ -343,6 +345,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_nt_halo = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "res64")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_res64 = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "smallc")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_smallc = value;
@@ -374,7 +381,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 3) return SEG_EINVAL;
+        if (value < 0 || value > 4) return SEG_EINVAL;
         seg::g_nt2_ablate = value;
         return SEG_OK;
     }

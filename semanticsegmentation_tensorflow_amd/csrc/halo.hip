@@ -35,6 +35,7 @@ int g_nt_halo = 1;
 int g_halo_wide = 1;
 int g_halo_stagger = 1;
 int g_halo_phases = 2;
+int g_res64 = 1;
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -591,6 +592,217 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent variant for a single 64-channel chunk with N <= 64 (conv1_2 fwd
+// and its input gradient: 384 x 1248 px, C = K = 64).  The whole 3x3 filter
+// (9 x 64 rows x 128 B = 72 KB) is loaded into LDS once per block; the block
+// then walks tiles t = blockIdx.x, +gridDim.x, ...: the 8 x 32 tile's halo
+// (10 x 34 px x 128 B) sits in LDS, all 9 taps run without a barrier, and the
+// NEXT tile's halo is prefetched into VGPRs (6 x 16 B per thread) while the
+// current one computes.  The epilogue is staged in the (dead) halo buffer.
+// ---------------------------------------------------------------------------
+constexpr int R64_BH = 8, R64_BW = 32, R64_HW = R64_BW + 2, R64_HROWS = (R64_BH + 2) * R64_HW;   // 340
+constexpr int R64_PER = (R64_HROWS * 8 + 511) / 512;                                             // 6
+
+// ABL (diagnostics only, garbage results): 1 no halo fetch, 2 no MFMA,
+// 3 no epilogue stores, 4 no LDS fragment reads
+template <int ABL = 0>
+__global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+    using T = bf16;
+    constexpr int NW = 8, WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2;
+    constexpr int BS = 9 * 64 * 128;                 // resident filter
+    constexpr int HS = R64_HROWS * 128;              // halo
+    __shared__ __attribute__((aligned(16))) char smem[BS + HS];
+    char* Bs = smem;
+    char* Hs = smem + BS;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const int fr = lane & 15, fg = lane >> 4;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const int hy0 = p.tsh < 0 ? 2 * p.tsh : 0, hx0 = p.tsw < 0 ? 2 * p.tsw : 0;
+    const int tpi = tiles_x * tiles_y;
+
+    // ---- filter: Bs[tap][n][chunk ^ swz(n)]
+    for (int i = tid; i < 9 * 64 * 8; i += 512) {
+        const int c8 = i & 7, n = (i >> 3) & 63, tap = i >> 9;
+        const int j = tap / 3, ii = tap - (tap / 3) * 3;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (n < p.N)
+            v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col +
+                                                (long)((p.rb + p.rstep * j) * p.Sfull + (p.sb + p.sstep * ii)) * p.w_tap +
+                                                c8 * 8);
+        *reinterpret_cast<uint4*>(Bs + (tap * 64 + n) * 128 + 16 * (c8 ^ ((n >> 1) & 7))) = v;
+    }
+    // ---- halo fetch into registers: slot q -> (row q / 8, chunk q % 8)
+    uint4 hv[R64_PER];
+    auto fetch = [&](int t) {
+        if constexpr (ABL == 1) return;
+        const int img = t / tpi;
+        const int rem = t - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+        const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+#pragma unroll
+        for (int k = 0; k < R64_PER; ++k) {
+            const int q = tid + k * 512;
+            const int hr = q >> 3, c8 = q & 7;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (hr < R64_HROWS) {
+                const int hy = hr / R64_HW, hx = hr - (hr / R64_HW) * R64_HW;
+                const int ih = oy0 + p.ioh + hy0 + hy, iw = ox0 + p.iow + hx0 + hx;
+                if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW)
+                    v = *reinterpret_cast<const uint4*>(X + (long)img * p.x_img + ((long)ih * p.IW + iw) * p.ldx + c8 * 8);
+            }
+            hv[k] = v;
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int k = 0; k < R64_PER; ++k) {
+            const int q = tid + k * 512;
+            const int hr = q >> 3, c8 = q & 7;
+            if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 128 + 16 * (c8 ^ ((hr >> 1) & 7))) = hv[k];
+        }
+    };
+
+    int rowbase[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+        const int ml = wm * WTM + mi * 16;
+        rowbase[mi] = (ml / R64_BW) * R64_HW + (ml % R64_BW) + fr;
+    }
+    int toff[9];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) toff[tap] = ((tap / 3) * p.tsh - hy0) * R64_HW + (tap % 3) * p.tsw - hx0;
+
+    // epilogue constants: the MFMA computes D^T (filter rows x pixels), so a
+    // lane holds 4 consecutive channels of one pixel -> 8-byte stores
+    const EpiParams& e = p.epi;
+    float bias[TN][4], scl[TN][4], shf[TN][4];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = wn * WTN + ni * 16 + 4 * fg + j;
+            const bool cv = col < e.n_valid;
+            bias[ni][j] = (e.bias && cv) ? e.bias[col] : 0.f;
+            scl[ni][j] = (e.scale && cv) ? e.scale[col] : 1.f;
+            shf[ni][j] = (e.shift && cv) ? e.shift[col] : 0.f;
+        }
+
+    int t = blockIdx.x;
+    if (t < ntiles) fetch(t);
+    commit();
+    __syncthreads();
+    for (; t < ntiles; t += gridDim.x) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fetch(tn);                  // in flight during this tile's MFMAs
+        f32x4 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // software pipeline over the 18 (tap, k-half) steps: fragments of step
+        // s+1 are read while the MFMAs of step s issue
+        uint4 fa[2][TM], fb[2][TN];
+        auto load_step = [&](int st, uint4* a, uint4* b) {
+            const int tap = st >> 1, chunk = (st & 1) * 4 + fg;
+            if constexpr (ABL == 4) {
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi) a[mi] = uint4{(unsigned)st, (unsigned)mi, 0u, (unsigned)tap};
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) b[ni] = uint4{(unsigned)chunk, (unsigned)ni, 1u, 0u};
+                return;
+            }
+            const char* Bt = Bs + tap * 64 * 128;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int row = rowbase[mi] + toff[tap];
+                a[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int row = wn * WTN + ni * 16 + fr;
+                b[ni] = *reinterpret_cast<const uint4*>(Bt + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+        };
+        load_step(0, fa[0], fb[0]);
+#pragma unroll
+        for (int st = 0; st < 18; ++st) {
+            const int cur = st & 1;
+            if (st + 1 < 18) load_step(st + 1, fa[cur ^ 1], fb[cur ^ 1]);
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {  // D^T[n][px] += W[n][k] X[px][k]
+                    if constexpr (ABL == 2) {
+                        asm volatile("" ::"v"(fb[cur][ni].x), "v"(fa[cur][mi].x), "v"(fb[cur][ni].w), "v"(fa[cur][mi].w));
+                    } else {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, fb[cur][ni]), __builtin_bit_cast(bf16x8, fa[cur][mi]),
+                            acc[mi][ni], 0, 0, 0);
+                    }
+                }
+        }
+        // ---- epilogue straight from registers: pixel (mi, fr), channels 4*fg..+3 of (ni)
+        {
+            const int img = t / tpi;
+            const int rem = t - img * tpi;
+            const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+            const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int ml = wm * WTM + mi * 16 + fr;
+                const int oy = oy0 + ml / R64_BW, ox = ox0 + ml % R64_BW;
+                if (oy >= p.OH || ox >= p.OW) continue;
+                const long pix = (long)oy * p.OW + ox;
+                const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col0 = wn * WTN + ni * 16 + 4 * fg;
+                    if (col0 >= p.N) continue;
+                    float mk[4] = {1.f, 1.f, 1.f, 1.f}, res[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (e.mask) {
+                        const uint2 mv = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.mask) +
+                                                                         img * e.mask_img + pix * e.ld_mask + col0);
+                        mk[0] = __uint_as_float(mv.x << 16); mk[1] = __uint_as_float(mv.x & 0xffff0000u);
+                        mk[2] = __uint_as_float(mv.y << 16); mk[3] = __uint_as_float(mv.y & 0xffff0000u);
+                    }
+                    if (e.residual) {
+                        const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.residual) +
+                                                                         img * e.res_img + pix * e.ld_res + col0);
+                        res[0] = __uint_as_float(rv.x << 16); res[1] = __uint_as_float(rv.x & 0xffff0000u);
+                        res[2] = __uint_as_float(rv.y << 16); res[3] = __uint_as_float(rv.y & 0xffff0000u);
+                    }
+                    bf16 o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int col = col0 + j;
+                        float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
+                        if (e.relu) x = fmaxf(x, 0.f);
+                        if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+                        x += res[j];
+                        if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                        o[j] = (bf16)(col < e.n_valid ? x : 0.f);
+                    }
+                    if constexpr (ABL == 3) {
+                        asm volatile("" ::"v"(o[0]), "v"(o[3]));
+                    } else {
+                        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
+                            *reinterpret_cast<const uint2*>(o);
+                    }
+                }
+            }
+        }
+        __syncthreads();                             // all taps read the halo
+        commit();                                    // next tile's halo (waits for its loads)
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -679,6 +891,26 @@ template <int BW, int HI>
 static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s) {
     if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s);
     else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s);
+}
+
+bool res64_ok(const NTParams& p, int dtype) {
+    return g_res64 && g_nt_halo && dtype == SEG_BF16 && !p.phase && p.ish == 1 && p.isw == 1 && p.osh == 1 &&
+           p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.Ha == p.OH && p.Wa == p.OW && p.C == 64 && p.K == 9 * 64 &&
+           p.taps_w == 3 && (p.tsh == 1 || p.tsh == -1) && (p.tsw == 1 || p.tsw == -1) && p.N <= 64 &&
+           p.N % 8 == 0 && p.OH > 0 && p.OW > 0 && p.M % (p.OH * p.OW) == 0;
+}
+
+void launch_res64(NTParams& p, int cus, hipStream_t s) {
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
+    const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
+    const int grid = std::min(ntiles, cus);
+    switch (g_nt2_ablate) {
+        case 1: hipLaunchKernelGGL(conv_res64<1>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
+        case 2: hipLaunchKernelGGL(conv_res64<2>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
+        case 3: hipLaunchKernelGGL(conv_res64<3>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
+        case 4: hipLaunchKernelGGL(conv_res64<4>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
+    }
+    hipLaunchKernelGGL(conv_res64<0>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
 }
 
 void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {

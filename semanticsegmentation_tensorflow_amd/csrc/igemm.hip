@@ -664,6 +664,11 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
     if (nphases > 1) splits = 1;
     p.partial = nullptr;
+    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
+        launch_res64(p, num_cus(), s);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     HaloPlan hp;
     if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, splits, num_cus(), &hp)) {
         if (hp.splits > 1) {

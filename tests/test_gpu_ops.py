@@ -60,6 +60,7 @@ CONV_CASES = [
     (1, 18, 19, 128, 72, 3, 3, 1, 1, "VALID"),
     (2, 33, 45, 64, 328, 3, 3, 1, 1, "SAME"),   # 256-wide halo tiles: 2 N tiles + tail
     (2, 19, 131, 3, 48, 3, 3, 1, 1, "SAME"),    # first-layer kernel (C=3->8): ragged 8x64 tiles, K=48
+    (1, 17, 70, 64, 48, 3, 3, 1, 1, "VALID"),   # resident-filter kernel: VALID, N=48 < 64
 ]
 
 
