@@ -31,7 +31,7 @@ namespace seg {
 static __device__ uint4 wg_zero_page[4];
 
 int g_wgrad_halo = 1;
-int g_wgrad_nt = 64;
+int g_wgrad_nt = 128;
 
 struct WGGeom {
     int tiles_x, tiles_y, nimg, hwd, hrows;
@@ -168,11 +168,11 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
         if (t + NST - 1 < t_end) stage_tile(t + NST - 1, buf == 0 ? NST - 1 : buf - 1);
         const char* Hs = smem + buf * STAGE;
         const char* Ds = Hs + HBUF;
-#pragma unroll 1
-        for (int ss = 0; ss < 4; ++ss) {
-            const int kk = ss * 32 + 8 * fg + tq;          // tile pixel of this lane's lo row
-            const int py = kk / BW, px = kk - (kk / BW) * BW;
-            bf16x8 bfr[NF], af[9];
+        // flat software pipeline over the 36 (substep, tap) steps of the tile:
+        // the A fragment of step s+1 (and the B fragments of the next substep)
+        // are read while the MFMAs of step s issue
+        auto read_b = [&](int ss, bf16x8* bo) {
+            const int kk = ss * 32 + 8 * fg + tq;
             const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
 #pragma unroll
             for (int ni = 0; ni < NF; ++ni) {
@@ -181,29 +181,46 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * q1 + 8 * (tpp & 1)));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bfr[ni] = __builtin_bit_cast(bf16x8, v);
+                bo[ni] = __builtin_bit_cast(bf16x8, v);
                 if (do_bias) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
                         dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
                 }
             }
-            const int hbase = py * g.hwd + px;
+        };
+        auto read_a = [&](int ss, int tap) {
+            const int kk = ss * 32 + 8 * fg + tq;
+            const int py = kk / BW, px = kk - (kk / BW) * BW;
+            const int r1 = py * g.hwd + px + tapoff[tap];
             const int achk = cf * 2 + (tpp >> 1);
+            const int a1 = achk ^ wg_swz<128>(r1), a2 = achk ^ wg_swz<128>(r1 + 4);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + r1 * 128 + 16 * a1 + 8 * (tpp & 1)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (r1 + 4) * 128 + 16 * a2 + 8 * (tpp & 1)));
+            s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            return __builtin_bit_cast(bf16x8, v);
+        };
+        bf16x8 b0[NF], b1[NF];
+        read_b(0, b0);
+        bf16x8 a_cur = read_a(0, 0);
+        // one substep: 9 taps, A(tap+1) read ahead, next substep's B at tap 4
+        auto substep = [&](int ss, bf16x8* bc, bf16x8* bn) {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                const int r1 = hbase + tapoff[tap];
-                const int a1 = achk ^ wg_swz<128>(r1), a2 = achk ^ wg_swz<128>(r1 + 4);
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + r1 * 128 + 16 * a1 + 8 * (tpp & 1)));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (r1 + 4) * 128 + 16 * a2 + 8 * (tpp & 1)));
-                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                af[tap] = __builtin_bit_cast(bf16x8, v);
-            }
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
+                bf16x8 a_nxt = a_cur;
+                if (tap < 8) a_nxt = read_a(ss, tap + 1);
+                else if (ss + 1 < 4) a_nxt = read_a(ss + 1, 0);
+                if (tap == 4 && ss + 1 < 4) read_b(ss + 1, bn);
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni)
-                    acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap], bfr[ni], acc[tap][ni], 0, 0, 0);
+                    acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, bc[ni], acc[tap][ni], 0, 0, 0);
+                a_cur = a_nxt;
+            }
+        };
+#pragma unroll 1
+        for (int ss = 0; ss < 4; ss += 2) {
+            substep(ss, b0, b1);
+            substep(ss + 1, b1, b0);
         }
         buf = buf == NST - 1 ? 0 : buf + 1;
     }
@@ -265,7 +282,6 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
         const int bh = 128 / bw;
         const int hwd = bw + 2 * p.tsw, hrows = hwd * (bh + 2 * p.tsh);
         if (hrows > 5 * 64) continue;
-        if (g_wgrad_nt == 128 && hrows > 4 * 64) continue;
         const int tx = (p.Wa + bw - 1) / bw, ty = (p.Ha + bh - 1) / bh;
         const long cost = (long)tx * ty * (128 * 8 + hrows);
         if (best < 0 || cost < best) {
@@ -275,7 +291,8 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
         }
     }
     if (best < 0) return false;
-    wp->nt = (g_wgrad_nt == 128 && p.N > 64) ? 128 : 64;
+    // 128-wide dy tiles (2 LDS stages, 4 halo pieces) when N allows and the halo fits
+    wp->nt = (g_wgrad_nt == 128 && p.N > 64 && wp->g[4] <= 4 * 64) ? 128 : 64;
     wp->g[2] = nimg;
     const int nct = p.Cg / 64, nnt = (p.N + wp->nt - 1) / wp->nt;
     const int nout = nct * nnt;

@@ -141,7 +141,7 @@ def tnv(request, dev):
     yield v
     ops.set_option("igemm_tn_variant", 2)
     ops.set_option("wgrad_halo", 1)
-    ops.set_option("wgrad_nt", 64)
+    ops.set_option("wgrad_nt", 128)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

@@ -82,6 +82,6 @@ for (name, H, W, C, K) in LAYERS:
             ops.set_option("wgrad_nt", nt)
             res.setdefault(m, []).append(timeit(lambda: ops.conv2d_bwd_filter(d, x, dy, dw, ws)))
     ops.set_option("wgrad_halo", 1)
-    ops.set_option("wgrad_nt", 64)
+    ops.set_option("wgrad_nt", 128)
     print(name, ops.conv_kernel_info(d, 2)[:2],
           "  ".join(f"{m}={min(v)*1e3:.1f}us({flops/min(v)/1e9:.0f}TF)" for m, v in res.items()), flush=True)
