@@ -35,11 +35,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4, help="images per GPU")
+    ap.add_argument("--model", default="fcn", choices=["fcn", "fcdensenet"],
+                    help="fcn = config C2/C4 (headline); fcdensenet = config C3 (U-Net)")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (fcn 4, fcdensenet 8)")
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--keep-prob", type=float, default=0.8)
+    ap.add_argument("--keep-prob", type=float, default=None,
+                    help="fcn 0.8 (FCN.py:395), fcdensenet 0.2 (FCDenseNet.py:13)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -71,8 +74,8 @@ def synthetic(batch, H, W, HP, WP, seed, device):
     return img, lab.contiguous()
 
 
-def cpu_baseline(H, W, HP, WP, steps):
-    """The oracle's FCN forward+backward (torch-CPU fp32) on this host."""
+def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
+    """The oracle's FCN (or FC-DenseNet) forward+backward (torch-CPU fp32) on this host."""
     import numpy as np
     import torch
     from oracle import models as M
@@ -80,9 +83,11 @@ def cpu_baseline(H, W, HP, WP, steps):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
+    shapes = M.fcn_param_shapes(3, 2) if model == "fcn" else M.fcdensenet_param_shapes(3, 2)
+    fwd = M.fcn_forward if model == "fcn" else M.fcdensenet_forward
     p = {k: torch.from_numpy((rng.standard_normal(s, dtype=np.float32) * 0.01).astype(np.float32)
                              ).requires_grad_(True)
-         for k, s in M.fcn_param_shapes(3, 2).items()}
+         for k, s in shapes.items()}
     x = torch.zeros(1, HP, WP, 3)
     x[:, :H, :W] = torch.from_numpy(rng.integers(0, 256, (1, H, W, 3)).astype(np.float32))
     lab = torch.zeros(1, HP, WP, dtype=torch.long)
@@ -94,7 +99,7 @@ def cpu_baseline(H, W, HP, WP, steps):
     def step():
         for v in p.values():
             v.grad = None
-        _, logits = M.fcn_forward(p, x)
+        _, logits = fwd(p, x)
         T.mean_softmax_xent(logits, y1, mask).backward()
 
     step()                              # warm-up
@@ -103,7 +108,8 @@ def cpu_baseline(H, W, HP, WP, steps):
         step()
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(1.0 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle FCN fwd+bwd, torch-CPU fp32, 1 image {HP}x{WP} ({H}x{W} padded), "
+            "sample": f"oracle {'FCN' if model == 'fcn' else 'FC-DenseNet'} fwd+bwd, torch-CPU fp32, "
+                      f"1 image {HP}x{WP} ({H}x{W} padded), "
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
 
 
@@ -125,23 +131,28 @@ def main():
 
     from semanticsegmentation_tensorflow_amd import graph as G
     from semanticsegmentation_tensorflow_amd import ops, tf
+    from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
     from semanticsegmentation_tensorflow_amd.fcn import FCN
 
     H, W = args.height, args.width
     HP, WP = pad32(H), pad32(W)
-    B = args.batch
+    B = args.batch or (4 if args.model == "fcn" else 8)
+    kp = args.keep_prob if args.keep_prob is not None else (0.8 if args.model == "fcn" else 0.2)
     G.reset_default_graph()
     image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
     labels = tf.placeholder(tf.uint8, [None, HP, WP], name="annotation")
     keep = tf.placeholder(tf.float32, name="keep_probability")
-    pred, logits = FCN(image, keep, 2).create()
+    if args.model == "fcn":
+        pred, logits = FCN(image, keep, 2).create()
+    else:
+        pred, logits = FCDenseNet(image, keep, 2)
     loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
                                                                    valid_hw=(H, W)))
     train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
     sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp)
     sess.run(tf.global_variables_initializer())
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
-    feed = {image: img, labels: lab, keep: args.keep_prob}
+    feed = {image: img, labels: lab, keep: kp}
 
     for _ in range(args.warmup):
         sess.run(train_step, feed_dict=feed)
@@ -207,13 +218,14 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic",
         "config": {
-            "workload": "FCN (reference Network/model/FCN.py topology) train step: fwd + softmax-xent "
-                        "+ bwd + TF1 Adam, 375x1242x3 zero-padded to 384x1248",
+            "workload": ("FCN (reference Network/model/FCN.py topology)" if args.model == "fcn" else
+                         "FC-DenseNet 'U-Net' (reference Network/model/FCDenseNet.py topology)")
+                        + " train step: fwd + softmax-xent + bwd + TF1 Adam, 375x1242x3 zero-padded to 384x1248",
             "global_batch": B * world,
             "batch_per_gpu": B,
             "image": f"{H}x{W} -> {HP}x{WP}",
             "parallelism": f"dp{world}",
-            "keep_prob": args.keep_prob,
+            "keep_prob": kp,
         },
         "roofline": {
             "bound": "mfma",
@@ -227,14 +239,15 @@ def main():
             "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
             "avg_launch_ms": round(dms / dn, 4),
         },
-        "step_mfma_frac": round(FCN_TRAIN_FLOP_PER_IMG * B / (ms_per_step * 1e-3) / peak, 4)
-        if (HP, WP) == (384, 1248) else None,
+        "step_mfma_frac": round((FCN_TRAIN_FLOP_PER_IMG * B if args.model == "fcn" else step_conv_flops)
+                                / (ms_per_step * 1e-3) / peak, 4)
+        if (HP, WP) == (384, 1248) or args.model != "fcn" else None,
         "conv_gflop_per_step_measured": round(step_conv_flops / 1e9, 2),
         "loss_after": round(loss_val, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps)
+            result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps, args.model)
         except Exception as exc:  # report, never crash the headline line
             result["cpu_baseline"] = {"value": None, "error": repr(exc)}
     if rank == 0:

@@ -195,6 +195,22 @@ int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, 
 /* dx is zeroed then scatter-added (fp32 dx only). */
 int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, int W, int C, int OH,
                             int OW, int dtype, void* stream);
+/* tf.concat(axis=-1) (Network/utils/utils.py:332-333; DenseBlock
+ * FCDenseNet.py:48-61): parts at arbitrary (unaligned) channel offsets.
+ * fwd: y[p, off_i + c] = part_i[p, c]; channels >= sum are written 0.
+ * bwd: part_i[p, c] (+)= dy[p, off_i + c]  (accumulate != 0 adds), padding
+ * channels of each part are left 0 (or unchanged when accumulating).     */
+#define SEG_CONCAT_MAX 64
+typedef struct seg_concat_part {
+    const void* ptr;     /* fwd: source; bwd: destination (cast away const) */
+    int ld;              /* pixel stride (elements) */
+    int channels;        /* valid channels of this part */
+    int accumulate;      /* bwd only */
+} seg_concat_part;
+int seg_concat_fwd(const seg_concat_part* parts, int nparts, void* y, int ldy, int ychannels, long P, int dtype,
+                   void* stream);
+int seg_concat_bwd(const void* dy, int ldy, const seg_concat_part* parts, int nparts, long P, int dtype,
+                   void* stream);
 /* Channel-slice copy: y[p, 0:C] = x[p, 0:C] (tf.concat building block). */
 int seg_copy_channels(const void* x, int ldx, void* y, int ldy, long P, int C, int dtype,
                       void* stream);

@@ -129,6 +129,8 @@ SIGNATURES = {
     "seg_confusion": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "seg_adam_tf1_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _I, _F, _P]),
     "seg_adam_segments_plan": (_I, [_P, _I]),
+    "seg_concat_fwd": (_I, [_P, _I, _P, _I, _I, _L, _I, _P]),
+    "seg_concat_bwd": (_I, [_P, _I, _P, _I, _L, _I, _P]),
     "seg_adam_tf1_pack": (_I, [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _I, _F, _I, _P]),
     "seg_fill": (_I, [_P, _L, _F, _I, _P]),
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),

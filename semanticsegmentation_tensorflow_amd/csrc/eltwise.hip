@@ -290,6 +290,76 @@ __global__ void copy_channels_k(const T* __restrict__ x, int ldx, T* __restrict_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// tf.concat over channels with unaligned part offsets (FC-DenseNet)
+// ---------------------------------------------------------------------------
+struct ConcatArgs {
+    seg_concat_part part[SEG_CONCAT_MAX];
+    int off[SEG_CONCAT_MAX + 1];
+    int n;
+};
+
+template <typename T>
+__global__ void concat_fwd_k(ConcatArgs a, T* __restrict__ y, int ldy, int yc8, long P) {
+    const long total = P * yc8;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / yc8;
+        const int k = (int)(i - p * yc8);
+        float v[8];
+        int src = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = k * 8 + j;
+            while (src < a.n && c >= a.off[src + 1]) ++src;
+            v[j] = 0.f;
+            if (src < a.n) {
+                const T* xp = reinterpret_cast<const T*>(a.part[src].ptr);
+                v[j] = to_f32(xp[p * a.part[src].ld + (c - a.off[src])]);
+            }
+        }
+        T* yp = y + p * ldy + k * 8;
+        if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        } else {
+            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+            *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
+        }
+    }
+}
+
+// one thread per (pixel, 8-channel chunk of a destination part)
+template <typename T>
+__global__ void concat_bwd_k(const T* __restrict__ dy, int ldy, ConcatArgs a, const int* __restrict__ dummy,
+                             long P, int chunks_per_px) {
+    (void)dummy;
+    const long total = P * chunks_per_px;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / chunks_per_px;
+        int k = (int)(i - p * chunks_per_px);
+        int d = 0;
+        while (d < a.n && k >= (a.part[d].channels + 7) / 8) { k -= (a.part[d].channels + 7) / 8; ++d; }
+        if (d >= a.n) continue;
+        const seg_concat_part& pt = a.part[d];
+        T* xp = reinterpret_cast<T*>(const_cast<void*>(pt.ptr)) + p * pt.ld + k * 8;
+        float v[8];
+        if (pt.accumulate) {
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp), v);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp + 4), v + 4);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = k * 8 + j;
+            if (c < pt.channels) v[j] += to_f32(dy[p * ldy + a.off[d] + c]);
+        }
+        *reinterpret_cast<uint4*>(xp) = Chunk<T>::pack(v);
+        if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(xp + 4) = Chunk<T>::pack(v + 4);
+    }
+}
+
 template <typename T>
 __global__ void prepare_input_k(const float* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
                                 int WP, int CP) {
@@ -724,6 +794,48 @@ extern "C" int seg_copy_channels(const void* x, int ldx, void* y, int ldy, long 
     const long total = P * (C / epc_of(dtype));
     DISPATCH_T(dtype, hipLaunchKernelGGL(copy_channels_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
                                          (hipStream_t)stream, (const T*)x, ldx, (T*)y, ldy, P, C));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+
+static int concat_args(const seg_concat_part* parts, int n, ConcatArgs* a) {
+    if (!parts || n <= 0 || n > SEG_CONCAT_MAX) return SEG_EINVAL;
+    a->n = n;
+    a->off[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!parts[i].ptr || parts[i].channels <= 0 || (parts[i].ld & 7) || parts[i].ld < parts[i].channels)
+            return SEG_EINVAL;
+        a->part[i] = parts[i];
+        a->off[i + 1] = a->off[i] + parts[i].channels;
+    }
+    return SEG_OK;
+}
+
+extern "C" int seg_concat_fwd(const seg_concat_part* parts, int nparts, void* y, int ldy, int ychannels, long P,
+                              int dtype, void* stream) {
+    ConcatArgs a;
+    int st = concat_args(parts, nparts, &a);
+    if (st) return st;
+    if (!y || (ldy & 7) || (ychannels & 7) || ychannels < a.off[nparts] || ldy < ychannels) return SEG_EINVAL;
+    const long total = P * (ychannels / 8);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(concat_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, a, (T*)y, ldy, ychannels / 8, P));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_concat_bwd(const void* dy, int ldy, const seg_concat_part* parts, int nparts, long P, int dtype,
+                              void* stream) {
+    ConcatArgs a;
+    int st = concat_args(parts, nparts, &a);
+    if (st) return st;
+    if (!dy || ldy < a.off[nparts]) return SEG_EINVAL;
+    int chunks = 0;
+    for (int i = 0; i < nparts; ++i) chunks += (parts[i].channels + 7) / 8;
+    const long total = P * chunks;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(concat_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)dy, ldy, a, (const int*)nullptr, P, chunks));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

@@ -315,6 +315,36 @@ def resize_bilinear_bwd(dy, dx_f32, stream=None):
     return dx_f32
 
 
+class ConcatPart(ctypes.Structure):
+    """seg_concat_part (include/segkern.h)."""
+    _fields_ = [("ptr", ctypes.c_void_p), ("ld", ctypes.c_int), ("channels", ctypes.c_int),
+                ("accumulate", ctypes.c_int)]
+
+
+def _parts(items):
+    arr = (ConcatPart * len(items))()
+    for e, (t, c, acc) in zip(arr, items):
+        e.ptr, e.ld, e.channels, e.accumulate = ptr(t), pixel_stride(t), int(c), 1 if acc else 0
+    return arr
+
+
+def concat_fwd(parts, y, channels, stream=None):
+    """tf.concat(axis=-1): parts = [(tensor, valid_channels)], y padded [.., round8(sum)]."""
+    N, H, W, _ = y.shape
+    arr = _parts([(t, c, False) for t, c in parts])
+    check(_lib.lib().seg_concat_fwd(arr, len(parts), ptr(y), pixel_stride(y), round8(channels), N * H * W,
+                                    seg_dtype(y), stream_ptr(stream)), "concat")
+    return y
+
+
+def concat_bwd(dy, parts, stream=None):
+    """Split the concat gradient: parts = [(dst, valid_channels, accumulate)]."""
+    N, H, W, _ = dy.shape
+    arr = _parts(parts)
+    check(_lib.lib().seg_concat_bwd(ptr(dy), pixel_stride(dy), arr, len(parts), N * H * W, seg_dtype(dy),
+                                    stream_ptr(stream)), "concat_grad")
+
+
 def copy_channels(x, y, stream=None):
     N, H, W, C = x.shape
     check(_lib.lib().seg_copy_channels(ptr(x), pixel_stride(x), ptr(y), pixel_stride(y), N * H * W,

@@ -577,6 +577,9 @@ class Session:
                 labels = buf[id(n.labels)]
                 ops.softmax_xent(lg, labels, n.dlogits, n.loss_sum, n.num_classes, n.valid_hw,
                                  grad_scale=1.0 / n.count, ws=self.ws)
+            elif k == "ConcatV2":
+                ops.concat_fwd([(buf[id(t)], p.shapes[id(t)][3]) for t in n.inputs], y,
+                               p.shapes[id(n.output)][3])
             elif k == "ArgMax":
                 x = buf[id(n.inputs[0])]
                 C = p.shapes[id(n.inputs[0])][3]
@@ -750,6 +753,28 @@ class Session:
             elif k == "Add":
                 for t in n.inputs:
                     contribute_alias(t, dy)
+            elif k == "ConcatV2":
+                parts = []
+                for t in n.inputs:
+                    if id(t) not in ng:
+                        # still consume its channel range: a zero-width part is not allowed,
+                        # so write into a scratch gradient that nobody reads
+                        g = p.tmp.get(("cz", id(t)))
+                        if g is None:
+                            g = torch.zeros_like(buf[id(t)])
+                            p.tmp[("cz", id(t))] = g
+                        parts.append((g, p.shapes[id(t)][3], False))
+                        continue
+                    if id(t) in grad:
+                        parts.append((grad[id(t)], p.shapes[id(t)][3], True))
+                    else:
+                        g = p.tmp.get(("g", id(t)))
+                        if g is None:
+                            g = torch.zeros_like(buf[id(t)])
+                            p.tmp[("g", id(t))] = g
+                        grad[id(t)] = g
+                        parts.append((g, p.shapes[id(t)][3], False))
+                ops.concat_bwd(dy, parts)
             elif k == "bn":
                 x = n.inputs[0]
                 C = p.shapes[id(x)][3]

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 from oracle import models as M          # noqa: E402
 from oracle import tf1_ops as T         # noqa: E402
-from tests.model_inputs import he_weights, reference_init_weights, synthetic_batch  # noqa: E402
+from tests.model_inputs import densenet_weights, he_weights, reference_init_weights, synthetic_batch  # noqa: E402
 
 N, H, W = 2, 64, 96
 SLICE = 512
@@ -39,6 +39,28 @@ def fcn_case(weights, img, lab):
         out[f"gnorm/{k}"] = np.array(np.linalg.norm(g))
         out[f"gslice/{k}"] = g[:SLICE].copy()
         out[f"adam1/{k}"] = upd[k].numpy().reshape(-1)[:SLICE].copy()
+    return out
+
+
+DN_N, DN_SLICE = 1, 64
+
+
+def densenet_case(weights, img, lab):
+    """FC-DenseNet (FCDenseNet.py:83-163) 1x64x96x3: logits, loss, per-variable
+    gradient norms, 64-element gradient / Adam slices (SURVEY.md 8c item iii)."""
+    p = {k: torch.from_numpy(v).double().requires_grad_(True) for k, v in weights.items()}
+    pred, logits = M.fcdensenet_forward(p, torch.from_numpy(img).double())
+    loss = T.mean_softmax_xent(logits, T.one_hot(torch.from_numpy(lab), 2))
+    loss.backward()
+    out = {"logits": logits.detach().numpy(), "loss": np.array(loss.item()),
+           "pred": pred.numpy().astype(np.int8)}
+    opt = T.AdamTF1(1e-4)
+    upd = opt.apply({k: v.detach() for k, v in p.items()}, {k: v.grad for k, v in p.items()})
+    for k, v in p.items():
+        g = v.grad.numpy().reshape(-1)
+        out[f"gnorm/{k}"] = np.array(np.linalg.norm(g))
+        out[f"gslice/{k}"] = g[:DN_SLICE].copy()
+        out[f"adam1/{k}"] = upd[k].numpy().reshape(-1)[:DN_SLICE].copy()
     return out
 
 
@@ -94,6 +116,9 @@ def main():
     np.savez_compressed(os.path.join(HERE, "fcn_ref_init.npz"),
                         **fcn_case(reference_init_weights(shapes, 0), img, lab))
     np.savez_compressed(os.path.join(HERE, "fcn_he_init.npz"), **fcn_case(he_weights(shapes, 1), img, lab))
+    dimg, dlab = synthetic_batch(DN_N, H, W, 8)
+    np.savez_compressed(os.path.join(HERE, "fcdensenet_he.npz"),
+                        **densenet_case(densenet_weights(M.fcdensenet_param_shapes(3, 2), 7), dimg, dlab))
     print("golden vectors written to", HERE)
 
 

@@ -28,6 +28,25 @@ def he_weights(shapes, seed):
     return out
 
 
+def densenet_weights(shapes, seed):
+    """FC-DenseNet test weights: He-scaled convs (transposed-conv fan-in =
+    (k/stride)^2 * C_in), BN gamma ~ 1, so activations stay O(1) through the
+    pre-activation stack; first conv scaled for raw 0..255 pixels."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, s in shapes.items():
+        if len(s) == 4:
+            R, S_, A, B = s
+            fan = (R // 2) * (S_ // 2) * B if name.startswith("transition_up") else R * S_ * A
+            out[name] = (rng.standard_normal(s) * math.sqrt(2.0 / fan)).astype(np.float32)
+        elif name.endswith("gamma"):
+            out[name] = (1.0 + 0.1 * rng.standard_normal(s)).astype(np.float32)
+        else:
+            out[name] = (0.1 * rng.standard_normal(s)).astype(np.float32)
+    out["dense_init/weights"] /= np.float32(128.0)
+    return out
+
+
 def reference_init_weights(shapes, seed=0):
     """The reference's init (N(0, 0.01) weights, zero biases; FCN.py:125-127)
     drawn by the product's counter-based generator (variables.init_value)."""

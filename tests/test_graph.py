@@ -55,3 +55,23 @@ def test_shape_helpers_resolve_tf_shape_stack():
     st = tf.stack([s[0], s[1], s[2], 2])
     assert G.resolve_shape(st, lambda t: (5, 64, 96, 3)) == (5, 64, 96, 2)
     assert G.resolve_shape(tf.shape(x), lambda t: (5, 64, 96, 3)) == (5, 64, 96, 3)
+
+
+def test_fcdensenet_variables_match_reference():
+    """FCDenseNet.py:83-163 builds 250 variables (125 bias-free convs incl. 5
+    transposed, 123 BN gamma/beta pairs counted separately) with the
+    reference's auto-generated batch_normalization names."""
+    from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
+    G.reset_default_graph()
+    x = tf.placeholder(tf.float32, [None, 64, 96, 3])
+    kp = tf.placeholder(tf.float32)
+    pred, logits = FCDenseNet(x, kp, 2)
+    vs = {v.var_name: tuple(v.shape) for v in tf.global_variables()}
+    ref = {k: tuple(s) for k, s in M.fcdensenet_param_shapes(3, 2).items()}
+    assert vs == ref
+    assert logits.shape[1:] == (64, 96, 2)
+    assert pred.shape[-1] == 1
+    # channel widths of the encoder skips (SURVEY.md 8a-15: 128/160/208/280/348/430)
+    assert ref["transition_up1/weights"] == (4, 4, 348, 430)
+    assert ref["transition_up5/weights"] == (4, 4, 128, 320)
+    assert ref["final_conv/weights"] == (1, 1, 256, 2)

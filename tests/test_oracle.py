@@ -147,3 +147,15 @@ def test_fcn_golden_vectors(which):
     if which == "ref":
         # reference init: activations vanish, loss ~ ln 2
         assert abs(float(gold["loss"]) - math.log(2)) < 1e-3
+
+
+def test_fcdensenet_golden_vectors():
+    """FC-DenseNet oracle (FCDenseNet.py:23-163) pinned to its committed fixture."""
+    from tests.model_inputs import densenet_weights
+    w = densenet_weights(M.fcdensenet_param_shapes(3, 2), 7)
+    img, lab = synthetic_batch(MG.DN_N, MG.H, MG.W, 8)
+    now = MG.densenet_case(w, img, lab)
+    gold = np.load(os.path.join(GOLD, "fcdensenet_he.npz"))
+    assert set(gold.files) == set(now)
+    for k in gold.files:
+        np.testing.assert_allclose(now[k], gold[k], rtol=1e-9, atol=1e-30, err_msg=k)

@@ -122,3 +122,31 @@ def test_tconv_shape_rule_at_375x1242(dry):
     sess = S.Session(device=torch.device("cpu"))
     with pytest.raises(ValueError):
         sess.run(logits, feed_dict={image: np.zeros((1, 375, 1242, 3), np.float32)})
+
+
+def test_fcdensenet_train_plan(dry):
+    """C3 model plans: 125 convs + 5 transposed, pre-activation BN+ReLU fused,
+    64 concats executed (fwd) and split (bwd), dropout as separate nodes."""
+    from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
+    G.reset_default_graph()
+    H, W = 64, 96
+    image = tf.placeholder(tf.float32, [None, H, W, 3])
+    labels = tf.placeholder(tf.uint8, [None, H, W])
+    keep = tf.placeholder(tf.float32)
+    pred, logits = FCDenseNet(image, keep, 2)
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="bf16")
+    sess.run(tf.global_variables_initializer())
+    dry.calls.clear()
+    sess.run([train, loss], feed_dict={image: np.zeros((1, H, W, 3), np.float32),
+                                       labels: np.zeros((1, H, W), np.uint8), keep: 0.8})
+    c = dry.calls
+    assert c.count("seg_conv2d_fwd") == 125          # stem + 118 bottleneck + 5 transition + head
+    assert c.count("seg_tconv2d_fwd") == 5
+    assert c.count("seg_concat_fwd") == 5 * 1 + sum(n + 1 for n in (4, 5, 7, 10, 12, 15))
+    assert c.count("seg_concat_bwd") == c.count("seg_concat_fwd")
+    assert c.count("seg_bn_relu_fwd") == 123 and c.count("seg_bn_relu_bwd") == 123
+    assert c.count("seg_avgpool2x2_fwd") == 5
+    assert c.count("seg_conv2d_bwd_filter") == 125
+    assert c.count("seg_adam_tf1_pack") == 1
