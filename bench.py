@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--kernel-table", action="store_true", help="print per-launch timings to stderr")
+    ap.add_argument("--no-overlap-optimizer", action="store_true",
+                    help="run the fused Adam once after backward instead of per layer on a side stream")
     return ap.parse_args()
 
 
@@ -149,7 +151,8 @@ def main():
     loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
                                                                    valid_hw=(H, W)))
     train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
-    sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp)
+    sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp,
+                      overlap_optimizer=not args.no_overlap_optimizer)
     sess.run(tf.global_variables_initializer())
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
     feed = {image: img, labels: lab, keep: kp}

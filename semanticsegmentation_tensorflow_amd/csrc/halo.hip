@@ -36,6 +36,7 @@ int g_halo_wide = 1;
 int g_halo_stagger = 1;
 int g_halo_phases = 2;
 int g_res64 = 1;
+int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -308,14 +309,15 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
 // MFMA, 3 = no LDS fragment reads.
 // PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
 // both B halves read in the first).
-template <int BW, bool STAG, int ABL = 0, int PH = 4>
+template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256>
 __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     using T = bf16;
-    constexpr int NW = 8, BM = 256, BN = 256, BH = BM / BW, HI = 6;
+    constexpr int NW = 8, BM = 256, BN = BNT, BH = BM / BW, HI = 6;
+    constexpr int WTN = BN / 4, NFH = WTN / 32;   // per-wave columns, n-fragments per B half
     constexpr int HBUF = HI * NW * 1024;
     constexpr int BBUF = BN * 128;
     constexpr int SMEM = 2 * HBUF + 2 * BBUF;
-    constexpr int B_INS = BN / 8 / NW;   // 4
+    constexpr int B_INS = BN / 8 / NW;   // 4 (BN 256) or 2 (BN 128)
     static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -384,11 +386,11 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         }
     };
 
-    f32x4 acc[8][4];
+    f32x4 acc[8][2 * NFH];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 2 * NFH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (iters > 0) {
         for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         const char* Hs = smem + hbuf * HBUF;
         const char* Bs = smem + 2 * HBUF + bbuf * BBUF;
         const int toff = (t_j * p.tsh - g.hy0) * g.hwd + t_i * p.tsw - g.hx0;
-        uint4 af[2][4], bq[2][2][2];   // A half [ks][mi]; B [nh][ks][ni]
+        uint4 af[2][4], bq[2][2][NFH];   // A half [ks][mi]; B [nh][ks][ni]
         auto read_a = [&](int mh) {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -425,8 +427,8 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni) {
-                    const int row = wn * 64 + nh * 32 + ni * 16 + fr;
+                for (int ni = 0; ni < NFH; ++ni) {
+                    const int row = wn * WTN + nh * (WTN / 2) + ni * 16 + fr;
                     if constexpr (ABL == 3) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
                     else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
                 }
@@ -439,13 +441,13 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < 2; ++ni) {
+                    for (int ni = 0; ni < NFH; ++ni) {
                         if constexpr (ABL == 2) {
                             asm volatile("" ::"v"(af[ks][mi].x), "v"(af[ks][mi].w), "v"(bq[nh][ks][ni].x), "v"(bq[nh][ks][ni].w));
                         } else {
-                            acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            acc[mh * 4 + mi][nh * NFH + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[nh][ks][ni]),
-                                acc[mh * 4 + mi][nh * 2 + ni], 0, 0, 0);
+                                acc[mh * 4 + mi][nh * NFH + ni], 0, 0, 0);
                         }
                     }
             __builtin_amdgcn_s_setprio(0);
@@ -522,18 +524,19 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 const long m = ((long)img * p.OH + oy) * p.OW + ox;
                 float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni) {
-                    const int col = n0 + wn * 64 + ni * 16 + fr;
+                for (int ni = 0; ni < 2 * NFH; ++ni) {
+                    const int col = n0 + wn * WTN + ni * 16 + fr;
                     if (col < p.N) prow[col] = acc[mi][ni][r];
                 }
             }
         return;
     }
-    // ---- epilogue in two 64-row halves per wave (LDS holds 8 x 64 x 64 fp32)
-    constexpr int SROW = 64 * 4 + 16;
+    // ---- epilogue in two 64-row halves per wave (LDS holds 8 x 64 x WTN fp32)
+    constexpr int SROW = WTN * 4 + 16;
+    constexpr int CPR = WTN / 8, RPP = 64 / CPR;
     static_assert(NW * 64 * SROW <= SMEM, "epilogue staging must fit");
-    const int cch = lane & 7, rsub = lane >> 3;
-    const int col0 = n0 + wn * 64 + cch * 8;
+    const int cch = lane % CPR, rsub = lane / CPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
     const EpiParams& e = p.epi;
     float bias[8], scl[8], shf[8];
 #pragma unroll
@@ -553,12 +556,12 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < 2 * NFH; ++ni)
                     *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
                         acc[mh * 4 + mi][ni][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll 2
-        for (int rr = rsub; rr < 64; rr += 8) {
+        for (int rr = rsub; rr < 64; rr += RPP) {
             const int ml = wm * 128 + mh * 64 + rr;
             const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
             if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
@@ -583,7 +586,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 if (e.relu) x = fmaxf(x, 0.f);
                 if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
                 if (e.residual) x += res[j];
-            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
             }
             T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
@@ -918,6 +921,12 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {
     g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
     g.hwd = hp.geom[4]; g.hrows = hp.geom[5]; g.hy0 = hp.geom[6]; g.hx0 = hp.geom[7];
     g.nchunks = hp.geom[8]; g.kc_per_split = hp.geom[9];
+    if (hp.bn == 128 && hp.hi == 6 && g_halo_wide && g_halo2_n128) {
+        const dim3 grid((unsigned)hp.tiles, 1, gridz);
+        if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 128>), grid, dim3(512), 0, s, p, g);
+        else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 128>), grid, dim3(512), 0, s, p, g);
+        return;
+    }
     if (hp.bn == 256) {
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
         if (g_nt2_ablate && hp.bw == 16) {

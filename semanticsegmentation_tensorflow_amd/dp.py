@@ -28,6 +28,10 @@ class DataParallel:
         self.buckets = []
         self.var_bucket = {}
         self.store = None
+        # optional hook (work_or_None, var_names) called as each bucket's
+        # all-reduce is issued: the Session runs that bucket's Adam update on a
+        # side stream once the collective completes
+        self.on_launch = None
 
     def prepare(self, store):
         """Cut the flat gradient buffer into contiguous buckets (backward order)."""
@@ -63,12 +67,15 @@ class DataParallel:
         self.works = []
 
     def _launch(self, i):
-        s, e, _ = self.buckets[i]
+        s, e, names = self.buckets[i]
+        w = None
         if e > s:
             w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
                                 async_op=True)
             self.works.append(w)
         self.launched[i] = True
+        if self.on_launch is not None:
+            self.on_launch(w, names)
 
     def ready(self, names):
         for nm in names:

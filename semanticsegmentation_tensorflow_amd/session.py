@@ -52,8 +52,58 @@ def _np(x):
     return torch.from_numpy(np.ascontiguousarray(x))
 
 
+class _AdamOverlap:
+    """Per-step driver of the overlapped optimizer: each variable group's fused
+    Adam + pack launch runs on a side stream after an event on the compute
+    stream (or, with data parallelism, after the bucket's all-reduce), so the
+    HBM-bound update of layer L hides under the MFMA-bound backward of layers
+    < L.  Nothing later in the step reads L's parameters or packed copies
+    (its input gradient is enqueued before its filter gradient).  finish()
+    updates the remaining variables and makes the compute stream wait."""
+
+    def __init__(self, sess, opt, gs):
+        self.s = sess
+        self.opt = opt
+        self.gs = gs
+        if sess._side is None:
+            sess._side = torch.cuda.Stream(device=sess.device)
+        self.side = sess._side
+        self.main = torch.cuda.current_stream(sess.device)
+        self.done = set()
+
+    def _adam(self, names):
+        st = self.s.store
+        o = self.opt
+        ops.adam_tf1_pack(st.params, st.grads, st.m, st.v, self.s._adam_plan(names), o.lr, st.step, o.beta1,
+                          o.beta2, o.epsilon, grad_scale=self.gs, dtype=self.s._pack_dtype(), stream=self.side)
+        self.done.update(names)
+
+    def launch(self, names):
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        self._adam(names)
+
+    def after_work(self, work, names):
+        if work is not None:
+            with torch.cuda.stream(self.side):
+                work.wait()
+        else:
+            ev = torch.cuda.Event()
+            ev.record(self.main)
+            self.side.wait_event(ev)
+        self._adam(names)
+
+    def finish(self):
+        rest = [v.var_name for v in self.s.store.order if v.var_name not in self.done]
+        if rest:
+            self.launch(rest)
+        self.main.wait_stream(self.side)
+
+
 class Session:
-    def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None):
+    def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None,
+                 overlap_optimizer=True):
         self.graph = graph or G.get_default_graph()
         if not torch.cuda.is_available():
             raise RuntimeError("Session needs an MI355X (HIP device); there is no CPU fallback")
@@ -69,6 +119,10 @@ class Session:
         self._packed_version = -1
         self._adam_key = None
         self._adam = None
+        self._adam_groups = {}
+        self.overlap_optimizer = overlap_optimizer
+        self._side = None
+        self._adam_ctx = None
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
 
     # ------------------------------------------------------------------ vars
@@ -463,15 +517,31 @@ class Session:
             ops.pack_filter(store.param(name), t, ap, bp, mode)
         self._packed_version = store.version
 
-    def _adam_plan(self):
+    def _adam_plan(self, names=None):
         """Segment table of the fused Adam + pack launch: every variable of the
-        store, with the packed copies that exist (rebuilt when packs are added)."""
+        store (or the subset `names`), with the packed copies that exist
+        (rebuilt when packs are added)."""
         store = self.store
         key = (len(store.packed), store.numel)
+        if names is not None:
+            gk = (key, tuple(names))
+            plan = self._adam_groups.get(gk)
+            if plan is None:
+                plan = ops.AdamPlan(self._adam_segments(set(names)), self.device)
+                self._adam_groups[gk] = plan
+            return plan
         if self._adam_key == key:
             return self._adam
+        self._adam = ops.AdamPlan(self._adam_segments(None), self.device)
+        self._adam_key = key
+        return self._adam
+
+    def _adam_segments(self, subset):
+        store = self.store
         segs = []
         for v in store.order:
+            if subset is not None and v.var_name not in subset:
+                continue
             shape = tuple(v.shape)
             n = int(np.prod(shape))
             if len(shape) == 4:
@@ -488,9 +558,7 @@ class Session:
                 else:
                     tr = e
             segs.append((store.offset[v.var_name], rs, a, b, rows, tr))
-        self._adam = ops.AdamPlan(segs, self.device)
-        self._adam_key = key
-        return self._adam
+        return segs
 
     def _feed(self, p, feed_dict):
         feeds = {id(k): v for k, v in feed_dict.items()}
@@ -590,18 +658,27 @@ class Session:
                 raise NotImplementedError(k)
         # ---------------- backward + optimizer
         if p.train:
-            self._backward(p, scal)
             ts = p.train.attrs
             opt = ts["optimizer"]
-            gs = ts["grad_scale"]
+            gs = ts["grad_scale"] / (self.dp.world if self.dp is not None else 1)
+            fresh = self._packed_version == store.version
+            store.step += 1
+            if self.overlap_optimizer and self.device.type == "cuda":
+                # per-layer Adam on a side stream as soon as the layer's gradient is final
+                self._adam_ctx = _AdamOverlap(self, opt, gs)
+                if self.dp is not None:
+                    self.dp.on_launch = self._adam_ctx.after_work
+            self._backward(p, scal)
             if self.dp is not None:
                 self.dp.finish()
-                gs = gs / self.dp.world
-            store.step += 1
-            fresh = self._packed_version == store.version
-            ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(), opt.lr,
-                              store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
-                              dtype=ops.BF16 if self.tdt == torch.bfloat16 else ops.F32)
+                self.dp.on_launch = None
+            if self._adam_ctx is not None:
+                self._adam_ctx.finish()
+                self._adam_ctx = None
+            else:
+                ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(), opt.lr,
+                                  store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
+                                  dtype=self._pack_dtype())
             store.version += 1
             if fresh:           # the fused update rewrote every packed copy
                 self._packed_version = store.version
@@ -636,6 +713,18 @@ class Session:
         one = torch.ones(C, dtype=torch.float32, device=self.device)
         zero = torch.zeros(C, dtype=torch.float32, device=self.device)
         ops.bn_relu_fwd(x, y, one, zero, C, True, eps=0.0)
+
+    def _pack_dtype(self):
+        return ops.BF16 if self.tdt == torch.bfloat16 else ops.F32
+
+    def _grad_ready(self, names):
+        """The gradients of `names` are final once the kernels enqueued so far
+        run: hand them to the all-reduce (DP) or straight to the overlapped
+        optimizer."""
+        if self.dp is not None:
+            self.dp.ready(names)
+        elif self._adam_ctx is not None:
+            self._adam_ctx.launch(names)
 
     def _mask_epi(self, p, x):
         """Epilogue fusing the ReluGrad (x 1/keep_prob) of x's producer into the
@@ -719,8 +808,7 @@ class Session:
                     done(dx, acc)
                 self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
                             store.grad(n.w.var_name), ws, None, fused_db)
-                if self.dp is not None:
-                    self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
+                self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "tconv":
                 x = n.inputs[0]
                 if n.residual is not None:
@@ -734,8 +822,7 @@ class Session:
                 self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
                             store.grad(n.w.var_name), ws, None,
                             store.grad(n.bias.var_name) if n.bias is not None else None)
-                if self.dp is not None:
-                    self.dp.ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
+                self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
                 if id(x) in ng:
@@ -783,8 +870,7 @@ class Session:
                                 store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
                                 n.eps, ws)
                 done(dx, acc)
-                if self.dp is not None:
-                    self.dp.ready([n.gamma.var_name, n.beta.var_name])
+                self._grad_ready([n.gamma.var_name, n.beta.var_name])
             elif k == "Relu":
                 x = n.inputs[0]
                 dx, acc = dest(x)

@@ -17,25 +17,29 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7],
+                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128"])
 def ntv(request, dev):
     """Run NT tests on every kernel generation: 1 = register-staged GEMM,
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
     (bf16, stride 1, C % 64 == 0; 256x256 four-phase tiles for N > 128),
     4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
-    stagger (two-phase schedule), 6 = 3 with four phases per iteration."""
+    stagger (two-phase schedule), 6 = 3 with four phases per iteration,
+    7 = 3 with the two-phase kernel also for N <= 128 (off by default)."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
     ops.set_option("nt_halo", 1 if v >= 3 else 0)
     ops.set_option("halo_wide", 0 if v == 4 else 1)
     ops.set_option("halo_stagger", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
+    ops.set_option("halo2_n128", 1 if v == 7 else 0)
     yield v
     ops.set_option("igemm_nt_variant", 2)
     ops.set_option("nt_halo", 1)
     ops.set_option("halo_wide", 1)
     ops.set_option("halo_stagger", 1)
     ops.set_option("halo_phases", 2)
+    ops.set_option("halo2_n128", 0)
 
 
 DTYPES = [torch.float32, torch.bfloat16]
