@@ -19,6 +19,7 @@ restatement timed on this host's cores, N=1 only).
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -47,8 +48,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--kernel-table", action="store_true", help="print per-launch timings to stderr")
-    ap.add_argument("--no-overlap-optimizer", action="store_true",
-                    help="run the fused Adam once after backward instead of per layer on a side stream")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--overlap-optimizer", action="store_true",
+                    help="per-layer Adam on a side stream as gradients become final (measured slower: the "
+                         "HBM-bound update steals CUs from the MFMA-bound backward)")
     return ap.parse_args()
 
 
@@ -115,6 +120,81 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
 
 
+def kernel_symbol(name):
+    """rocprof symbol pattern of a seg_conv_kernel_info family name (the main
+    kernel; its split-K reducer launches are attributed to it separately)."""
+    fam, rest = name.split("<", 1)
+    a = rest.rstrip(">").split(",")
+    bm, bn = a[1], a[2]
+    if fam == "conv_halo":
+        return r"conv_halo2<" if bn == "256" else r"conv_halo<"
+    if fam == "igemm_nt2":
+        return rf"igemm_nt2I\w*Li{bm}ELi{bn}E"
+    if fam == "igemm_tn2":
+        return rf"igemm_tn2<{bm}, {bn},"
+    if fam == "wgrad_halo":
+        return rf"wgrad_halo<\d+, {bn},"
+    return {"conv_res64": r"conv_res64<", "conv_c8": r"conv_c8_fwd", "wgrad_c8": r"wgrad_c8",
+            "igemm_nt": r"igemm_ntI", "igemm_tn": r"igemm_tnI"}.get(fam, re.escape(fam))
+
+
+def pmc_traffic(argv, symbol, out_dir):
+    """HBM bytes per launch of the dominant kernel from two separate rocprofv3
+    --pmc passes over a child run of this benchmark (one warm-up + one timed
+    step; only the last step's dispatches are used).  Corrections per
+    MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB;
+    on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming
+    read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  A
+    launch's split-K reducer dispatches are attributed to it."""
+    import csv
+    import shutil
+    import signal
+    import subprocess
+    res = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out_dir, ctr.lower())
+        shutil.rmtree(d, ignore_errors=True)
+        cmd = ["rocprofv3", "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+               "--", sys.executable, os.path.abspath(__file__)] + argv + ["--pmc-child"]
+        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env,
+                             start_new_session=True)
+        try:
+            p.wait(timeout=180)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            raise RuntimeError(f"rocprofv3 --pmc {ctr} timed out")
+        path = None
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    path = os.path.join(root, f)
+        if p.returncode != 0 or path is None:
+            raise RuntimeError(f"rocprofv3 --pmc {ctr} failed (rc={p.returncode})")
+        rows = list(csv.DictReader(open(path)))
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        starts = [i for i, r in enumerate(rows) if "prepare_input" in r["Kernel_Name"]]
+        step = rows[starts[-1]:]
+        pat = re.compile(symbol)
+        total, launches, inside = 0.0, 0, False
+        for r in step:
+            k = r["Kernel_Name"]
+            if pat.search(k):
+                launches += 1
+                inside = True
+                total += float(r["Counter_Value"])
+            elif inside and "splitk_reduce" in k:
+                total += float(r["Counter_Value"])
+            else:
+                inside = False
+        if launches == 0:
+            raise RuntimeError(f"no dispatch of {symbol} in the PMC pass")
+        res[ctr] = total * 1024.0 / launches * (2.0 if ctr == "FETCH_SIZE" else 1.0)
+        res["launches"] = launches
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -152,7 +232,7 @@ def main():
                                                                    valid_hw=(H, W)))
     train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
     sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp,
-                      overlap_optimizer=not args.no_overlap_optimizer)
+                      overlap_optimizer=args.overlap_optimizer)
     sess.run(tf.global_variables_initializer())
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
     feed = {image: img, labels: lab, keep: kp}
@@ -171,6 +251,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.pmc_child:
+        return
     if dp:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -248,6 +330,18 @@ def main():
         "conv_gflop_per_step_measured": round(step_conv_flops / 1e9, 2),
         "loss_after": round(loss_val, 5),
     }
+    if rank == 0 and world == 1 and not args.no_traffic:
+        try:
+            argv = [a for a in sys.argv[1:] if a not in ("--kernel-table",)]
+            argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic"]
+            t = pmc_traffic(argv, kernel_symbol(dname), os.path.join(ROOT, "gpurun_out", "bench_pmc"))
+            result["roofline"]["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
+            result["roofline"]["traffic_detail"] = {
+                "unit": "bytes per launch", "fetch_x2": round(t["FETCH_SIZE"]), "write": round(t["WRITE_SIZE"]),
+                "symbol": kernel_symbol(dname), "launches": t["launches"],
+                "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes; FETCH_SIZE doubled (gfx950)"}
+        except Exception as exc:  # report, never crash the headline line
+            result["roofline"]["traffic_error"] = repr(exc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps, args.model)

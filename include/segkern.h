@@ -118,6 +118,13 @@ int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_c
 /* Filter gradient in TF layout [R][S][k_valid][c_valid], fp32; dbias as above. */
 int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
                            float* dw_f32, float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* Output-channel extent `a_pad` of the packed tconv filters (modes 2 and 3)
+ * that the three tconv entry points expect for this descriptor: d->K (the
+ * channel count padded to 8) in general; the true even channel count for a
+ * "tap-dense" tconv (few output channels, stride >= 4, square kernel -- FCN
+ * conv_t3, Network/model/FCN.py:101-107), whose GEMMs skip padding channels.
+ * Negative status on an invalid descriptor. */
+int seg_tconv_filter_apad(const seg_conv_desc* d);
 
 /* Workspace bytes for op: 0 fwd, 1 bwd_data, 2 bwd_filter, 3 tconv fwd,
  * 4 tconv bwd_data, 5 tconv bwd_filter. */

@@ -100,6 +100,7 @@ SIGNATURES = {
     "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_conv_workspace": (_Z, [_DP, _I]),
+    "seg_tconv_filter_apad": (_I, [_DP]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
                                   ctypes.POINTER(ctypes.c_double)]),

@@ -182,16 +182,26 @@ static TNParams tconv_bwd_filter_params(const seg_conv_desc* d) {
 }
 
 
-// conv2d_transpose forward for few output channels (FCN conv_t3: 256 -> 2,
-// k16 s8): Z[p_in][(r,s,k)] = sum_c x[p_in][c] * W[r][s][k][c] as one dense
-// GEMM (N = R*S*K, every phase at once), then each output pixel gathers its
-// (R/st)*(S/st) contributions: y[oh][ow][k] = b[k] + res + sum Z[ih][iw][(r,s,k)].
-template <typename T>
+// conv2d_transpose with few output channels and a large stride (FCN conv_t3:
+// 256 -> 2, k16 s8): the "tap-dense" path.  Its packed filters keep the true
+// output-channel count Kq (even, <= 8) instead of padding it to 8, so no MFMA
+// work is spent on padding channels:
+//   forward   Z[p_in][(r,s,k)] = sum_c x[p_in][c] W[r][s][k][c]  (dense GEMM,
+//             N = R*S*Kq), then every output pixel gathers its (R/st)*(S/st)
+//             taps: y[oh][ow][k] = b[k] + res + sum Z[ih][iw][(r,s,k)];
+//   input grad  D[p_in][(r,s,k)] = dy[ih*st - pt + r][iw*st - pl + s][k] (gather),
+//             dx = D . Wt^T with Wt = [c][(r,s,k)] (dense GEMM, K = R*S*Kq);
+//   filter grad dW[(r,s,k)][c] = sum_p D[p][(r,s,k)] x[p][c] (dense TN GEMM).
+template <typename T, int KQ>
 __global__ void tconv_col2im_k(const T* __restrict__ Z, T* __restrict__ y, int N, int H, int W, int OH, int OW,
-                               int Kp, int kv, int R, int S, int st, int pt, int pl, int ldy,
+                               int kv, int R, int S, int st, int pt, int pl, int ldy,
                                const float* __restrict__ bias, const T* __restrict__ res, int ldr) {
+    static_assert(KQ == 2 || KQ == 4 || KQ == 8, "tap-dense channel counts");
     const long total = (long)N * OH * OW;
-    const int zrow = R * S * Kp;
+    const int zrow = R * S * KQ;
+    float b8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b8[k] = (bias && k < kv) ? bias[k] : 0.f;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int ow = (int)(i % OW);
         const long t = i / OW;
@@ -207,12 +217,15 @@ __global__ void tconv_col2im_k(const T* __restrict__ Z, T* __restrict__ y, int N
             for (int s2 = rw; s2 < S; s2 += st) {
                 const int iw = (ow + pl - s2) / st;
                 if (iw < 0 || iw >= W) continue;
-                const T* zp = Z + (((long)n * H + ih) * W + iw) * zrow + (r * S + s2) * Kp;
-                float v[8];
-                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(zp), v);
-                if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(zp + 4), v + 4);
+                const T* zp = Z + (((long)n * H + ih) * W + iw) * zrow + (r * S + s2) * KQ;
+                if constexpr (sizeof(T) == 2 && KQ == 2) {
+                    const unsigned u = *reinterpret_cast<const unsigned*>(zp);
+                    acc[0] += __uint_as_float(u << 16);
+                    acc[1] += __uint_as_float(u & 0xffff0000u);
+                } else {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) acc[k] += v[k];
+                    for (int k = 0; k < KQ; ++k) acc[k] += to_f32(zp[k]);
+                }
             }
         }
         float r8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -222,22 +235,101 @@ __global__ void tconv_col2im_k(const T* __restrict__ Z, T* __restrict__ y, int N
             if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), r8 + 4);
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = k < kv ? acc[k] + (bias ? bias[k] : 0.f) + r8[k] : 0.f;
+        for (int k = 0; k < 8; ++k) acc[k] = k < kv ? acc[k] + b8[k] + r8[k] : 0.f;
         T* yp = y + i * ldy;
         *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(acc);
         if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(acc + 4);
     }
 }
 
-static bool tconv_use_gemm(const seg_conv_desc* d) {
-    return d->K == 8 && d->stride_h == d->stride_w && d->stride_h >= 4 && d->R == d->S;
+// D[p_in][(r,s,k)] for the tap-dense input / filter gradients.  One thread per
+// 16-byte chunk of a row = 8 / KQ consecutive taps (r, s..s+8/KQ-1) of one
+// input pixel: KQ-channel reads (4 bytes for bf16 KQ=2) of consecutive output
+// pixels, so a wave covers 16 output pixels of each of 2..8 filter rows.
+template <typename T, int KQ>
+__global__ void tconv_gather_dy_k(const T* __restrict__ dy, T* __restrict__ D, int N, int H, int W, int OH, int OW,
+                                  int ldy, int R, int S, int st, int pt, int pl) {
+    constexpr int TPC = 8 / KQ;                       // taps per 16-byte chunk
+    const int row = R * S * KQ, r8 = row / 8;
+    const long total = (long)N * H * W * r8;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int q = (int)(i % r8);
+        const long pix = i / r8;
+        const int iw = (int)(pix % W);
+        const long t = pix / W;
+        const int ih = (int)(t % H);
+        const int n = (int)(t / H);
+        const int tap0 = q * TPC;
+        const int r = tap0 / S, s0 = tap0 - (tap0 / S) * S;   // S % TPC == 0: one filter row
+        const int oh = ih * st - pt + r;
+        const bool rok = (unsigned)oh < (unsigned)OH;
+        const T* src = dy + ((long)n * OH + (rok ? oh : 0)) * OW * ldy;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < TPC; ++j) {
+            const int ow = iw * st - pl + s0 + j;
+            const bool ok = rok && (unsigned)ow < (unsigned)OW;
+            if constexpr (sizeof(T) == 2 && KQ == 2) {
+                const unsigned u = ok ? *reinterpret_cast<const unsigned*>(src + (long)ow * ldy) : 0u;
+                v[2 * j] = __uint_as_float(u << 16);
+                v[2 * j + 1] = __uint_as_float(u & 0xffff0000u);
+            } else {
+#pragma unroll
+                for (int k = 0; k < KQ; ++k) v[j * KQ + k] = ok ? to_f32(src[(long)ow * ldy + k]) : 0.f;
+            }
+        }
+        T* dp = D + pix * row + q * 8;
+        *reinterpret_cast<uint4*>(dp) = Chunk<T>::pack(v);
+        if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(dp + 4) = Chunk<T>::pack(v + 4);
+    }
 }
 
-static size_t tconv_gemm_ws(const seg_conv_desc* d) {
+// tap-dense applies: few (even) output channels, K padded to 8, stride >= 4, square kernel
+static int tconv_dense_kq(const seg_conv_desc* d) {
+    if (d->K != 8 || d->stride_h != d->stride_w || d->stride_h < 4 || d->R != d->S) return 0;
+    const int kq = d->k_valid;
+    if (kq != 2 && kq != 4 && kq != 8) return 0;
+    if ((d->R * d->S * kq) % 8 || d->S % (8 / kq)) return 0;
+    return kq;
+}
+
+static size_t tconv_dense_zbytes(const seg_conv_desc* d) {
     const size_t esz = d->dtype == SEG_BF16 ? 2 : 4;
-    NTParams z = {};
-    const int M = d->N * d->H * d->W, Nn = d->R * d->S * d->K;
-    return (size_t)M * Nn * esz + seg::nt_workspace(M, Nn, d->C, d->dtype, 0) + 256;
+    return ((size_t)d->N * d->H * d->W * d->R * d->S * tconv_dense_kq(d) * esz + 255) & ~(size_t)255;
+}
+
+// the dense GEMM over the Z / D matrix viewed as a 1x1 "conv" of C_g channels
+static NTParams dense_nt(int M, int N, int K, const void* x, int ldx, const void* w, void* y, int ldy) {
+    NTParams g = {};
+    g.M = M; g.N = N; g.K = K;
+    g.x = x; g.x_img = (long)M * ldx; g.IH = 1; g.IW = M; g.C = K; g.ldx = ldx;
+    g.Ha = 1; g.Wa = M; g.ish = 1; g.isw = 1; g.ioh = 0; g.iow = 0; g.tsh = 1; g.tsw = 1; g.taps_w = 1;
+    g.w = w; g.w_col = K; g.w_tap = K; g.rstep = 1; g.sstep = 1; g.Sfull = 1;
+    g.y = y; g.y_img = (long)M * ldy; g.OH = 1; g.OW = M; g.ldy = ldy; g.osh = 1; g.osw = 1;
+    g.epi.n_valid = N; g.epi.keep_prob = 1.f;
+    return g;
+}
+
+static int launch_gather_dy(const seg_conv_desc* d, const void* dy, void* D, hipStream_t st) {
+    const int kq = tconv_dense_kq(d);
+    const long total = (long)d->N * d->H * d->W * (d->R * d->S * kq / 8);
+    const int grid = seg_grid_1d(total, 256);
+#define GATHER(T, KQ) hipLaunchKernelGGL((tconv_gather_dy_k<T, KQ>), dim3(grid), dim3(256), 0, st, (const T*)dy, (T*)D, \
+                                         d->N, d->H, d->W, d->OH, d->OW, d->ldy, d->R, d->S, d->stride_h, d->pad_top, d->pad_left)
+    if (d->dtype == SEG_BF16) {
+        if (kq == 2) GATHER(bf16, 2); else if (kq == 4) GATHER(bf16, 4); else GATHER(bf16, 8);
+    } else {
+        if (kq == 2) GATHER(float, 2); else if (kq == 4) GATHER(float, 4); else GATHER(float, 8);
+    }
+#undef GATHER
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_tconv_filter_apad(const seg_conv_desc* d) {
+    if (check_desc(d)) return -SEG_EINVAL;
+    const int kq = tconv_dense_kq(d);
+    return kq ? kq : d->K;
 }
 
 extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
@@ -256,9 +348,26 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
                                           sizeof(float));
             return std::max(need, seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
         }
-        case 3: return tconv_use_gemm(d) ? tconv_gemm_ws(d) : 0;
-        case 4: { NTParams p = tconv_bwd_data_params(d); return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0); }
+        case 3:
+            if (tconv_dense_kq(d)) {
+                const int M = d->N * d->H * d->W, Nn = d->R * d->S * tconv_dense_kq(d);
+                return tconv_dense_zbytes(d) + seg::nt_workspace(M, Nn, d->C, d->dtype, 0);
+            }
+            return 0;
+        case 4: {
+            if (tconv_dense_kq(d)) {
+                const int M = d->N * d->H * d->W, Kd = d->R * d->S * tconv_dense_kq(d);
+                return tconv_dense_zbytes(d) + seg::nt_workspace(M, d->C, Kd, d->dtype, 0);
+            }
+            NTParams p = tconv_bwd_data_params(d);
+            return seg::nt_workspace(p.M, p.N, p.K, d->dtype, 0);
+        }
         case 5: {
+            if (tconv_dense_kq(d)) {
+                const int P = d->N * d->H * d->W, Md = d->R * d->S * tconv_dense_kq(d);
+                return tconv_dense_zbytes(d) + std::max(seg::tn_workspace(Md, d->C, P, d->dtype),
+                                                        seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
+            }
             TNParams p = tconv_bwd_filter_params(d);
             return std::max(seg::tn_workspace(p.M, p.N, p.P, d->dtype),
                             seg_bias_grad_workspace((long)d->N * d->OH * d->OW, d->K));
@@ -311,8 +420,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             break;
         }
         case 3: {
-            if (tconv_use_gemm(d)) {
-                seg::nt_info(d->N * d->H * d->W, d->R * d->S * d->K, d->C, d->dtype, 0, &bm, &bn, &sp);
+            if (tconv_dense_kq(d)) {
+                seg::nt_info(d->N * d->H * d->W, d->R * d->S * tconv_dense_kq(d), d->C, d->dtype, 0, &bm, &bn, &sp);
             } else {
                 NTParams p = tconv_fwd_params(d);
                 seg::nt_info(p.M, p.N, p.K, d->dtype, 1, &bm, &bn, &sp);
@@ -320,12 +429,24 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             macs = macs_t;
             break;
         }
-        case 4: { NTParams p = tconv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); macs = macs_t; break; }
-        case 5: { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); fam = "igemm_tn"; macs = macs_t; break; }
+        case 4: {
+            if (tconv_dense_kq(d)) seg::nt_info(d->N * d->H * d->W, d->C, d->R * d->S * tconv_dense_kq(d), d->dtype, 0, &bm, &bn, &sp);
+            else { NTParams p = tconv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); }
+            macs = macs_t;
+            break;
+        }
+        case 5: {
+            if (tconv_dense_kq(d)) seg::tn_info(d->R * d->S * tconv_dense_kq(d), d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
+            else { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); }
+            fam = "igemm_tn";
+            macs = macs_t;
+            break;
+        }
         default: return SEG_EINVAL;
     }
     if (bm == 256 && fam[0] == 'i' && fam[6] == 'n') fam = "igemm_nt2";
-    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[0] == 'i' && fam[6] == 't' && (op == 2 ? d->R * d->S * d->C : d->R * d->S * d->K) >= 128)
+    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[0] == 'i' && fam[6] == 't' &&
+        (op == 2 ? d->R * d->S * d->C : d->R * d->S * (tconv_dense_kq(d) ? tconv_dense_kq(d) : d->K)) >= 128)
         fam = "igemm_tn2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
     if (splits) *splits = sp;
@@ -455,20 +576,13 @@ extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void
     if (st) return st;
     if (!x || !w || !y) return SEG_EINVAL;
     if (d->R % d->stride_h || d->S % d->stride_w) return SEG_EINVAL;
-    if (tconv_use_gemm(d)) {
-        // dense GEMM over all taps: a 1x1 "conv" with K_gemm = C, N = R*S*Kp,
-        // filter rows = the packed [R][S][Kp][Cp] image as is
-        const size_t esz = d->dtype == SEG_BF16 ? 2 : 4;
-        const int M = d->N * d->H * d->W, Nn = d->R * d->S * d->K;
-        const size_t zbytes = ((size_t)M * Nn * esz + 255) & ~(size_t)255;
-        if (!ws || ws_bytes < tconv_gemm_ws(d)) return SEG_EWORKSPACE;
-        NTParams g = {};
-        g.M = M; g.N = Nn; g.K = d->C;
-        g.x = x; g.x_img = (long)d->H * d->W * d->ldx; g.IH = d->H; g.IW = d->W; g.C = d->C; g.ldx = d->ldx;
-        g.Ha = d->H; g.Wa = d->W; g.ish = 1; g.isw = 1; g.ioh = 0; g.iow = 0; g.tsh = 1; g.tsw = 1; g.taps_w = 1;
-        g.w = w; g.w_col = d->C; g.w_tap = d->C; g.rstep = 1; g.sstep = 1; g.Sfull = 1;
-        g.y = ws; g.y_img = (long)d->H * d->W * Nn; g.OH = d->H; g.OW = d->W; g.ldy = Nn; g.osh = 1; g.osw = 1;
-        g.epi.n_valid = Nn; g.epi.keep_prob = 1.f;
+    if (const int kq = tconv_dense_kq(d)) {
+        const int M = d->N * d->H * d->W, Nn = d->R * d->S * kq;
+        const size_t zbytes = tconv_dense_zbytes(d);
+        if (!ws || ws_bytes < seg_conv_workspace(d, 3)) return SEG_EWORKSPACE;
+        NTParams g = dense_nt(M, Nn, d->C, x, d->ldx, w, ws, Nn);
+        g.x_img = (long)d->H * d->W * d->ldx; g.IH = d->H; g.IW = d->W; g.Ha = d->H; g.Wa = d->W;
+        g.y_img = (long)d->H * d->W * Nn; g.OH = d->H; g.OW = d->W;
         int st2 = seg::launch_nt(g, d->dtype, 1, g.M, (char*)ws + zbytes, ws_bytes - zbytes, (hipStream_t)stream);
         if (st2) return st2;
         const long total = (long)d->N * d->OH * d->OW;
@@ -476,14 +590,15 @@ extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void
         const float* bias = epi ? epi->bias : nullptr;
         const void* res = epi ? epi->residual : nullptr;
         const int ldr = epi ? epi->ld_residual : 0;
-        if (d->dtype == SEG_BF16)
-            hipLaunchKernelGGL(tconv_col2im_k<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)ws,
-                               (bf16*)y, d->N, d->H, d->W, d->OH, d->OW, d->K, d->k_valid, d->R, d->S, d->stride_h,
-                               d->pad_top, d->pad_left, d->ldy, bias, (const bf16*)res, ldr);
-        else
-            hipLaunchKernelGGL(tconv_col2im_k<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)ws,
-                               (float*)y, d->N, d->H, d->W, d->OH, d->OW, d->K, d->k_valid, d->R, d->S, d->stride_h,
-                               d->pad_top, d->pad_left, d->ldy, bias, (const float*)res, ldr);
+#define COL2IM(T, KQ) hipLaunchKernelGGL((tconv_col2im_k<T, KQ>), dim3(grid), dim3(256), 0, (hipStream_t)stream, \
+                                         (const T*)ws, (T*)y, d->N, d->H, d->W, d->OH, d->OW, d->k_valid, d->R, d->S, \
+                                         d->stride_h, d->pad_top, d->pad_left, d->ldy, bias, (const T*)res, ldr)
+        if (d->dtype == SEG_BF16) {
+            if (kq == 2) COL2IM(bf16, 2); else if (kq == 4) COL2IM(bf16, 4); else COL2IM(bf16, 8);
+        } else {
+            if (kq == 2) COL2IM(float, 2); else if (kq == 4) COL2IM(float, 4); else COL2IM(float, 8);
+        }
+#undef COL2IM
         SEG_CHECK_LAUNCH();
         return SEG_OK;
     }
@@ -498,6 +613,22 @@ extern "C" int seg_tconv2d_bwd_data(const seg_conv_desc* d, const void* dy, cons
     int st = check_desc(d);
     if (st) return st;
     if (!dy || !w || !dx) return SEG_EINVAL;
+    if (const int kq = tconv_dense_kq(d)) {
+        const int M = d->N * d->H * d->W, Kd = d->R * d->S * kq;
+        const size_t zbytes = tconv_dense_zbytes(d);
+        if (!ws || ws_bytes < seg_conv_workspace(d, 4)) return SEG_EWORKSPACE;
+        st = launch_gather_dy(d, dy, ws, (hipStream_t)stream);
+        if (st) return st;
+        NTParams g = dense_nt(M, d->C, Kd, ws, Kd, w, dx, d->ldx);
+        g.x_img = (long)d->H * d->W * Kd; g.IH = d->H; g.IW = d->W; g.Ha = d->H; g.Wa = d->W;
+        g.y_img = (long)d->H * d->W * d->ldx; g.OH = d->H; g.OW = d->W;
+        if (epi) {
+            const int ldr = epi->ld_residual ? epi->ld_residual : d->ldx;
+            g.epi = make_epi(epi, d->C, (long)d->H * d->W * ldr, (long)d->H * d->W, d->ldx);
+            if (epi->residual && epi->ld_residual == 0) g.epi.ld_res = d->ldx;
+        }
+        return seg::launch_nt(g, d->dtype, 1, g.M, (char*)ws + zbytes, ws_bytes - zbytes, (hipStream_t)stream);
+    }
     NTParams p = tconv_bwd_data_params(d);
     p.x = dy; p.w = w; p.y = dx;
     if (epi) {
@@ -513,6 +644,23 @@ extern "C" int seg_tconv2d_bwd_filter(const seg_conv_desc* d, const void* x, con
     int st = check_desc(d);
     if (st) return st;
     if (!x || !dy || !dw) return SEG_EINVAL;
+    if (const int kq = tconv_dense_kq(d)) {
+        const int P = d->N * d->H * d->W, Md = d->R * d->S * kq;
+        const size_t zbytes = tconv_dense_zbytes(d);
+        if (!ws || ws_bytes < seg_conv_workspace(d, 5)) return SEG_EWORKSPACE;
+        st = launch_gather_dy(d, dy, ws, (hipStream_t)stream);
+        if (st) return st;
+        TNParams g = {};
+        g.M = Md; g.N = d->C; g.P = P;
+        g.x = ws; g.x_img = (long)d->H * d->W * Md; g.IH = d->H; g.IW = d->W; g.Cg = Md; g.ldx = Md;
+        g.Ha = d->H; g.Wa = d->W; g.ish = 1; g.isw = 1; g.ioh = 0; g.iow = 0; g.tsh = 1; g.tsw = 1; g.taps_w = 1;
+        g.b = x; g.ldb = d->ldx;
+        g.out = dw; g.o_tap = 0; g.o_c = d->c_valid; g.o_n = 1;   // [(r,s,k)][c] = TF [kh][kw][Cout][Cin]
+        g.c_valid = Md; g.n_valid = d->c_valid;
+        st = seg::launch_tn(g, d->dtype, (char*)ws + zbytes, ws_bytes - zbytes, (hipStream_t)stream);
+        if (st || !dbias) return st;
+        return bias_grad_fallback(d, dy, dbias, (char*)ws + zbytes, ws_bytes - zbytes, stream);
+    }
     TNParams p = tconv_bwd_filter_params(d);
     p.x = dy; p.b = x; p.out = dw;          // dy is the gathered operand here: bias via the fallback
     st = seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
@@ -584,7 +732,9 @@ extern "C" int seg_pack_filter(const float* src, void* dst, int R, int S, int a_
     const int bmajor = (mode == 0 || mode == 3);
     hipStream_t st = (hipStream_t)stream;
     const int RS = R * S;
-    if ((a_pad & 7) || (b_pad & 7)) return SEG_EALIGN;
+    // a_pad may be the true channel count of a tap-dense tconv copy (modes 2, 3:
+    // seg_tconv_filter_apad); everything else is padded to 8
+    if ((b_pad & 7) || ((a_pad & 7) && (mode < 2 || (a_pad & 1)))) return SEG_EALIGN;
     if (bmajor) {
         dim3 grid(((a_pad + 63) / 64) * ((b_pad + 63) / 64), RS);
         if (dtype == SEG_BF16)

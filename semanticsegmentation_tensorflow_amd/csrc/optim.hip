@@ -4,8 +4,10 @@
 // every variable; the conv kernels then need the new weights in their packed
 // layouts ([K][R][S][C] forward, HWIO dgrad, tconv variants).  Running Adam and
 // then a pack pass re-reads all fp32 weights once per layout.  Here one launch
-// walks a device-resident segment table: each block owns a 64 x 64 [a][b] tile
-// of one variable viewed as [rs][a][b], applies Adam to params / m / v, and
+// walks a device-resident segment table: each block owns a TA x TB [a][b] tile
+// of one variable viewed as [rs][a][b] (TB = 128 fp32 = 512-byte runs per
+// array row, so HBM rows are streamed, not hopped), applies Adam to params /
+// m / v, and
 // writes the packed copies of the updated values:
 //   rows copy       dst[(rs * ap + a) * bp + b]      (HWIO, tconv-forward)
 //   transposed copy dst[(b * RS + rs) * ap + a]      (KRSC, tconv-input-grad)
@@ -16,7 +18,7 @@
 
 namespace {
 
-constexpr int TILE = 64;
+constexpr int TA = 32, TB = 128;   // tile [a][b]; 256 threads = 32 lanes x float4 per b-row
 
 __device__ __forceinline__ uint2 pack4_bf16(const float* v) {
     bf16 h[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
@@ -38,21 +40,21 @@ __global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const 
                                                     float* __restrict__ Mm, float* __restrict__ Vv,
                                                     const seg_adam_segment* __restrict__ segs, int nsegs,
                                                     float lr_t, float b1, float b2, float eps, float gs) {
-    __shared__ float lds[TILE][TILE + 1];
+    __shared__ float lds[TB][TA + 1];
     const int si = find_segment(segs, nsegs, blockIdx.x);
     const seg_adam_segment sg = segs[si];
-    const int ta = (sg.a + TILE - 1) / TILE, tb = (sg.b + TILE - 1) / TILE;
+    const int ta = (sg.a + TA - 1) / TA, tb = (sg.b + TB - 1) / TB;
     int t = blockIdx.x - sg.tile_begin;
     const int rs = t / (ta * tb);
     t -= rs * ta * tb;
-    const int a0 = (t / tb) * TILE, b0 = (t - (t / tb) * tb) * TILE;
+    const int a0 = (t / tb) * TA, b0 = (t - (t / tb) * tb) * TB;
     const int tid = threadIdx.x;
-    const int bl = (tid & 15) * 4;
+    const int bl = (tid & 31) * 4;
     const bool vec = ((sg.b & 3) == 0) && ((sg.offset & 3) == 0);
     T* rows = reinterpret_cast<T*>(sg.rows_dst);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int al = (tid >> 4) + 16 * i;
+    for (int i = 0; i < TA / 8; ++i) {
+        const int al = (tid >> 5) + 8 * i;
         const int a = a0 + al, b = b0 + bl;
         float pv[4] = {0.f, 0.f, 0.f, 0.f};
         if (a < sg.a && b < sg.b) {
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const 
     // transposed copy: thread -> (b row, 16 consecutive a)
     T* tr = reinterpret_cast<T*>(sg.tr_dst);
     const int RS = sg.rs;
-    const int blr = tid >> 2, ab = (tid & 3) * 16;
+    const int blr = tid >> 1, ab = (tid & 1) * 16;
     const int b = b0 + blr;
     if (b >= sg.b) return;
     T* d = tr + ((long)b * RS + rs) * sg.tr_ap + a0 + ab;
@@ -147,7 +149,7 @@ extern "C" int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs) {
         if (s.rows_dst && (s.rows_ap < s.a || s.rows_bp < s.b)) return -SEG_EINVAL;
         if (s.tr_dst && s.tr_ap < s.a) return -SEG_EINVAL;
         s.tile_begin = (int)total;
-        total += (long)s.rs * ((s.a + TILE - 1) / TILE) * ((s.b + TILE - 1) / TILE);
+        total += (long)s.rs * ((s.a + TA - 1) / TA) * ((s.b + TB - 1) / TB);
         if (total > 0x7fffffff) return -SEG_EINVAL;
     }
     return (int)total;

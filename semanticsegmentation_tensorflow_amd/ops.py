@@ -104,6 +104,10 @@ def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_
     e.relu_mask = None if relu_mask is None else relu_mask.data_ptr()
     e.ld_relu_mask = 0 if relu_mask is None else pixel_stride(relu_mask)
     e.mask_scale = float(mask_scale)
+    # the struct holds raw device pointers: keep the tensors alive with it, or a
+    # temporary (epilogue(bias=b.to(dev))) is freed and its memory reused by the
+    # next allocation before the kernel reads it
+    e._keep = (bias, scale, shift, residual, relu_mask)
     return e
 
 
@@ -208,8 +212,18 @@ def pack_filter(src, dst, a_pad, b_pad, mode, stream=None):
     return dst
 
 
-def packed_shape(R, S, A, B, mode):
-    a, b = round8(A), round8(B)
+def tconv_filter_apad(desc):
+    """Output-channel extent of the packed tconv filters (modes 2, 3) for this
+    descriptor: 8-padded in general, the true channel count on the tap-dense
+    path (seg_tconv_filter_apad)."""
+    r = int(_lib.lib().seg_tconv_filter_apad(ctypes.byref(desc)))
+    if r <= 0:
+        raise ValueError("tconv_filter_apad: invalid descriptor")
+    return r
+
+
+def packed_shape(R, S, A, B, mode, a_pad=None):
+    a, b = (a_pad if a_pad is not None else round8(A)), round8(B)
     if mode in (PACK_KRSC, PACK_TCONV_BWD):
         return (b, R, S, a)
     return (R, S, a, b)

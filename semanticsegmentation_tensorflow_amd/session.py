@@ -103,7 +103,7 @@ class _AdamOverlap:
 
 class Session:
     def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None,
-                 overlap_optimizer=True):
+                 overlap_optimizer=False):
         self.graph = graph or G.get_default_graph()
         if not torch.cuda.is_available():
             raise RuntimeError("Session needs an MI355X (HIP device); there is no CPU fallback")
@@ -376,6 +376,7 @@ class Session:
         store = self.store
         ws_need = 0
         p.packs = set()
+        p.pack_apad = {}
         for n in p.nodes:
             y = n.output
             if n.kind == "input":
@@ -437,9 +438,12 @@ class Session:
                 _, OH, OW, _ = s
                 n.desc = ops.tconv_desc(N, H, W, C, OH, OW, Co, R, S, n.stride, n.padding, self.cdt)
                 ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_TFWD))
+                ap = ops.tconv_filter_apad(n.desc)
                 p.packs.add((n.w.var_name, ops.PACK_TCONV_FWD))
+                p.pack_apad[(n.w.var_name, ops.PACK_TCONV_FWD)] = ap
                 if id(x) in p.needs_grad:
                     p.packs.add((n.w.var_name, ops.PACK_TCONV_BWD))
+                    p.pack_apad[(n.w.var_name, ops.PACK_TCONV_BWD)] = ap
                 if p.train:
                     ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_TBWD_DATA),
                                   ops.conv_workspace(n.desc, ops.OP_TBWD_FILTER),
@@ -450,10 +454,13 @@ class Session:
         self.ws.get(ws_need)
         # packed filter copies
         for name, mode in sorted(p.packs):
-            if (name, mode) not in store.packed:
+            ap = p.pack_apad.get((name, mode))
+            old = store.packed.get((name, mode))
+            if old is None or (ap is not None and old[1] != ap):
                 R, S, A, B = store.by_name[name].shape
-                t = torch.zeros(ops.packed_shape(R, S, A, B, mode), dtype=self.tdt, device=dev)
-                store.packed[(name, mode)] = (t, round8(A), round8(B))
+                ap = ap if ap is not None else round8(A)
+                t = torch.zeros(ops.packed_shape(R, S, A, B, mode, ap), dtype=self.tdt, device=dev)
+                store.packed[(name, mode)] = (t, ap, round8(B))
                 self._packed_version = -1          # new copies must be filled
         # gradient buffers / plan for backward
         if p.train:

@@ -77,11 +77,12 @@ def _conv_case(case, seed):
     return x, w, b
 
 
-def _pack(w64, mode, dtype, dev):
+def _pack(w64, mode, dtype, dev, a_pad=None):
     R, S, A, B = w64.shape
     src = w64.float().to(dev).contiguous()
-    dst = torch.empty(ops.packed_shape(R, S, A, B, mode), dtype=dtype, device=dev)
-    return ops.pack_filter(src, dst, ops.round8(A), ops.round8(B), mode)
+    ap = a_pad if a_pad is not None else ops.round8(A)
+    dst = torch.empty(ops.packed_shape(R, S, A, B, mode, ap), dtype=dtype, device=dev)
+    return ops.pack_filter(src, dst, ap, ops.round8(B), mode)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -177,7 +178,9 @@ TCONV_CASES = [
     (2, 3, 5, 16, 6, 10, 8, 4, 2),       # conv_t1/t2-like k4 s2
     (1, 3, 4, 2, 6, 8, 512, 4, 2),       # conv_t1 exact channel shape (2 -> 512)
     (1, 6, 6, 16, 11, 12, 16, 4, 2),     # odd output: asymmetric tconv pads
-    (1, 2, 3, 16, 16, 24, 2, 16, 8),     # conv_t3-like k16 s8 -> 2 classes
+    (1, 2, 3, 16, 16, 24, 2, 16, 8),     # conv_t3-like k16 s8 -> 2 classes (tap-dense path)
+    (2, 3, 2, 24, 24, 16, 4, 16, 8),     # tap-dense with 4 output channels
+    (1, 4, 5, 16, 16, 20, 2, 8, 4),      # tap-dense k8 s4
     (2, 4, 4, 136, 8, 8, 72, 4, 2),      # tails in both channel dims
 ]
 
@@ -200,7 +203,7 @@ def test_tconv2d_fwd_bias_residual(dev, ntv, case, dtype):
     res = rnd(torch.randn(N, OH, OW, Co, generator=g, dtype=torch.float64), dtype)
     ref = tf.conv2d_transpose(rnd(x, dtype), rnd(w, dtype), (N, OH, OW, Co), s) + b.float().double() + res
     d = ops.tconv_desc(N, IH, IW, Ci, OH, OW, Co, k, k, s, "SAME", DT[dtype])
-    wp = _pack(w, ops.PACK_TCONV_FWD, dtype, dev)
+    wp = _pack(w, ops.PACK_TCONV_FWD, dtype, dev, ops.tconv_filter_apad(d))
     y = torch.full((N, OH, OW, d.K), float("nan"), dtype=dtype, device=dev)
     resd = to_dev(res, dtype, dev)
     ops.tconv2d_fwd(d, to_dev(x, dtype, dev), wp, y, ops.epilogue(bias=b.float().to(dev), residual=resd))
@@ -221,7 +224,7 @@ def test_tconv2d_grads(dev, ntv, tnv, case, dtype):
     (y * dy).sum().backward()
     d = ops.tconv_desc(N, IH, IW, Ci, OH, OW, Co, k, k, s, "SAME", DT[dtype])
     dyd = to_dev(dy, dtype, dev)
-    wb = _pack(w, ops.PACK_TCONV_BWD, dtype, dev)
+    wb = _pack(w, ops.PACK_TCONV_BWD, dtype, dev, ops.tconv_filter_apad(d))
     dx = torch.full((N, IH, IW, d.C), float("nan"), dtype=dtype, device=dev)
     ops.tconv2d_bwd_data(d, dyd, wb, dx)
     dw = torch.full((k, k, Co, Ci), float("nan"), dtype=torch.float32, device=dev)

@@ -22,7 +22,7 @@ class _Rec:
         real_fn = getattr(self.real, name)
         host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
-                             "seg_adam_segments_plan")
+                             "seg_adam_segments_plan", "seg_tconv_filter_apad")
 
         def fn(*a):
             if host_only:
