@@ -88,15 +88,15 @@ def test_fcn_train_plan(dry):
 
 
 def test_adam_segment_plan_host():
-    """seg_adam_segments_plan: tile prefix over 64x64 [a][b] tiles per rs slice."""
+    """seg_adam_segments_plan: tile prefix over 32x128 [a][b] tiles per rs slice."""
     lib = _lib.load()
     arr = (ops.AdamSegment * 3)()
     for e, (rs, a, b) in zip(arr, [(9, 3, 64), (1, 1, 130), (49, 512, 4096)]):
         e.rs, e.a, e.b = rs, a, b
     import ctypes
     total = lib.seg_adam_segments_plan(ctypes.byref(arr), 3)
-    assert [e.tile_begin for e in arr] == [0, 9, 9 + 3]
-    assert total == 9 + 3 + 49 * 8 * 64
+    assert [e.tile_begin for e in arr] == [0, 9, 9 + 2]
+    assert total == 9 + 2 + 49 * 16 * 32
     assert ctypes.sizeof(ops.AdamSegment) == 56
     bad = (ops.AdamSegment * 1)()
     assert lib.seg_adam_segments_plan(ctypes.byref(bad), 1) < 0      # rs = 0
