@@ -128,6 +128,8 @@ def kernel_symbol(name):
     bm, bn = a[1], a[2]
     if fam == "conv_halo":
         return r"conv_halo2<" if bn == "256" else r"conv_halo<"
+    if fam == "igemm_nt3":
+        return r"igemm_nt3<"
     if fam == "igemm_nt2":
         return rf"igemm_nt2I\w*Li{bm}ELi{bn}E"
     if fam == "igemm_tn2":

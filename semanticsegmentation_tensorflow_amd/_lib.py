@@ -18,7 +18,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",

@@ -391,19 +391,13 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 0:
         case 1: {
             NTParams p = op == 0 ? conv_fwd_params(d) : conv_bwd_data_params(d);
-            seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp);
             p.epi.keep_prob = 1.f;
+            macs = macs_conv;
             if (op == 0 && d->dil_w == d->dil_h && seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) {
-                fam = "conv_c8"; bm = 512; bn = d->K; sp = 1; macs = macs_conv;
+                fam = "conv_c8"; bm = 512; bn = d->K; sp = 1;
                 break;
             }
-            seg::HaloPlan hp;
-            if (seg::g_nt_variant == 2 && seg::res64_ok(p, d->dtype)) {
-                fam = "conv_res64"; bn = 64; sp = 1;
-            } else if (seg::g_nt_variant == 2 && seg::halo_plan(p, d->dtype, sp, seg::device_cus(), &hp)) {
-                fam = "conv_halo"; bn = hp.bn; sp = hp.splits;
-            }
-            macs = macs_conv;
+            fam = seg::nt_choice(p, d->dtype, 1, p.M, &bm, &bn, &sp);
             break;
         }
         case 2: {
@@ -415,39 +409,47 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
                 fam = "wgrad_c8"; bm = 72; bn = p.N; sp = seg::smallc_wgrad_splits(p, seg::device_cus());
             } else if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
+            } else if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && p.M >= 128) {
+                fam = "igemm_tn2";
             }
             macs = macs_conv;
             break;
         }
         case 3: {
-            if (tconv_dense_kq(d)) {
-                seg::nt_info(d->N * d->H * d->W, d->R * d->S * tconv_dense_kq(d), d->C, d->dtype, 0, &bm, &bn, &sp);
+            macs = macs_t;
+            if (const int kq = tconv_dense_kq(d)) {
+                const int M = d->N * d->H * d->W, Nn = d->R * d->S * kq;
+                NTParams g = dense_nt(M, Nn, d->C, nullptr, d->ldx, nullptr, nullptr, Nn);
+                g.IH = d->H; g.IW = d->W; g.Ha = d->H; g.Wa = d->W; g.OH = d->H; g.OW = d->W;
+                fam = seg::nt_choice(g, d->dtype, 1, g.M, &bm, &bn, &sp);
             } else {
                 NTParams p = tconv_fwd_params(d);
-                seg::nt_info(p.M, p.N, p.K, d->dtype, 1, &bm, &bn, &sp);
+                fam = seg::nt_choice(p, d->dtype, d->stride_h * d->stride_w, p.M, &bm, &bn, &sp);
             }
-            macs = macs_t;
             break;
         }
         case 4: {
-            if (tconv_dense_kq(d)) seg::nt_info(d->N * d->H * d->W, d->C, d->R * d->S * tconv_dense_kq(d), d->dtype, 0, &bm, &bn, &sp);
-            else { NTParams p = tconv_bwd_data_params(d); seg::nt_info(p.M, p.N, p.K, d->dtype, 0, &bm, &bn, &sp); }
             macs = macs_t;
+            if (const int kq = tconv_dense_kq(d)) {
+                const int M = d->N * d->H * d->W, Kd = d->R * d->S * kq;
+                NTParams g = dense_nt(M, d->C, Kd, nullptr, Kd, nullptr, nullptr, d->ldx);
+                g.IH = d->H; g.IW = d->W; g.Ha = d->H; g.Wa = d->W; g.OH = d->H; g.OW = d->W;
+                fam = seg::nt_choice(g, d->dtype, 1, g.M, &bm, &bn, &sp);
+            } else {
+                NTParams p = tconv_bwd_data_params(d);
+                fam = seg::nt_choice(p, d->dtype, 1, p.M, &bm, &bn, &sp);
+            }
             break;
         }
         case 5: {
-            if (tconv_dense_kq(d)) seg::tn_info(d->R * d->S * tconv_dense_kq(d), d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
-            else { TNParams p = tconv_bwd_filter_params(d); seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp); }
-            fam = "igemm_tn";
+            const int Mt = tconv_dense_kq(d) ? d->R * d->S * tconv_dense_kq(d) : d->R * d->S * d->K;
+            seg::tn_info(Mt, d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
+            fam = (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
             macs = macs_t;
             break;
         }
         default: return SEG_EINVAL;
     }
-    if (bm == 256 && fam[0] == 'i' && fam[6] == 'n') fam = "igemm_nt2";
-    if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && fam[0] == 'i' && fam[6] == 't' &&
-        (op == 2 ? d->R * d->S * d->C : d->R * d->S * (tconv_dense_kq(d) ? tconv_dense_kq(d) : d->K)) >= 128)
-        fam = "igemm_tn2";
     if (name && len > 0) snprintf(name, len, "%s<%s,%d,%d>", fam, ty, bm, bn);
     if (splits) *splits = sp;
     if (flops) *flops = 2.0 * macs;
@@ -464,6 +466,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt_halo")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "nt3")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_nt3 = value;
         return SEG_OK;
     }
     if (!strcmp(name, "halo2_n128")) {

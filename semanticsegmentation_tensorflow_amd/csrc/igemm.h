@@ -77,12 +77,20 @@ int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
 size_t tn_workspace(int M, int N, int P, int dtype);
 void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits);
+const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits);
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
 extern int g_nt_variant;
 extern int g_tn_variant;
 extern int g_nt2_ablate;
 void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s);
+
+// 256 x 256 NT tiles (igemm3.hip) for bf16 with N > 128
+extern int g_nt3;
+bool nt3_ok(const NTParams& p, int dtype);
+inline bool nt3_applies(int N, int dtype) { return g_nt3 && dtype == SEG_BF16 && N > 128; }
+void nt3_info(int M, int N, int K, int cus, int* splits);
+void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s);
 
 // halo-tiled direct conv (halo.hip) for stride-1 NT problems
 struct HaloPlan {

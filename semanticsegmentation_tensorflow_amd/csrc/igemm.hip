@@ -648,6 +648,11 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     if (phase) return 0;
     int bm, bn, splits;
     choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, bm, bn, splits);
+    if (g_nt_variant == 2 && nt3_applies(N, dtype)) {
+        int s3;
+        nt3_info(M, N, K, num_cus(), &s3);
+        splits = std::max(splits, s3);
+    }
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
@@ -686,6 +691,11 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         }
         return SEG_OK;
     }
+    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_ok(p, SEG_BF16);
+    if (nt3) {
+        nt3_info(max_m, p.N, p.K, num_cus(), &splits);
+        if (nphases > 1) splits = 1;
+    }
     int gridz = nphases;
     if (splits > 1) {
         const int kt = (p.K + BK - 1) / BK;
@@ -696,7 +706,8 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
+    if (nt3) launch_nt3(p, gridz, max_m, s);
+    else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
     SEG_CHECK_LAUNCH();
@@ -707,6 +718,29 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = nullptr;
     }
     return SEG_OK;
+}
+
+// The kernel launch_nt would pick for p (host-only mirror of launch_nt_typed).
+const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits) {
+    const int bk = dtype == SEG_BF16 ? 64 : 32;
+    choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
+    if (nphases > 1) *splits = 1;
+    if (dtype == SEG_BF16 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
+        *bn = 64; *splits = 1;
+        return "conv_res64";
+    }
+    HaloPlan hp;
+    if (dtype == SEG_BF16 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, *splits, num_cus(), &hp)) {
+        *bm = 256; *bn = hp.bn; *splits = hp.splits;
+        return "conv_halo";
+    }
+    if (dtype == SEG_BF16 && g_nt_variant == 2 && nt3_ok(p, SEG_BF16)) {
+        nt3_info(max_m, p.N, p.K, num_cus(), splits);
+        if (nphases > 1) *splits = 1;
+        *bm = *bn = 256;
+        return "igemm_nt3";
+    }
+    return *bm == 256 ? "igemm_nt2" : "igemm_nt";
 }
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {

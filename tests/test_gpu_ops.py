@@ -17,18 +17,21 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7],
-                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8],
+                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3"])
 def ntv(request, dev):
     """Run NT tests on every kernel generation: 1 = register-staged GEMM,
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
     (bf16, stride 1, C % 64 == 0; 256x256 four-phase tiles for N > 128),
     4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
     stagger (two-phase schedule), 6 = 3 with four phases per iteration,
-    7 = 3 with the two-phase kernel also for N <= 128 (off by default)."""
+    7 = 3 with the two-phase kernel also for N <= 128 (off by default),
+    8 = 2 with the 256x256-tile GEMM (igemm_nt3) for N > 128 (on by default;
+    variant 2 keeps it off so igemm_nt2 stays covered for wide N)."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
-    ops.set_option("nt_halo", 1 if v >= 3 else 0)
+    ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
+    ops.set_option("nt3", 0 if v == 2 else 1)
     ops.set_option("halo_wide", 0 if v == 4 else 1)
     ops.set_option("halo_stagger", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
@@ -36,6 +39,7 @@ def ntv(request, dev):
     yield v
     ops.set_option("igemm_nt_variant", 2)
     ops.set_option("nt_halo", 1)
+    ops.set_option("nt3", 1)
     ops.set_option("halo_wide", 1)
     ops.set_option("halo_stagger", 1)
     ops.set_option("halo_phases", 2)
@@ -65,6 +69,10 @@ CONV_CASES = [
     (2, 33, 45, 64, 328, 3, 3, 1, 1, "SAME"),   # 256-wide halo tiles: 2 N tiles + tail
     (2, 19, 131, 3, 48, 3, 3, 1, 1, "SAME"),    # first-layer kernel (C=3->8): ragged 8x64 tiles, K=48
     (1, 17, 70, 64, 48, 3, 3, 1, 1, "VALID"),   # resident-filter kernel: VALID, N=48 < 64
+    # 256x256-tile GEMM (N > 128): K tiles straddling taps, N tail, split-K
+    (1, 5, 7, 40, 264, 7, 7, 1, 1, "SAME"),     # conv6-like, C=40: a 64-deep K tile spans taps
+    (2, 6, 9, 512, 512, 1, 1, 1, 1, "SAME"),    # conv7-like 1x1
+    (1, 4, 6, 64, 384, 7, 7, 1, 1, "SAME"),     # M = 24, K = 3136: split-K slabs
 ]
 
 
