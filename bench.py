@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-fuse-adam", action="store_true",
+                    help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
     ap.add_argument("--overlap-optimizer", action="store_true",
                     help="per-layer Adam on a side stream as gradients become final (measured slower: the "
                          "HBM-bound update steals CUs from the MFMA-bound backward)")
@@ -128,8 +130,8 @@ def kernel_symbol(name):
     bm, bn = a[1], a[2]
     if fam == "conv_halo":
         return r"conv_halo2<" if bn == "256" else r"conv_halo<"
-    if fam == "igemm_nt3":
-        return r"igemm_nt3<"
+    if fam in ("igemm_nt3", "igemm_tn3"):
+        return fam + "<"
     if fam == "igemm_nt2":
         return rf"igemm_nt2I\w*Li{bm}ELi{bn}E"
     if fam == "igemm_tn2":
@@ -234,7 +236,8 @@ def main():
                                                                    valid_hw=(H, W)))
     train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
     sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp,
-                      overlap_optimizer=args.overlap_optimizer)
+                      overlap_optimizer=args.overlap_optimizer,
+                      fuse_adam=not args.no_fuse_adam)
     sess.run(tf.global_variables_initializer())
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
     feed = {image: img, labels: lab, keep: kp}

@@ -279,6 +279,34 @@ int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_ad
                       int nsegs, int total_tiles, float lr, float beta1, float beta2, float eps, int t,
                       float grad_scale, int dtype, void* stream);
 
+/* Conv2DBackpropFilter fused with TF1 Adam (AdamOptimizer.minimize,
+ * Network/model/FCN.py:338-340) on that filter, for single-process training
+ * where nothing (no all-reduce) sits between the gradient and the update:
+ * the filter-gradient epilogue reads p/m/v, applies the update of
+ * seg_adam_tf1_pack element-for-element and rewrites the packed bf16 copies,
+ * so the fp32 gradient never round-trips through HBM.  p/m/v are the flat
+ * fp32 [R][S][c_valid][k_valid] slices of the variable; rows_dst = the HWIO
+ * copy (mode 1, [RS][rows_ap][rows_bp]) and tr_dst = the KRSC copy (mode 0,
+ * [K][RS][tr_ap]), either may be NULL.  dw_f32 may be NULL; if given, the
+ * gradient is stored too.  dbias as seg_conv2d_bwd_filter (not fused into
+ * Adam).  Returns SEG_EINVAL when seg_conv_wgrad_adam_fusable(d) is 0. */
+typedef struct seg_adam_fused {
+    float* p;
+    float* m;
+    float* v;
+    void* rows_dst;
+    int rows_ap, rows_bp;
+    void* tr_dst;
+    int tr_ap;
+    float lr, beta1, beta2, eps;
+    int t;
+    float grad_scale;
+} seg_adam_fused;
+int seg_conv_wgrad_adam_fusable(const seg_conv_desc* d);
+int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void* dy, float* dw_f32,
+                               float* dbias, const seg_adam_fused* adam, void* ws, size_t ws_bytes,
+                               void* stream);
+
 /* ---- misc ---------------------------------------------------------------- */
 int seg_fill(void* y, long n, float value, int dtype, void* stream);
 int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);

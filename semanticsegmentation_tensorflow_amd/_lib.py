@@ -81,6 +81,14 @@ class SegEpilogue(ctypes.Structure):
                 ("ld_relu_mask", ctypes.c_int), ("mask_scale", ctypes.c_float)]
 
 
+class SegAdamFused(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("rows_dst", ctypes.c_void_p), ("rows_ap", ctypes.c_int), ("rows_bp", ctypes.c_int),
+                ("tr_dst", ctypes.c_void_p), ("tr_ap", ctypes.c_int), ("lr", ctypes.c_float),
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("t", ctypes.c_int), ("grad_scale", ctypes.c_float)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
@@ -101,6 +109,8 @@ SIGNATURES = {
     "seg_tconv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_conv_workspace": (_Z, [_DP, _I]),
     "seg_tconv_filter_apad": (_I, [_DP]),
+    "seg_conv_wgrad_adam_fusable": (_I, [_DP]),
+    "seg_conv2d_bwd_filter_adam": (_I, [_DP, _P, _P, _P, _P, ctypes.POINTER(SegAdamFused), _P, _Z, _P]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
                                   ctypes.POINTER(ctypes.c_double)]),
@@ -160,6 +170,11 @@ def lib():
         with _LOCK:
             if _LIB is None:
                 _LIB = load()
+                # kernel-selection overrides for experiments: SEG_OPTIONS="nt3=0,tn3_mfast=1"
+                for kv in filter(None, os.environ.get("SEG_OPTIONS", "").split(",")):
+                    k, v = kv.split("=")
+                    if _LIB.seg_set_option(k.strip().encode(), int(v)) != 0:
+                        raise SegKernelError(f"SEG_OPTIONS: bad option {kv!r}")
     return _LIB
 
 

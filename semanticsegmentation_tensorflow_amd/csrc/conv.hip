@@ -5,6 +5,7 @@
 #include "igemm.h"
 #include <stdio.h>
 #include <string.h>
+#include <math.h>
 
 using seg::NTParams;
 using seg::TNParams;
@@ -409,6 +410,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
                 fam = "wgrad_c8"; bm = 72; bn = p.N; sp = seg::smallc_wgrad_splits(p, seg::device_cus());
             } else if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
+            } else if (seg::g_tn_variant == 2 && seg::tn3_ok(p, d->dtype)) {
+                fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(p.M, p.N, p.P, seg::device_cus(), &sp);
             } else if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && p.M >= 128) {
                 fam = "igemm_tn2";
             }
@@ -445,6 +448,9 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             const int Mt = tconv_dense_kq(d) ? d->R * d->S * tconv_dense_kq(d) : d->R * d->S * d->K;
             seg::tn_info(Mt, d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
             fam = (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
+            if (seg::g_tn_variant == 2 && seg::tn3_applies(Mt, d->C, d->dtype)) {
+                fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(Mt, d->C, d->N * d->H * d->W, seg::device_cus(), &sp);
+            }
             macs = macs_t;
             break;
         }
@@ -466,6 +472,21 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt_halo")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_halo = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn3_abl")) {   // diagnostic builds only: results are garbage
+        if (value < 0 || value > 3) return SEG_EINVAL;
+        seg::g_tn3_abl = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn3_mfast")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_tn3_mfast = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn3")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_tn3 = value;
         return SEG_OK;
     }
     if (!strcmp(name, "nt3")) {
@@ -574,6 +595,45 @@ extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, cons
     p.x = x; p.b = dy; p.out = dw; p.dbias = dbias;
     st = seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
     if (st || !p.dbias) return st;
+    return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
+}
+
+static bool wgrad_adam_params(const seg_conv_desc* d, TNParams* out) {
+    if (check_desc(d) || d->dtype != SEG_BF16 || seg::g_tn_variant != 2) return false;
+    TNParams p = conv_bwd_filter_params(d);
+    if (seg::smallc_wgrad_ok(p, d->dtype)) return false;
+    seg::WgradPlan wp;
+    if (seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) return false;
+    if (!seg::tn3_adam_ok(p, d->dtype)) return false;
+    *out = p;
+    return true;
+}
+
+extern "C" int seg_conv_wgrad_adam_fusable(const seg_conv_desc* d) {
+    TNParams p;
+    return wgrad_adam_params(d, &p) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void* dy, float* dw,
+                                          float* dbias, const seg_adam_fused* a, void* ws, size_t ws_bytes,
+                                          void* stream) {
+    TNParams p;
+    if (!x || !dy || !a || !a->p || !a->m || !a->v || a->t < 1) return SEG_EINVAL;
+    if (!wgrad_adam_params(d, &p)) return SEG_EINVAL;
+    if ((((uintptr_t)a->p | (uintptr_t)a->m | (uintptr_t)a->v | (uintptr_t)dw) & 15)) return SEG_EALIGN;
+    p.x = x; p.b = dy; p.out = dw; p.dbias = nullptr;
+    const double lr_t = (double)a->lr * sqrt(1.0 - pow((double)a->beta2, a->t)) / (1.0 - pow((double)a->beta1, a->t));
+    p.adam.p = a->p; p.adam.m = a->m; p.adam.v = a->v;
+    p.adam.rows = a->rows_dst; p.adam.rows_ap = a->rows_ap; p.adam.rows_bp = a->rows_bp;
+    p.adam.tr = a->tr_dst; p.adam.tr_ap = a->tr_ap; p.adam.RS = d->R * d->S;
+    p.adam.lr_t = (float)lr_t; p.adam.b1 = a->beta1; p.adam.b2 = a->beta2; p.adam.eps = a->eps;
+    p.adam.gs = a->grad_scale;
+    p.adam.store_grad = dw != nullptr;
+    p.Mp = p.M;
+    p.partial = nullptr;
+    seg::launch_tn3(p, 1, (hipStream_t)stream);
+    SEG_CHECK_LAUNCH();
+    if (!dbias) return SEG_OK;
     return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
 }
 

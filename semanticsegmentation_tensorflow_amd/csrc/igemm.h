@@ -70,6 +70,16 @@ struct TNParams {
     // slabs then carry it as an extra row M, so slabs hold Mp = M + 1 rows.
     float* dbias;
     int Mp;
+    // TF1 Adam fused into the filter-gradient epilogue (igemm_tn3 only; p == null: off)
+    struct {
+        float *p, *m, *v;      // fp32 master slices indexed like out
+        void* rows;            // bf16 rows copy [(tap*rows_ap + c)*rows_bp + n] or null
+        int rows_ap, rows_bp;
+        void* tr;              // bf16 transposed copy [(n*RS + tap)*tr_ap + c] or null
+        int tr_ap, RS;
+        float lr_t, b1, b2, eps, gs;
+        int store_grad;        // also write the gradient to out
+    } adam;
 };
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
@@ -91,6 +101,14 @@ bool nt3_ok(const NTParams& p, int dtype);
 inline bool nt3_applies(int N, int dtype) { return g_nt3 && dtype == SEG_BF16 && N > 128; }
 void nt3_info(int M, int N, int K, int cus, int* splits);
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s);
+extern int g_tn3;
+extern int g_tn3_abl;
+extern int g_tn3_mfast;
+bool tn3_ok(const TNParams& p, int dtype);
+inline bool tn3_applies(int M, int N, int dtype) { return g_tn3 && dtype == SEG_BF16 && M >= 256 && N > 128; }
+void tn3_info(int M, int N, int P, int cus, int* splits);
+void launch_tn3(TNParams& p, int splits, hipStream_t s);
+bool tn3_adam_ok(const TNParams& p, int dtype);
 
 // halo-tiled direct conv (halo.hip) for stride-1 NT problems
 struct HaloPlan {

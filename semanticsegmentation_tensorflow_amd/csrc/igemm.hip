@@ -784,6 +784,11 @@ void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits) {
 size_t tn_workspace(int M, int N, int P, int dtype) {
     int bm, bn, splits;
     choose_tn(M, N, P, dtype == SEG_BF16 ? 64 : 32, bm, bn, splits);
+    if (g_tn_variant == 2 && tn3_applies(M, N, dtype)) {
+        int s3;
+        tn3_info(M, N, P, num_cus(), &s3);
+        splits = std::max(splits, s3);
+    }
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
@@ -836,6 +841,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     int bm, bn, splits;
     choose_tn(p.M, p.N, p.P, BKP, bm, bn, splits);
+    const bool tn3 = sizeof(T) == 2 && g_tn_variant == 2 && tn3_ok(p, SEG_BF16);
+    if (tn3) tn3_info(p.M, p.N, p.P, num_cus(), &splits);
     int gridz = 1;
     if (splits > 1) {
         const int kt = (p.P + BKP - 1) / BKP;
@@ -846,7 +853,9 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
+    if (tn3) {
+        launch_tn3(p, gridz, s);
+    } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
         launch_tn2(p, bm, bn, gridz, s);
     } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
     else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);

@@ -343,4 +343,406 @@ void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s) {
     hipLaunchKernelGGL((igemm_nt3<true>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
 }
 
+
+// ---------------------------------------------------------------------------
+// TN v3: filter gradients C[m][n] = sum_p A[p][m] B[p][n] on 256 x 256 tiles.
+// LDS image per stage: 64 pixel rows x 512 B for A (gathered x columns) and
+// for B (dy columns); 16-byte chunks XOR-swizzled within 256-byte halves so
+// the column-wise ds_read_b64_tr_b16 fragment reads are conflict-free (as
+// igemm_tn2).  Same wave layout, rings and staggered two-phase schedule as
+// igemm_nt3.  Epilogue: fp32 tile staged in LDS, 32-byte row-contiguous
+// stores (filter gradient or split-K slab).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+
+int g_tn3 = 1;
+int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
+int g_tn3_mfast = 0;   // tile order: M fastest when the B (dy) panel is the larger operand
+
+// ABL: see g_tn3_abl.  MFAST: consecutive tiles walk M (share the dy panel).
+// ADAM: TF1 Adam on the parameters of the tile (p.adam) instead of (or besides)
+// storing the gradient -- the filter gradient never round-trips through HBM.
+template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false>
+__global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int tiles_n, int splits) {
+    using T = bf16;
+    constexpr int NW = 8, BM = 256, BN = 256, BKP = 64;
+    constexpr int ROWB = 512, RPI = 1024 / ROWB, CPR = ROWB / 16;   // 2 rows / DMA piece, 32 chunks / row
+    constexpr int A_INS = BKP / RPI / NW, B_INS = BKP / RPI / NW;   // 4 + 4
+    constexpr int WTM = 128, WTN = 64, TN = WTN / 16;
+    constexpr int ABUF = BKP * ROWB, BBUF = BKP * ROWB;             // 32 KiB each
+    __shared__ __attribute__((aligned(16))) char smem[3 * ABUF + 2 * BBUF];
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+    const int ntile = tiles_m * tiles_n;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int split = wg / ntile;
+    const int tile = wg - split * ntile;
+    if (split >= splits) return;
+    int tm, tn;
+    if (MFAST) {
+        tn = tile / tiles_m;
+        tm = tile - tn * tiles_m;
+    } else {
+        tm = tile / tiles_n;
+        tn = tile - tm * tiles_n;
+    }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int KT = (p.P + BKP - 1) / BKP;
+    int kt_begin = 0, kt_end = KT;
+    if (p.partial) {
+        kt_begin = split * p.kt_per_split;
+        kt_end = min(KT, kt_begin + p.kt_per_split);
+    }
+    const int nk = max(0, kt_end - kt_begin);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 2, wn = w & 3;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Bm = reinterpret_cast<const T*>(p.b);
+    const void* zero = (const void*)g_nt3_zero;
+
+    // lane -> (row of the DMA piece, physical chunk) -> global chunk (swizzle is piece-independent)
+    const int rsub = lane / CPR, pc = lane % CPR;
+    const int row0 = w * RPI + rsub;
+    const int gc = (pc & ~15) | ((pc & 15) ^ tn3_swz(row0));
+    // A: column m = m0 + gc*8 .. +7 -> (tap, channel)
+    const int am = m0 + gc * 8;
+    const bool a_mok = am < p.M;
+    const int atap = a_mok ? am / p.Cg : 0;
+    const int ac = a_mok ? am - atap * p.Cg : 0;
+    const int atj = atap / p.taps_w, ati = atap - atj * p.taps_w;
+    const int hoff = atj * p.tsh + p.ioh, woff = ati * p.tsw + p.iow;
+    int pimg[A_INS], pa[A_INS], pb[A_INS], pp[A_INS];
+    const int hw = p.Ha * p.Wa;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+        const int pix = kt_begin * BKP + (i * NW) * RPI + row0;
+        pp[i] = pix;
+        const int q = pix < p.P ? pix : 0;
+        pimg[i] = q / hw;
+        const int rem = q - pimg[i] * hw;
+        pa[i] = rem / p.Wa;
+        pb[i] = rem - pa[i] * p.Wa;
+    }
+    // B: column n = n0 + gc*8
+    const int bn = n0 + gc * 8;
+    const bool b_nok = bn < p.N;
+    int bpix = kt_begin * BKP + row0;
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+    const unsigned ldsB = lds0 + 3 * ABUF;
+    auto issue_a = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i) {
+            const int ih = pa[i] * p.ish + hoff, iw = pb[i] * p.isw + woff;
+            const bool ok = a_mok && pp[i] < p.P && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+            const void* src = ok ? (const void*)(X + (long)pimg[i] * p.x_img + ((long)ih * p.IW + iw) * p.ldx + ac) : zero;
+            glds16(src, lds0 + buf * ABUF + (i * NW + w) * 1024);
+            pp[i] += BKP;
+            pb[i] += BKP;
+            while (pb[i] >= p.Wa) {
+                pb[i] -= p.Wa;
+                if (++pa[i] == p.Ha) { pa[i] = 0; ++pimg[i]; }
+            }
+        }
+    };
+    auto issue_b = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const int pix = bpix + (i * NW) * RPI;
+            const bool ok = b_nok && pix < p.P;
+            const void* src = ok ? (const void*)(Bm + (long)pix * p.ldb + bn) : zero;
+            glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
+        }
+        bpix += BKP;
+    };
+
+    f32x4 acc[8][TN];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) {
+        issue_a(0);
+        issue_b(0);
+        if (nk > 1) {
+            issue_a(1);
+            wait_vmcnt<A_INS>();
+        } else {
+            wait_vmcnt<0>();
+        }
+    }
+    lds_barrier();
+    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
+
+    const int fg = lane >> 4;
+    const int tq = (lane & 15) >> 2, tpp = lane & 3;
+    int abuf = 0, bbuf = 0;
+    for (int it = 0; it < nk; ++it) {
+        const char* As = smem + abuf * ABUF;
+        const char* Bs = smem + 3 * ABUF + bbuf * BBUF;
+        bf16x8 af[2][4], bq[2][TN];
+        // 16 columns x 32 pixel rows fragment at column `col0`, k rows ks*32 ..
+        auto frag = [&](const char* base, int col0, int ks) {
+            const int r1 = ks * 32 + 8 * fg + tq;
+            const int chk = (col0 >> 3) + (tpp >> 1);
+            const int c1 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1));
+            const int c2 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1 + 4));
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + r1 * ROWB + 16 * c1 + 8 * (tpp & 1)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + (r1 + 4) * ROWB + 16 * c2 + 8 * (tpp & 1)));
+            s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            return __builtin_bit_cast(bf16x8, v);
+        };
+        auto read_a = [&](int mh) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) af[ks][mi] = frag(As, wm * WTM + mh * 64 + mi * 16, ks);
+        };
+        auto mma = [&](int mh) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[mh * 4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][mi], bq[ks][ni],
+                                                                                       acc[mh * 4 + mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        };
+        read_a(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, wn * WTN + ni * 16, ks);
+        if (ABL != 1 && it + 1 < nk) issue_b(bbuf ^ 1);
+        __builtin_amdgcn_s_barrier();
+        if (ABL != 2) mma(0);
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[1][3]), "v"(bq[0][0]), "v"(bq[1][3]) : "memory");
+        __builtin_amdgcn_s_barrier();
+        read_a(1);
+        const int anext = abuf == 0 ? 2 : abuf - 1;
+        if (ABL != 1 && it + 2 < nk) {
+            issue_a(anext);
+            wait_vmcnt<A_INS>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (ABL != 2) mma(1);
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[1][3]) : "memory");
+        __builtin_amdgcn_s_barrier();
+        abuf = abuf == 2 ? 0 : abuf + 1;
+        bbuf ^= 1;
+    }
+    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
+    if (ABL == 3) {
+        if (acc[0][0][0] == 12345.f && acc[7][3][3] == 54321.f) p.out[tid] = acc[3][1][2];
+        return;
+    }
+
+    if constexpr (ADAM) {
+        // ---- fused Adam epilogue, per wave in four 32-row quarters (waves
+        // work independently: no block barrier after the first): the fp32
+        // gradient rows go through the wave's LDS slice so each lane owns 8
+        // consecutive columns (n) of a row (tap, c); all p/m/v loads of a
+        // quarter are in flight before the update; the transposed (KRSC) copy
+        // is re-staged as bf16 [n][32 rows] and stored as 16-byte runs along c.
+        // (A block-wide variant with 1 KiB row runs measured slower: the
+        // epilogue is latency-, not DRAM-page-bound.)
+        constexpr int QR = 32, SROWF = WTN * 4 + 16, SROWT = QR * 2 + 16;
+        constexpr int WB = QR * SROWF + WTN * SROWT;
+        static_assert(NW * WB <= 3 * ABUF + 2 * BBUF, "fused epilogue staging must fit");
+        const auto& A = p.adam;
+        const int fr = lane & 15;
+        const int cch = lane & 7, esub = lane >> 3;          // 8 lanes x 8 columns per row, 8 rows per pass
+        const int col0 = n0 + wn * WTN + cch * 8;
+        char* fbuf = smem + w * WB;
+        char* tbuf = fbuf + QR * SROWF;
+        lds_barrier();                                       // ring buffers are dead for every wave
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        *reinterpret_cast<float*>(fbuf + (mi * 16 + fg * 4 + r) * SROWF + (ni * 16 + fr) * 4) =
+                            acc[q * 2 + mi][ni][r];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            float pv[4][8], mv[4][8], vv[4][8];
+            long eo[4];
+            bool ok[4];
+            int tp[4], cc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rr = esub + 8 * i;
+                const int m = m0 + wm * WTM + q * QR + rr;
+                tp[i] = m / p.Cg;
+                cc[i] = m - tp[i] * p.Cg;
+                ok[i] = m < p.M && cc[i] < p.c_valid && col0 + 8 <= p.n_valid;
+                eo[i] = (long)tp[i] * p.o_tap + (long)cc[i] * p.o_c + col0;
+                if (ok[i]) {
+                    *reinterpret_cast<float4*>(pv[i]) = *reinterpret_cast<const float4*>(A.p + eo[i]);
+                    *reinterpret_cast<float4*>(pv[i] + 4) = *reinterpret_cast<const float4*>(A.p + eo[i] + 4);
+                    *reinterpret_cast<float4*>(mv[i]) = *reinterpret_cast<const float4*>(A.m + eo[i]);
+                    *reinterpret_cast<float4*>(mv[i] + 4) = *reinterpret_cast<const float4*>(A.m + eo[i] + 4);
+                    *reinterpret_cast<float4*>(vv[i]) = *reinterpret_cast<const float4*>(A.v + eo[i]);
+                    *reinterpret_cast<float4*>(vv[i] + 4) = *reinterpret_cast<const float4*>(A.v + eo[i] + 4);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rr = esub + 8 * i;
+                const float4 g0 = *reinterpret_cast<const float4*>(fbuf + rr * SROWF + cch * 32);
+                const float4 g1 = *reinterpret_cast<const float4*>(fbuf + rr * SROWF + cch * 32 + 16);
+                const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                float np[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if (ok[i]) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float gc = gg[j] * A.gs;
+                        const float mj = A.b1 * mv[i][j] + (1.f - A.b1) * gc;
+                        const float vj = A.b2 * vv[i][j] + (1.f - A.b2) * gc * gc;
+                        np[j] = pv[i][j] - A.lr_t * mj / (sqrtf(vj) + A.eps);
+                        mv[i][j] = mj;
+                        vv[i][j] = vj;
+                    }
+                    *reinterpret_cast<float4*>(A.p + eo[i]) = *reinterpret_cast<const float4*>(np);
+                    *reinterpret_cast<float4*>(A.p + eo[i] + 4) = *reinterpret_cast<const float4*>(np + 4);
+                    *reinterpret_cast<float4*>(A.m + eo[i]) = *reinterpret_cast<const float4*>(mv[i]);
+                    *reinterpret_cast<float4*>(A.m + eo[i] + 4) = *reinterpret_cast<const float4*>(mv[i] + 4);
+                    *reinterpret_cast<float4*>(A.v + eo[i]) = *reinterpret_cast<const float4*>(vv[i]);
+                    *reinterpret_cast<float4*>(A.v + eo[i] + 4) = *reinterpret_cast<const float4*>(vv[i] + 4);
+                    if (A.store_grad) {
+                        *reinterpret_cast<float4*>(p.out + eo[i]) = g0;
+                        *reinterpret_cast<float4*>(p.out + eo[i] + 4) = g1;
+                    }
+                    if (A.rows)
+                        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(A.rows) +
+                                                  ((long)tp[i] * A.rows_ap + cc[i]) * A.rows_bp + col0) = Chunk<bf16>::pack(np);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    *reinterpret_cast<bf16*>(tbuf + (cch * 8 + j) * SROWT + rr * 2) = (bf16)np[j];
+            }
+            if (A.tr) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const int n = n0 + wn * WTN + lane;              // one transposed row per lane
+#pragma unroll
+                for (int k = 0; k < QR / 8; ++k) {
+                    const int m = m0 + wm * WTM + q * QR + 8 * k;
+                    const int tap = m / p.Cg, c = m - (m / p.Cg) * p.Cg;
+                    if (m >= p.M || n >= p.n_valid || c >= p.c_valid) continue;
+                    const uint4 v8 = *reinterpret_cast<const uint4*>(tbuf + lane * SROWT + k * 16);
+                    bf16* dst = reinterpret_cast<bf16*>(A.tr) + ((long)n * A.RS + tap) * A.tr_ap + c;
+                    if (c + 8 <= p.c_valid && ((((uintptr_t)dst) & 15) == 0)) {
+                        *reinterpret_cast<uint4*>(dst) = v8;
+                    } else {
+                        const bf16* h = reinterpret_cast<const bf16*>(&v8);
+                        for (int j = 0; j < 8 && c + j < p.c_valid; ++j) dst[j] = h[j];
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tbuf / fbuf reads done before the next quarter
+        }
+        return;
+    }
+    // ---- epilogue: two 64-row halves per wave staged in LDS, then each lane
+    // stores 8 consecutive columns of a row (filter gradient or split slab)
+    constexpr int SROW = WTN * 4 + 16;
+    constexpr int ECPR = WTN / 8, RPP = 64 / ECPR;
+    const int fr = lane & 15;
+    const int cch = lane % ECPR, esub = lane / ECPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
+    char* wbuf = smem + w * 64 * SROW;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+        lds_barrier();
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                        acc[mh * 4 + mi][ni][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 2
+        for (int rr = esub; rr < 64; rr += RPP) {
+            const int m = m0 + wm * WTM + mh * 64 + rr;
+            if (m >= p.M || col0 >= p.N) continue;
+            const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
+            const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
+            if (p.partial) {
+                float* dst = p.partial + ((long)split * p.Mp + m) * p.N + col0;
+                *reinterpret_cast<float4*>(dst) = lo;
+                *reinterpret_cast<float4*>(dst + 4) = hi;
+                continue;
+            }
+            const int tap = m / p.Cg;
+            const int c = m - tap * p.Cg;
+            if (c >= p.c_valid) continue;
+            float* orow = p.out + (long)tap * p.o_tap + (long)c * p.o_c;
+            const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            if (p.o_n == 1 && col0 + 8 <= p.n_valid && ((((uintptr_t)(orow + col0)) & 15) == 0)) {
+                *reinterpret_cast<float4*>(orow + col0) = lo;
+                *reinterpret_cast<float4*>(orow + col0 + 4) = hi;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (col0 + j < p.n_valid) orow[(long)(col0 + j) * p.o_n] = v[j];
+            }
+        }
+    }
+}
+
+bool tn3_ok(const TNParams& p, int dtype) { return g_tn3 && dtype == SEG_BF16 && p.M >= 256 && p.N > 128; }
+
+void tn3_info(int M, int N, int P, int cus, int* splits) {
+    const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+    const int kt = (P + 63) / 64;
+    int s = 1;
+    if (tiles < cus) {
+        s = (int)((cus + tiles - 1) / tiles);
+        s = std::min(s, std::max(1, kt / 6));
+        s = std::min(s, 64);
+    }
+    *splits = s;
+}
+
+void launch_tn3(TNParams& p, int splits, hipStream_t s) {
+    const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256;
+    const dim3 g(tm * tn * splits), b(512);
+    const bool mfast = g_tn3_mfast && tm > tn;
+#define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<true, A, MF>), g, b, 0, s, p, tm, tn, splits)
+    switch (g_tn3_abl) {
+        case 1: TN3(1, false); return;
+        case 2: TN3(2, false); return;
+        case 3: TN3(3, false); return;
+    }
+    if (p.adam.p) {
+        if (mfast) hipLaunchKernelGGL((igemm_tn3<true, 0, true, true>), g, b, 0, s, p, tm, tn, splits);
+        else hipLaunchKernelGGL((igemm_tn3<true, 0, false, true>), g, b, 0, s, p, tm, tn, splits);
+        return;
+    }
+    if (mfast) TN3(0, true);
+    else TN3(0, false);
+#undef TN3
+}
+
+// the fused-Adam epilogue needs the whole reduction in one tile (no split-K
+// slabs), vector-aligned rows (o_n = 1, n_valid % 8 == 0) and 8-aligned taps
+bool tn3_adam_ok(const TNParams& p, int dtype) {
+    if (!tn3_ok(p, dtype) || p.o_n != 1 || (p.n_valid & 7) || (p.Cg & 7) || (p.o_c & 7) || (p.o_tap & 7)) return false;
+    int sp;
+    tn3_info(p.M, p.N, p.P, device_cus(), &sp);
+    return sp == 1;
+}
+
 }  // namespace seg

@@ -204,6 +204,32 @@ def tconv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None, dbias=None):
 PACK_KRSC, PACK_HWIO, PACK_TCONV_FWD, PACK_TCONV_BWD = 0, 1, 2, 3
 
 
+def wgrad_adam_fusable(desc):
+    """Whether seg_conv2d_bwd_filter_adam applies to this conv (bf16, the
+    256x256 TN kernel without split-K)."""
+    return bool(_lib.lib().seg_conv_wgrad_adam_fusable(ctypes.byref(desc)))
+
+
+def conv2d_bwd_filter_adam(desc, x, dy, p, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0,
+                           rows=None, tr=None, dw=None, dbias=None, ws=None, stream=None):
+    """Filter gradient fused with TF1 Adam on the filter (p, m, v: flat fp32
+    slices; rows / tr = (tensor, a_pad, b_pad) packed HWIO / KRSC copies)."""
+    d = _with_ld(desc, x, dy)
+    a = _lib.SegAdamFused()
+    a.p, a.m, a.v = p.data_ptr(), m.data_ptr(), v.data_ptr()
+    if rows is not None:
+        a.rows_dst, a.rows_ap, a.rows_bp = rows[0].data_ptr(), rows[1], rows[2]
+    if tr is not None:
+        a.tr_dst, a.tr_ap = tr[0].data_ptr(), tr[1]
+    a.lr, a.beta1, a.beta2, a.eps = float(lr), float(beta1), float(beta2), float(eps)
+    a.t, a.grad_scale = int(t), float(grad_scale)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_BWD_FILTER))
+    check(_lib.lib().seg_conv2d_bwd_filter_adam(ctypes.byref(d), ptr(x), ptr(dy),
+                                                None if dw is None else ptr(dw),
+                                                None if dbias is None else ptr(dbias), ctypes.byref(a), wsp, wss,
+                                                stream_ptr(stream)), "conv2d_backprop_filter_adam")
+
+
 def pack_filter(src, dst, a_pad, b_pad, mode, stream=None):
     """src fp32 [R,S,A,B] master -> dst packed compute copy (see segkern.h)."""
     R, S, A, B = src.shape

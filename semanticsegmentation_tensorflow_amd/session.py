@@ -103,7 +103,7 @@ class _AdamOverlap:
 
 class Session:
     def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None,
-                 overlap_optimizer=False):
+                 overlap_optimizer=False, fuse_adam=True):
         self.graph = graph or G.get_default_graph()
         if not torch.cuda.is_available():
             raise RuntimeError("Session needs an MI355X (HIP device); there is no CPU fallback")
@@ -121,6 +121,11 @@ class Session:
         self._adam = None
         self._adam_groups = {}
         self.overlap_optimizer = overlap_optimizer
+        # Adam fused into the filter-gradient epilogue where the library supports
+        # it (single process: nothing sits between gradient and update)
+        self.fuse_adam = fuse_adam
+        self.store_fused_grads = False   # tests: also write the fused layers' gradients
+        self._fused = None               # names updated inside backward this step
         self._side = None
         self._adam_ctx = None
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
@@ -507,6 +512,10 @@ class Session:
             c = cs[0]
             if c.kind in ("conv", "tconv") or (c.kind == "MaxPool" and n.kp is None):
                 p.mask_fuse.add(id(n))
+        p.adam_fusable = set()
+        for n in p.nodes:
+            if n.kind == "conv" and ops.wgrad_adam_fusable(n.desc):
+                p.adam_fusable.add(id(n))
         p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
         p.uncovered = [v for v in p.var_names if v not in covered]
         for v in p.uncovered:            # no gradient path: keep the grad slice at 0
@@ -670,6 +679,9 @@ class Session:
             gs = ts["grad_scale"] / (self.dp.world if self.dp is not None else 1)
             fresh = self._packed_version == store.version
             store.step += 1
+            self._fused = None
+            if self.fuse_adam and self.dp is None and not self.overlap_optimizer and fresh and p.adam_fusable:
+                self._fused = (opt, gs, set())
             if self.overlap_optimizer and self.device.type == "cuda":
                 # per-layer Adam on a side stream as soon as the layer's gradient is final
                 self._adam_ctx = _AdamOverlap(self, opt, gs)
@@ -682,10 +694,18 @@ class Session:
             if self._adam_ctx is not None:
                 self._adam_ctx.finish()
                 self._adam_ctx = None
+            elif self._fused is not None and self._fused[2]:
+                done = self._fused[2]
+                rest = [v.var_name for v in store.order if v.var_name not in done]
+                if rest:
+                    ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(rest), opt.lr,
+                                      store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
+                                      dtype=self._pack_dtype())
             else:
                 ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(), opt.lr,
                                   store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
                                   dtype=self._pack_dtype())
+            self._fused = None
             store.version += 1
             if fresh:           # the fused update rewrote every packed copy
                 self._packed_version = store.version
@@ -813,8 +833,19 @@ class Session:
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
                                 self._mask_epi(p, x))
                     done(dx, acc)
-                self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
-                            store.grad(n.w.var_name), ws, None, fused_db)
+                if self._fused is not None and id(n) in p.adam_fusable:
+                    # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
+                    opt, gs, fdone = self._fused
+                    wn = n.w.var_name
+                    self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)], dz,
+                                store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
+                                opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
+                                store.packed.get((wn, ops.PACK_KRSC)),
+                                store.grad(wn) if self.store_fused_grads else None, fused_db, ws)
+                    fdone.add(wn)
+                else:
+                    self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
+                                store.grad(n.w.var_name), ws, None, fused_db)
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "tconv":
                 x = n.inputs[0]

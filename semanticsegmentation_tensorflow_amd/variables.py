@@ -74,6 +74,12 @@ class VariableStore:
     def grad(self, name):
         return self._view(self.grads, name)
 
+    def adam_m(self, name):
+        return self._view(self.m, name)
+
+    def adam_v(self, name):
+        return self._view(self.v, name)
+
     def initialize(self):
         host = np.zeros(self.numel, dtype=np.float32)
         for v in self.vars:

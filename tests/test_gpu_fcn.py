@@ -77,6 +77,7 @@ def test_fcn_logits_grads_adam(dev, dtype):
                                                     bf16_round if dtype == "bf16" else None)
 
     sess = tf.Session(compute_dtype=dtype)
+    sess.store_fused_grads = True      # bf16: conv6/conv7 filters take the fused wgrad+Adam path
     sess.run(tf.global_variables_initializer())
     for k, v in weights.items():
         sess.assign(k, v)

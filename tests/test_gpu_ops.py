@@ -142,16 +142,20 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128"])
+@pytest.fixture(params=[1, 2, 3, 4, 5], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
-    where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles."""
+    where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles,
+    5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off in 2 so
+    igemm_tn2 stays covered for wide problems)."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
-    ops.set_option("wgrad_halo", 1 if v >= 3 else 0)
+    ops.set_option("wgrad_halo", 1 if v in (3, 4) else 0)
     ops.set_option("wgrad_nt", 128 if v == 4 else 64)
+    ops.set_option("tn3", 0 if v == 2 else 1)
     yield v
+    ops.set_option("tn3", 1)
     ops.set_option("igemm_tn_variant", 2)
     ops.set_option("wgrad_halo", 1)
     ops.set_option("wgrad_nt", 128)
@@ -504,3 +508,60 @@ def test_adam_tf1_pack_matches_step_plus_pack(dev, dtype):
         ops.pack_filter(src, want, ops.round8(A), ops.round8(B), mode)
         torch.cuda.synchronize()
         assert torch.equal(t, want), f"copy mode {mode} of {shape}"
+
+
+# (N, H, W, C, K, R): filters whose gradient takes the fused wgrad + TF1 Adam launch
+ADAM_FUSED_CASES = [
+    (1, 5, 7, 40, 264, 7),      # conv6-like 7x7; K tail of the 256-wide tile
+    (1, 5, 7, 36, 264, 7),      # c_valid = 36 < Cg = 40: padding rows of the packed copies untouched
+    (2, 6, 9, 512, 512, 1),     # conv7-like 1x1
+]
+
+
+@pytest.mark.parametrize("case", ADAM_FUSED_CASES)
+def test_conv2d_bwd_filter_adam_fused(dev, case):
+    """seg_conv2d_bwd_filter_adam == Conv2DBackpropFilter, then TF1 Adam
+    (FCN.py:338) on the filter, then repacking of the HWIO / KRSC copies."""
+    N, H, W, C, K, R = case
+    d = ops.conv_desc(N, H, W, C, K, R, R, dtype=ops.BF16)
+    assert ops.wgrad_adam_fusable(d)
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    dy = torch.randn(N, H, W, K, generator=g, dtype=torch.float64)
+    p0 = torch.randn(R, R, C, K, generator=g) * 0.05
+    m0 = torch.randn(R, R, C, K, generator=g) * 1e-3
+    v0 = torch.rand(R, R, C, K, generator=g) * 1e-5
+    xd, dyd = to_dev(x, torch.bfloat16, dev), to_dev(dy, torch.bfloat16, dev)
+    # reference gradient from the plain filter-gradient path
+    gref = torch.empty(R, R, C, K, device=dev)
+    ops.conv2d_bwd_filter(d, xd, dyd, gref)
+    p, m, v = p0.to(dev), m0.to(dev), v0.to(dev)
+    cp, kp = ops.round8(C), ops.round8(K)
+    rows = torch.full(ops.packed_shape(R, R, C, K, ops.PACK_HWIO), 7.0, dtype=torch.bfloat16, device=dev)
+    tr = torch.full(ops.packed_shape(R, R, C, K, ops.PACK_KRSC), 7.0, dtype=torch.bfloat16, device=dev)
+    dw = torch.full((R, R, C, K), float("nan"), device=dev)
+    lr, t, gs = 1e-3, 3, 0.5
+    ops.conv2d_bwd_filter_adam(d, xd, dyd, p, m, v, lr, t, grad_scale=gs, rows=(rows, cp, kp), tr=(tr, cp, kp),
+                               dw=dw)
+    torch.cuda.synchronize()
+    gr = gref.cpu().double()
+    assert (dw.cpu().double() - gr).abs().max().item() <= 1e-6 * gr.abs().max().item()
+    gc = gr * gs
+    me = 0.9 * m0.double() + 0.1 * gc
+    ve = 0.999 * v0.double() + 0.001 * gc * gc
+    lr_t = lr * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+    pe = p0.double() - lr_t * me / (ve.sqrt() + 1e-8)
+    # fp32 arithmetic as TF1's kernel: (1 - beta2) = 1 - 0.999f carries 4.7e-5 relative
+    for got, ref, nm, tol in ((p, pe, "p", 1e-5), (m, me, "m", 1e-5), (v, ve, "v", 1e-4)):
+        err = (got.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < tol, (nm, err)
+    # packed copies: valid entries = bf16(new p), padding entries untouched (7.0)
+    pb = p.cpu().to(torch.bfloat16)
+    rh = rows.cpu().view(R * R, cp, kp)
+    assert torch.equal(rh[:, :C, :K], pb.view(R * R, C, K))
+    if cp > C:
+        assert (rh[:, C:, :] == 7.0).all()
+    tk = tr.cpu().view(kp, R * R, cp)
+    assert torch.equal(tk[:K, :, :C], pb.view(R * R, C, K).permute(2, 0, 1))
+    if cp > C:
+        assert (tk[:, :, C:] == 7.0).all()

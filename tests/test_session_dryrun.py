@@ -22,7 +22,8 @@ class _Rec:
         real_fn = getattr(self.real, name)
         host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
-                             "seg_adam_segments_plan", "seg_tconv_filter_apad")
+                             "seg_adam_segments_plan", "seg_tconv_filter_apad",
+                             "seg_conv_wgrad_adam_fusable")
 
         def fn(*a):
             if host_only:
@@ -65,7 +66,10 @@ def test_fcn_train_plan(dry):
     assert c.count("seg_softmax_xent_fwd_bwd") == 1
     # backward: conv1_1 needs no input gradient (image is a placeholder)
     assert c.count("seg_conv2d_bwd_data") == 16
-    assert c.count("seg_conv2d_bwd_filter") == 17
+    # conv6 / conv7 filters (bf16, 256x256 TN tiles without split-K) take the
+    # wgrad+Adam fused launch; the other 15 the plain filter gradient
+    assert c.count("seg_conv2d_bwd_filter") == 15
+    assert c.count("seg_conv2d_bwd_filter_adam") == 2
     assert c.count("seg_tconv2d_bwd_data") == 3
     assert c.count("seg_tconv2d_bwd_filter") == 3
     assert c.count("seg_maxpool2x2_bwd") == 5
@@ -81,9 +85,12 @@ def test_fcn_train_plan(dry):
     # the fused Adam launch rewrote every packed copy: no repack pass
     assert dry.calls.count("seg_pack_filter") == 0
     assert dry.calls.count("seg_adam_tf1_pack") == 1
-    # the segment table covers every variable once, with both copies of each conv
-    plan = sess._adam
-    assert plan.nsegs == len(sess.store.vars)
+    # the segment table covers every variable once (except the two filters
+    # updated by the fused wgrad+Adam launches), with both copies of each conv
+    assert dry.calls.count("seg_conv2d_bwd_filter_adam") == 2
+    (gk, plan), = sess._adam_groups.items()
+    assert plan.nsegs == len(sess.store.vars) - 2
+    assert "conv6/weights" not in gk[1] and "conv7/weights" not in gk[1]
     assert dry.calls.count("seg_conv2d_fwd") == 17
 
 

@@ -1,5 +1,7 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r01e
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r01e/pytest.log 2>&1; rc=$?; tail -4 gpurun_out/r01e/pytest.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/r01e/pytest.log | head -20; exit 1; }
-timeout -k 10 200 python bench.py --kernel-table --no-traffic --no-cpu-baseline > gpurun_out/r01e/bench.json 2> gpurun_out/r01e/kt.txt && cat gpurun_out/r01e/bench.json && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r01e/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-traffic > /dev/null 2> gpurun_out/r01e/prof.err
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "adam_fused" -x -q --timeout 120 --timeout-method thread > /tmp/pf.log 2>&1; rc=$?; tail -2 /tmp/pf.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" /tmp/pf.log | head; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fcn.py -x -q --timeout 120 --timeout-method thread > /tmp/pf2.log 2>&1; rc=$?; tail -2 /tmp/pf2.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" /tmp/pf2.log | head; exit 1; }
+for a in "--no-fuse-adam" ""; do
+  timeout -k 10 200 python bench.py $a --kernel-table --no-traffic --no-cpu-baseline > /tmp/b.json 2> /tmp/kt.txt || exit 1
+  echo "== $a: $(python -c "import json;print(json.load(open('/tmp/b.json'))['value'])")"; grep "op=2" /tmp/kt.txt | grep tn3
+done
