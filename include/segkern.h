@@ -242,6 +242,9 @@ int seg_softmax_xent_soft_fwd_bwd(const void* logits, int ld, const float* label
                                   int W, int C, int valid_h, int valid_w, float grad_scale,
                                   float* loss_sum, void* dlogits, int ld_d, int dtype, void* ws,
                                   size_t ws_bytes, void* stream);
+/* tf.nn.softmax over channels (eval path, Network/utils/utils.py:54 and
+ * Network/model/FCN.py gen_test_output): y[p, c] for c < C, 0 for padding. */
+int seg_softmax(const void* x, int ldx, int C, long P, void* y, int ldy, int dtype, void* stream);
 /* pred[p] = argmax_c logits[p, c] (ties -> lowest index). */
 int seg_argmax(const void* logits, int ld, int C, long P, int64_t* pred, int dtype, void* stream);
 /* Confusion matrix counts conf[t*C+p] += 1 over the valid region (mIoU). */

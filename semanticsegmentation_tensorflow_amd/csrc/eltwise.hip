@@ -609,6 +609,21 @@ __global__ void argmax_k(const T* __restrict__ logits, int ld, int C, long P, in
     }
 }
 
+// tf.nn.softmax over the channel dim (Network/utils/utils.py:54 eval path):
+// max-subtracted, padding channels >= C written as 0.
+template <typename T>
+__global__ void softmax_k(const T* __restrict__ x, int ldx, int C, long P, T* __restrict__ y, int ldy) {
+    for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+        float mx = to_f32(x[p * ldx]);
+        for (int c = 1; c < C; ++c) mx = fmaxf(mx, to_f32(x[p * ldx + c]));
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += expf(to_f32(x[p * ldx + c]) - mx);
+        const float inv = 1.f / s;
+        for (int c = 0; c < ldy; ++c)
+            y[p * ldy + c] = from_f32<T>(c < C ? expf(to_f32(x[p * ldx + c]) - mx) * inv : 0.f);
+    }
+}
+
 __global__ void confusion_k(const int64_t* __restrict__ pred, const uint8_t* __restrict__ lab, int N, int H, int W,
                             int vh, int vw, int C, unsigned long long* conf) {
     const long P = (long)N * H * W;
@@ -950,6 +965,14 @@ extern "C" int seg_argmax(const void* logits, int ld, int C, long P, int64_t* pr
     if (!logits || !pred || C < 1) return SEG_EINVAL;
     DISPATCH_T(dtype, hipLaunchKernelGGL(argmax_k<T>, dim3(seg_grid_1d(P, 256)), dim3(256), 0, (hipStream_t)stream,
                                          (const T*)logits, ld, C, P, pred));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_softmax(const void* x, int ldx, int C, long P, void* y, int ldy, int dtype, void* stream) {
+    if (!x || !y || C < 1 || ldx < C || ldy < C) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(softmax_k<T>, dim3(seg_grid_1d(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, ldx, C, P, (T*)y, ldy));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

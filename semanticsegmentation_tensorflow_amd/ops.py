@@ -422,6 +422,14 @@ def softmax_xent(logits, labels, dlogits, loss_sum, num_classes, valid_hw=None, 
     return loss_sum
 
 
+def softmax(x, y, num_classes, stream=None):
+    """tf.nn.softmax over the (padded) channel dim of NHWC x into y."""
+    P = x.numel() // x.shape[-1]
+    check(_lib.lib().seg_softmax(ptr(x), pixel_stride(x), int(num_classes), P, ptr(y), pixel_stride(y),
+                                 seg_dtype(x), stream_ptr(stream)), "softmax")
+    return y
+
+
 def argmax(logits, pred, num_classes, stream=None):
     N, H, W, _ = logits.shape
     check(_lib.lib().seg_argmax(ptr(logits), pixel_stride(logits), num_classes, N * H * W,
@@ -484,6 +492,13 @@ def adam_tf1_pack(p, g, m, v, plan, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, gra
     check(_lib.lib().seg_adam_tf1_pack(ptr(p), ptr(g), ptr(m), ptr(v), ptr(plan.table), plan.nsegs,
                                        plan.total_tiles, float(lr), float(beta1), float(beta2), float(eps),
                                        int(t), float(grad_scale), int(dtype), stream_ptr(stream)), "adam_pack")
+
+
+def cast(x, y, stream=None):
+    """Elementwise dtype conversion x -> y (same number of elements)."""
+    assert x.numel() == y.numel()
+    check(_lib.lib().seg_cast(ptr(x), seg_dtype(x), ptr(y), seg_dtype(y), x.numel(), stream_ptr(stream)), "cast")
+    return y
 
 
 def fill(y, value, stream=None):

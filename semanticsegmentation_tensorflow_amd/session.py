@@ -668,6 +668,10 @@ class Session:
                 x = buf[id(n.inputs[0])]
                 C = p.shapes[id(n.inputs[0])][3]
                 ops.argmax(x, y.view(-1), C)
+            elif k == "Softmax":
+                ops.softmax(buf[id(n.inputs[0])], y, p.shapes[id(n.inputs[0])][3])
+            elif k == "ResizeBilinear":
+                ops.resize_bilinear_fwd(buf[id(n.inputs[0])], y)
             elif k == "ExpandDims":
                 pass
             else:
@@ -922,6 +926,21 @@ class Session:
                 else:
                     ops.copy_channels(dy, dx)
                 done(dx, acc)
+            elif k == "ResizeBilinear":
+                # align_corners bilinear: fp32 scatter-add, then cast to the compute dtype
+                x = n.inputs[0]
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    g32 = p.tmp.get(("rb32", id(x)))
+                    if g32 is None:
+                        g32 = torch.zeros(dx.shape, dtype=torch.float32, device=self.device)
+                        p.tmp[("rb32", id(x))] = g32
+                    ops.resize_bilinear_bwd(dy, g32)
+                    ops.cast(g32, dx)
+                    done(dx, acc)
+            elif k == "Softmax":
+                raise NotImplementedError("gradient of tf.nn.softmax: the reference uses it for evaluation only "
+                                          "(Network/utils/utils.py:54); train on softmax_cross_entropy_with_logits")
             elif k in ("ArgMax", "ExpandDims"):
                 continue
             else:
