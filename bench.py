@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-miou", action="store_true", help="skip the mIoU parity probe")
     ap.add_argument("--no-fuse-adam", action="store_true",
                     help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
     ap.add_argument("--overlap-optimizer", action="store_true",
@@ -120,6 +121,42 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
             "sample": f"oracle {'FCN' if model == 'fcn' else 'FC-DenseNet'} fwd+bwd, torch-CPU fp32, "
                       f"1 image {HP}x{WP} ({H}x{W} padded), "
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
+
+
+def miou_parity(sess, pred, image, keep, img, lab, H, W, model):
+    """mIoU of the trained model's class map on the benchmark batch (device,
+    masked to HxW), and -- on image 0 -- the CPU oracle's class map from the
+    same fp32 master weights (float64, bf16-rounded at the device's rounding
+    points): agreement of the two maps and both mIoUs."""
+    import numpy as np
+    import torch
+    from oracle import models as M
+    from semanticsegmentation_tensorflow_amd import evaluate as E
+    from semanticsegmentation_tensorflow_amd import ops
+    pr = sess.run(pred, feed_dict={image: img, keep: 1.0}, as_numpy=False)
+    m = E.MeanIoU(2, img.device, (H, W)).update(pr, lab)
+    miou, _ = m.result()
+    out = {"miou": round(miou, 5), "miou_images": int(img.shape[0])}
+    if model != "fcn":
+        return out
+    names = M.fcn_param_shapes(3, 2)
+    p = {k: torch.from_numpy(sess.variable_value(k)).double() for k in names}
+    if sess.cdt == ops.BF16:   # bf16 compute: the device sees bf16 filters / input
+        p = {k: (v.to(torch.bfloat16).double() if v.dim() == 4 else v) for k, v in p.items()}
+    x0 = img[:1].double().cpu()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        q = (lambda t: t.to(torch.bfloat16).double()) if sess.cdt == ops.BF16 else None
+        rp, _ = M.fcn_forward(p, x0, quant=q)
+    dt = time.perf_counter() - t0
+    gp = pr[:1].reshape(rp.shape).cpu()
+    agree = (gp[:, :H, :W] == rp[:, :H, :W]).double().mean().item()
+    mo = E.MeanIoU(2, img.device, (H, W)).update(rp.to(img.device).reshape(1, *lab.shape[1:]), lab[:1])
+    mg = E.MeanIoU(2, img.device, (H, W)).update(gp.to(img.device).reshape(1, *lab.shape[1:]), lab[:1])
+    out.update({"image0_miou_device": round(mg.result()[0], 5), "image0_miou_oracle": round(mo.result()[0], 5),
+                "image0_class_map_agreement": round(agree, 6),
+                "oracle": f"oracle FCN forward, float64 (bf16 rounding points), {dt:.1f} s"})
+    return out
 
 
 def kernel_symbol(name):
@@ -263,6 +300,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     loss_val = float(sess.run(loss, feed_dict=feed))
+    miou = None
+    if rank == 0 and not args.no_miou:
+        try:
+            miou = miou_parity(sess, pred, image, keep, img, lab, H, W, args.model)
+        except Exception as exc:  # report, never crash the headline line
+            miou = {"error": repr(exc)}
 
     # ---- per-kernel timing (HIP events on the launch stream) for the roofline
     sess.timer = []
@@ -334,11 +377,12 @@ def main():
         if (HP, WP) == (384, 1248) or args.model != "fcn" else None,
         "conv_gflop_per_step_measured": round(step_conv_flops / 1e9, 2),
         "loss_after": round(loss_val, 5),
+        "miou_parity": miou,
     }
     if rank == 0 and world == 1 and not args.no_traffic:
         try:
             argv = [a for a in sys.argv[1:] if a not in ("--kernel-table",)]
-            argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic"]
+            argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-miou"]
             t = pmc_traffic(argv, kernel_symbol(dname), os.path.join(ROOT, "gpurun_out", "bench_pmc"))
             result["roofline"]["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
             result["roofline"]["traffic_detail"] = {
