@@ -692,8 +692,12 @@ extern "C" size_t seg_bias_grad_workspace(long P, int K) {
     return (size_t)RED_BLOCKS * 2 * K * sizeof(float);
 }
 
-static int red_blocks(long P) {
-    long b = (P + 63) / 64;
+// Enough workgroups to keep many rows in flight: each covers about two passes
+// of its row groups (64 pixels at K = 64, 2 pixels at K = 4096), capped.
+static int red_blocks(long P, int K, int epc) {
+    const RedGeom g = red_geom(K, epc);
+    const long per = 2L * g.rows;
+    long b = (P + per - 1) / per;
     if (b > RED_BLOCKS) b = RED_BLOCKS;
     if (b < 1) b = 1;
     return (int)b;
@@ -704,7 +708,7 @@ extern "C" int seg_bias_relu_bwd(const void* dy, int ld_dy, const void* y, int l
                                  size_t ws_bytes, void* stream) {
     if (!dy || !dz || (relu && !y) || (K & 7) || P <= 0) return SEG_EINVAL;
     if (K > 4096) return SEG_EINVAL;
-    const int nb = red_blocks(P);
+    const int nb = red_blocks(P, K, epc_of(dtype));
     hipStream_t s = (hipStream_t)stream;
     const RedGeom g = red_geom(K, epc_of(dtype));
     const size_t shm = (size_t)g.rows * K * sizeof(float);
@@ -882,7 +886,7 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
                                int cv, int relu, int dtype, void* ws, size_t ws_bytes, void* stream) {
     if (!x || !y || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7)) return SEG_EINVAL;
     if (C > 4096) return SEG_EINVAL;
-    const int nb = red_blocks(P);
+    const int nb = red_blocks(P, C, epc_of(dtype));
     if (!ws || ws_bytes < (size_t)nb * 2 * C * sizeof(float)) return SEG_EWORKSPACE;
     const float inv = 1.0f / sqrtf(1.0f + eps);
     const RedGeom g = red_geom(C, epc_of(dtype));

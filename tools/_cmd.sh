@@ -1,2 +1,4 @@
 export TMPDIR=/tmp
-timeout -k 10 400 python bench.py > /tmp/b.json 2>/tmp/b.err; rc=$?; cat /tmp/b.json; [ $rc -eq 0 ] || tail -20 /tmp/b.err
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > /tmp/pt.log 2>&1; rc=$?; tail -2 /tmp/pt.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" /tmp/pt.log | head -20; exit 1; }
+timeout -k 10 200 python bench.py --kernel-table --no-traffic --no-cpu-baseline --no-miou > /tmp/b.json 2> /tmp/kt.txt || exit 1
+python -c "import json;print(json.load(open('/tmp/b.json'))['value'])"
