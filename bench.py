@@ -36,11 +36,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="fcn", choices=["fcn", "fcdensenet"],
-                    help="fcn = config C2/C4 (headline); fcdensenet = config C3 (U-Net)")
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU (fcn 4, fcdensenet 8)")
-    ap.add_argument("--height", type=int, default=375)
-    ap.add_argument("--width", type=int, default=1242)
+    ap.add_argument("--model", default="fcn", choices=["fcn", "fcdensenet", "deeplab"],
+                    help="fcn = config C2/C4 (headline); fcdensenet = config C3 (U-Net); "
+                         "deeplab = config C5 (atrous + ASPP + bilinear, 1024x2048 Cityscapes-shaped)")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (fcn 4, fcdensenet 8, deeplab 2)")
+    ap.add_argument("--height", type=int, default=None, help="375 (KITTI); deeplab 1024")
+    ap.add_argument("--width", type=int, default=None, help="1242 (KITTI); deeplab 2048")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--keep-prob", type=float, default=None,
                     help="fcn 0.8 (FCN.py:395), fcdensenet 0.2 (FCDenseNet.py:13)")
@@ -93,8 +94,9 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
-    shapes = M.fcn_param_shapes(3, 2) if model == "fcn" else M.fcdensenet_param_shapes(3, 2)
-    fwd = M.fcn_forward if model == "fcn" else M.fcdensenet_forward
+    shapes = {"fcn": M.fcn_param_shapes, "fcdensenet": M.fcdensenet_param_shapes,
+              "deeplab": M.deeplab_param_shapes}[model](3, 2)
+    fwd = {"fcn": M.fcn_forward, "fcdensenet": M.fcdensenet_forward, "deeplab": M.deeplab_forward}[model]
     p = {k: torch.from_numpy((rng.standard_normal(s, dtype=np.float32) * 0.01).astype(np.float32)
                              ).requires_grad_(True)
          for k, s in shapes.items()}
@@ -118,7 +120,8 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
         step()
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(1.0 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle {'FCN' if model == 'fcn' else 'FC-DenseNet'} fwd+bwd, torch-CPU fp32, "
+            "sample": f"oracle {dict(fcn='FCN', fcdensenet='FC-DenseNet', deeplab='DeepLab-ASPP')[model]} "
+                      f"fwd+bwd, torch-CPU fp32, "
                       f"1 image {HP}x{WP} ({H}x{W} padded), "
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
 
@@ -254,19 +257,23 @@ def main():
 
     from semanticsegmentation_tensorflow_amd import graph as G
     from semanticsegmentation_tensorflow_amd import ops, tf
+    from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
     from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
     from semanticsegmentation_tensorflow_amd.fcn import FCN
 
-    H, W = args.height, args.width
+    H = args.height or (1024 if args.model == "deeplab" else 375)
+    W = args.width or (2048 if args.model == "deeplab" else 1242)
     HP, WP = pad32(H), pad32(W)
-    B = args.batch or (4 if args.model == "fcn" else 8)
-    kp = args.keep_prob if args.keep_prob is not None else (0.8 if args.model == "fcn" else 0.2)
+    B = args.batch or {"fcn": 4, "fcdensenet": 8, "deeplab": 2}[args.model]
+    kp = args.keep_prob if args.keep_prob is not None else {"fcn": 0.8, "fcdensenet": 0.2, "deeplab": 0.9}[args.model]
     G.reset_default_graph()
     image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
     labels = tf.placeholder(tf.uint8, [None, HP, WP], name="annotation")
     keep = tf.placeholder(tf.float32, name="keep_probability")
     if args.model == "fcn":
         pred, logits = FCN(image, keep, 2).create()
+    elif args.model == "deeplab":
+        pred, logits = DeepLabASPP(image, keep, 2)
     else:
         pred, logits = FCDenseNet(image, keep, 2)
     loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
@@ -351,9 +358,12 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic",
         "config": {
-            "workload": ("FCN (reference Network/model/FCN.py topology)" if args.model == "fcn" else
-                         "FC-DenseNet 'U-Net' (reference Network/model/FCDenseNet.py topology)")
-                        + " train step: fwd + softmax-xent + bwd + TF1 Adam, 375x1242x3 zero-padded to 384x1248",
+            "workload": {"fcn": "FCN (reference Network/model/FCN.py topology)",
+                         "fcdensenet": "FC-DenseNet 'U-Net' (reference Network/model/FCDenseNet.py topology)",
+                         "deeplab": "DeepLab-style atrous VGG16 + ASPP (rates 6/12/18) + bilinear x8 "
+                                    "(semanticsegmentation_tensorflow_amd/deeplab.py; config C5)"}[args.model]
+                        + f" train step: fwd + softmax-xent + bwd + TF1 Adam, {H}x{W}x3"
+                        + (f" zero-padded to {HP}x{WP}" if (HP, WP) != (H, W) else ""),
             "global_batch": B * world,
             "batch_per_gpu": B,
             "image": f"{H}x{W} -> {HP}x{WP}",

@@ -200,3 +200,69 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
     logits = conv(h, "final_conv")
     pred = tf.argmax(logits).unsqueeze(-1)
     return pred, logits
+
+
+# ---------------------------------------------------------------------------
+# DeepLab-style atrous model (config C5), semanticsegmentation_tensorflow_amd/
+# deeplab.py: VGG16 backbone at output stride 8 (conv5 rate 2), ASPP (1x1 +
+# rates 6/12/18, frozen BN + ReLU), 1x1 projection, classifier, bilinear x8.
+# ---------------------------------------------------------------------------
+DEEPLAB_ASPP_RATES = (6, 12, 18)
+
+
+def deeplab_param_shapes(in_channels=3, num_classes=2, depth=256):
+    shapes = {}
+    chans = [("conv1_1", in_channels, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
+             ("conv3_1", 128, 256), ("conv3_2", 256, 256), ("conv3_3", 256, 256), ("conv4_1", 256, 512),
+             ("conv4_2", 512, 512), ("conv4_3", 512, 512), ("conv5_1", 512, 512), ("conv5_2", 512, 512),
+             ("conv5_3", 512, 512)]
+    for n, ci, co in chans:
+        shapes[f"{n}/weights"] = (3, 3, ci, co)
+        shapes[f"{n}/biases"] = (co,)
+    bn = _BNCounter()
+
+    def bnv(c):
+        n = bn.next()
+        shapes[f"{n}/gamma"] = (c,)
+        shapes[f"{n}/beta"] = (c,)
+
+    shapes["aspp0/weights"] = (1, 1, 512, depth)
+    bnv(depth)
+    for i in range(3):
+        shapes[f"aspp{i + 1}/weights"] = (3, 3, 512, depth)
+        bnv(depth)
+    shapes["concat_projection/weights"] = (1, 1, 4 * depth, depth)
+    bnv(depth)
+    shapes["Last_layer/weights"] = (1, 1, depth, num_classes)
+    return shapes
+
+
+def deeplab_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
+    q = quant or (lambda t: t)
+    bn = _BNCounter()
+
+    def BN(h):
+        n = bn.next()
+        return tf.batch_norm_frozen(h, p[f"{n}/gamma"], p[f"{n}/beta"])
+
+    def cl(h, name, rate=1):
+        return q(tf.relu(tf.bias_add(tf.conv2d(h, p[f"{name}/weights"], dilation=rate), p[f"{name}/biases"])))
+
+    h = cl(cl(x, "conv1_1"), "conv1_2")
+    h = tf.max_pool2x2(h)
+    h = cl(cl(h, "conv2_1"), "conv2_2")
+    h = tf.max_pool2x2(h)
+    h = cl(cl(cl(h, "conv3_1"), "conv3_2"), "conv3_3")
+    h = tf.max_pool2x2(h)
+    h = cl(cl(cl(h, "conv4_1"), "conv4_2"), "conv4_3")
+    feat = cl(cl(cl(h, "conv5_1", 2), "conv5_2", 2), "conv5_3", 2)
+    br = [q(tf.relu(BN(q(tf.conv2d(feat, p["aspp0/weights"])))))]
+    for i, r in enumerate(DEEPLAB_ASPP_RATES):
+        br.append(q(tf.relu(BN(q(tf.conv2d(feat, p[f"aspp{i + 1}/weights"], dilation=r))))))
+    h = tf.concat(br)
+    h = q(tf.relu(BN(q(tf.conv2d(h, p["concat_projection/weights"])))))
+    h = tf.dropout(h, keep_prob)
+    last = q(tf.conv2d(h, p["Last_layer/weights"]))
+    logits = q(tf.resize_bilinear(last, (x.shape[1], x.shape[2])))
+    pred = tf.argmax(logits).unsqueeze(-1)
+    return pred, logits

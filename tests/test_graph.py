@@ -75,3 +75,16 @@ def test_fcdensenet_variables_match_reference():
     assert ref["transition_up1/weights"] == (4, 4, 348, 430)
     assert ref["transition_up5/weights"] == (4, 4, 128, 320)
     assert ref["final_conv/weights"] == (1, 1, 256, 2)
+
+
+def test_deeplab_variables_match_oracle():
+    """C5 DeepLab-style model: graph variables == the oracle's parameter table
+    (VGG16 stack with biases, ASPP / projection BN gammas+betas, bias-free heads)."""
+    from oracle import models as M
+    from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, 64, 96, 3])
+    pred, logits = DeepLabASPP(image, 1.0, 2)
+    got = {v.var_name: tuple(v.shape) for v in tf.global_variables()}
+    assert got == {k: tuple(s) for k, s in M.deeplab_param_shapes(3, 2).items()}
+    assert tuple(logits.shape) == (None, 64, 96, 2) or list(logits.shape)[1:] == [64, 96, 2]
