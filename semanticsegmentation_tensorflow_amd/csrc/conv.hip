@@ -514,6 +514,21 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_wgrad_halo = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "wgrad_abl")) {   // diagnostic builds only: results are garbage
+        if (value < 0 || value > 3) return SEG_EINVAL;
+        seg::g_wgrad_abl = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wgrad_nbias")) {
+        if (value < 1 || value > 4) return SEG_EINVAL;
+        seg::g_wgrad_nbias = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wgrad_la")) {
+        if (value != 1 && value != 2) return SEG_EINVAL;
+        seg::g_wgrad_la = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "wgrad_nt")) {
         if (value != 64 && value != 128) return SEG_EINVAL;
         seg::g_wgrad_nt = value;

@@ -138,12 +138,15 @@ void launch_smallc_wgrad(TNParams& p, int splits, hipStream_t s);
 
 // halo-tiled filter gradient (wgrad.hip) for stride-1 3x3 TN problems
 struct WgradPlan {
-    int bw, nt, splits;
+    int bw, nt, splits, nbias;
     long blocks;
     int g[10];
 };
 extern int g_wgrad_halo;
 extern int g_wgrad_nt;
+extern int g_wgrad_la;
+extern int g_wgrad_abl;
+extern int g_wgrad_nbias;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s);

@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
 
 __global__ void splitk_reduce_tn(TNParams p, int splits) {
     const int c4 = p.N / 4;
-    const long total = (long)p.Mp * c4;
+    const long total = (long)(p.Mp > p.M ? p.M + 1 : p.M) * c4;   // slab rows M..Mp-1: BiasAddGrad partials
     const long slab = (long)p.Mp * p.N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int m = (int)(i / c4);
@@ -582,6 +582,11 @@ __global__ void splitk_reduce_tn(TNParams p, int splits) {
             const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
             s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
         }
+        for (int r = p.M + 1; m == p.M && r < p.Mp; ++r)   // further BiasAddGrad partial rows
+            for (int zz = 0; zz < splits; ++zz) {
+                const float4 a = *reinterpret_cast<const float4*>(p.partial + zz * slab + (long)r * p.N + n0);
+                s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+            }
         const float vv[4] = {s.x, s.y, s.z, s.w};
         if (m == p.M) {               // fused BiasAddGrad row
 #pragma unroll
@@ -823,7 +828,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     WgradPlan wp;
     if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
-        if (p.dbias) p.Mp = p.M + 1;          // wgrad_halo sums dy columns too
+        if (p.dbias) p.Mp = p.M + wp.nbias;   // wgrad_halo sums dy columns too (nbias partial rows)
         if (wp.splits > 1) {
             if (!ws || ws_bytes < wgrad_workspace(wp, p)) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);

@@ -32,10 +32,14 @@ static __device__ uint4 wg_zero_page[4];
 
 int g_wgrad_halo = 1;
 int g_wgrad_nt = 128;
+int g_wgrad_la = 1;
+int g_wgrad_abl = 0;
+int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
 
 struct WGGeom {
     int tiles_x, tiles_y, nimg, hwd, hrows;
     int nct, nnt, splits, tps, ptiles;
+    int nbias;    // fused BiasAddGrad spread over the first nbias channel blocks
 };
 
 template <int ROWB>
@@ -46,7 +50,10 @@ __device__ __forceinline__ int wg_swz(int row) {
 
 // NST LDS stages (tile t+NST-1 in flight while t is consumed); HI halo DMA
 // pieces per wave (8 rows each): 4 covers dilation 1, 5 dilation 2.
-template <int BW, int NT, int NST, int HI>
+// LA: A-fragment read-ahead distance in (substep, tap) steps (1 or 2).
+// ABL (diagnostic builds, garbage results): 1 no DMA in the loop, 2 no MFMA,
+// 3 no LDS fragment reads.
+template <int BW, int NT, int NST, int HI, int LA = 1, int ABL = 0>
 __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     using T = bf16;
     constexpr int NW = 8, BH = 128 / BW;
@@ -128,9 +135,13 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // fused BiasAddGrad: the first channel chunk's cf == 0 waves sum their dy
-    // fragments (8 pixels x column fr per lane and substep)
-    const bool do_bias = p.dbias != nullptr && ct == 0 && cf == 0;
+    // fused BiasAddGrad, spread so no wave carries much extra VALU (a block
+    // waits for its slowest wave at every tile barrier, and the kernel for its
+    // slowest block): channel block ct < nbias sums the dy fragments of the
+    // substeps ss = ct (mod nbias), and within it wave cf only fragment ni = cf
+    // (8 pixels x column fr per lane).  Each (ct, n) partial goes to its own
+    // split-K slab row M + ct (or straight to dbias when nbias == 1).
+    const bool do_bias = p.dbias != nullptr && ct < g.nbias && cf < NF;
     float dsum[NF];
 #pragma unroll
     for (int j = 0; j < NF; ++j) dsum[j] = 0.f;
@@ -143,6 +154,27 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) tapoff[r * 3 + s] = r * p.tsh * g.hwd + s * p.tsw;
 
+    // LA == 2: per-lane LDS byte offsets of every tap's A fragment (rows kk and
+    // kk + 4 of substep 0) and of every B fragment
+    unsigned a_lo[9], a_hi[9], b_lo[NF], b_hi[NF];
+    if constexpr (LA == 2) {
+        const int kk = 8 * fg + tq;
+        const int py = kk / BW, px = kk - (kk / BW) * BW;
+        const int achk = cf * 2 + (tpp >> 1);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int r1 = py * g.hwd + px + tapoff[t];
+            a_lo[t] = r1 * 128 + 16 * (achk ^ wg_swz<128>(r1)) + 8 * (tpp & 1);
+            a_hi[t] = (r1 + 4) * 128 + 16 * (achk ^ wg_swz<128>(r1 + 4)) + 8 * (tpp & 1);
+        }
+        const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
+#pragma unroll
+        for (int ni = 0; ni < NF; ++ni) {
+            const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
+            b_lo[ni] = kk * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d1)) + 8 * (tpp & 1);
+            b_hi[ni] = (kk + 4) * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d2)) + 8 * (tpp & 1);
+        }
+    }
     // per-wave DMA instructions per tile (wave-uniform, tile-independent)
     const int per_tile = h_n + D_INS;
     for (int i = 0; i < NST - 1; ++i)
@@ -165,13 +197,21 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
         else if (allow <= 11) wait_vmcnt<11>();
         else wait_vmcnt<12>();
         lds_barrier();
-        if (t + NST - 1 < t_end) stage_tile(t + NST - 1, buf == 0 ? NST - 1 : buf - 1);
+        if (ABL != 1 && t + NST - 1 < t_end) stage_tile(t + NST - 1, buf == 0 ? NST - 1 : buf - 1);
         const char* Hs = smem + buf * STAGE;
         const char* Ds = Hs + HBUF;
         // flat software pipeline over the 36 (substep, tap) steps of the tile:
         // the A fragment of step s+1 (and the B fragments of the next substep)
         // are read while the MFMAs of step s issue
         auto read_b = [&](int ss, bf16x8* bo) {
+            if constexpr (ABL == 3) {
+#pragma unroll
+                for (int ni = 0; ni < NF; ++ni) {
+                    s16x8 v = {(short)ss, (short)ni, 1, 2, 3, 4, 5, (short)lane};
+                    bo[ni] = __builtin_bit_cast(bf16x8, v);
+                }
+                return;
+            }
             const int kk = ss * 32 + 8 * fg + tq;
             const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
 #pragma unroll
@@ -182,7 +222,7 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 bo[ni] = __builtin_bit_cast(bf16x8, v);
-                if (do_bias) {
+                if (do_bias && ni == cf && ss % g.nbias == ct) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
                         dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
@@ -190,6 +230,10 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             }
         };
         auto read_a = [&](int ss, int tap) {
+            if constexpr (ABL == 3) {
+                s16x8 v = {(short)ss, (short)tap, 1, 2, 3, 4, 5, (short)lane};
+                return __builtin_bit_cast(bf16x8, v);
+            }
             const int kk = ss * 32 + 8 * fg + tq;
             const int py = kk / BW, px = kk - (kk / BW) * BW;
             const int r1 = py * g.hwd + px + tapoff[tap];
@@ -201,6 +245,54 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             return __builtin_bit_cast(bf16x8, v);
         };
         bf16x8 b0[NF], b1[NF];
+        if constexpr (LA == 2) {
+            // flat 36-step pipeline (requires BW = 16 and hwd % 8 == 0, so a
+            // substep = +2 halo rows x hwd keeps every XOR swizzle): all LDS
+            // addresses are per-lane constants + immediates -- no VALU address
+            // math in the loop; A two steps ahead, next B at tap 4.
+            auto rd = [&](unsigned off) {
+                return __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + off));
+            };
+            auto rdd = [&](unsigned off) {
+                return __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + off));
+            };
+            auto fa = [&](int k) {
+                const int ss = k / 9, tap = k - (k / 9) * 9;
+                const unsigned so = (unsigned)ss * (32 / BW) * g.hwd * 128;
+                const s16x4 lo = rd(a_lo[tap] + so), hi = rd(a_hi[tap] + so);
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                return __builtin_bit_cast(bf16x8, v);
+            };
+            auto fb = [&](int ss, bf16x8* bo) {
+#pragma unroll
+                for (int ni = 0; ni < NF; ++ni) {
+                    const s16x4 lo = rdd(b_lo[ni] + ss * 32 * DROWB), hi = rdd(b_hi[ni] + ss * 32 * DROWB);
+                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    bo[ni] = __builtin_bit_cast(bf16x8, v);
+                    if (do_bias && ni == cf && ss % g.nbias == ct) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                    }
+                }
+            };
+            fb(0, b0);
+            bf16x8 ar[3];
+            ar[0] = fa(0);
+            ar[1] = fa(1);
+#pragma unroll
+            for (int k = 0; k < 36; ++k) {
+                const int ss = k / 9, tap = k - (k / 9) * 9;
+                if (k + 2 < 36) ar[(k + 2) % 3] = fa(k + 2);
+                if (tap == 4 && ss + 1 < 4) fb(ss + 1, (ss & 1) ? b0 : b1);
+                bf16x8* bc = (ss & 1) ? b1 : b0;
+#pragma unroll
+                for (int ni = 0; ni < NF; ++ni)
+                    acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[k % 3], bc[ni], acc[tap][ni], 0, 0, 0);
+            }
+            buf = buf == NST - 1 ? 0 : buf + 1;
+            continue;
+        }
         read_b(0, b0);
         bf16x8 a_cur = read_a(0, 0);
         // one substep: 9 taps, A(tap+1) read ahead, next substep's B at tap 4
@@ -212,8 +304,10 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 else if (ss + 1 < 4) a_nxt = read_a(ss + 1, 0);
                 if (tap == 4 && ss + 1 < 4) read_b(ss + 1, bn);
 #pragma unroll
-                for (int ni = 0; ni < NF; ++ni)
-                    acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, bc[ni], acc[tap][ni], 0, 0, 0);
+                for (int ni = 0; ni < NF; ++ni) {
+                    if constexpr (ABL == 2) asm volatile("" ::"v"(a_cur), "v"(bc[ni]));
+                    else acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, bc[ni], acc[tap][ni], 0, 0, 0);
+                }
                 a_cur = a_nxt;
             }
         };
@@ -235,9 +329,10 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
         if (fg == 0) {
 #pragma unroll
             for (int ni = 0; ni < NF; ++ni) {
+                if (ni != cf) continue;
                 const int n = n0 + nh * (NT / 2) + ni * 16 + fr;
                 if (p.partial) {
-                    if (n < p.N) p.partial[((long)split * p.Mp + p.M) * p.N + n] = dsum[ni];
+                    if (n < p.N) p.partial[((long)split * p.Mp + p.M + ct) * p.N + n] = dsum[ni];
                 } else if (n < p.n_valid) {
                     p.dbias[n] = dsum[ni];
                 }
@@ -279,8 +374,11 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     const int nimg = p.P / (p.Ha * p.Wa);
     long best = -1;
     for (int bw : {32, 16}) {
+        if (g_wgrad_la == 2 && bw != 16) continue;
         const int bh = 128 / bw;
-        const int hwd = bw + 2 * p.tsw, hrows = hwd * (bh + 2 * p.tsh);
+        int hwd = bw + 2 * p.tsw;
+        if (g_wgrad_la == 2) hwd = (hwd + 7) & ~7;          // substep row shifts keep the swizzle
+        const int hrows = hwd * (bh + 2 * p.tsh);
         if (hrows > 5 * 64) continue;
         const int tx = (p.Wa + bw - 1) / bw, ty = (p.Ha + bh - 1) / bh;
         const long cost = (long)tx * ty * (128 * 8 + hrows);
@@ -302,21 +400,39 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     splits = (ptiles + tps - 1) / tps;
     wp->g[5] = nct; wp->g[6] = nnt; wp->g[7] = splits; wp->g[8] = tps; wp->g[9] = ptiles;
     wp->splits = splits;
+    wp->nbias = splits > 1 ? std::max(1, std::min(nct, g_wgrad_nbias)) : 1;
     wp->blocks = (long)nout * splits;
     return true;
 }
 
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p) {
-    // +1 slab row for the fused BiasAddGrad
-    return wp.splits > 1 ? (size_t)wp.splits * (p.M + 1) * p.N * sizeof(float) : 0;
+    // + nbias slab rows for the fused BiasAddGrad partials
+    return wp.splits > 1 ? (size_t)wp.splits * (p.M + wp.nbias) * p.N * sizeof(float) : 0;
 }
 
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s) {
     WGGeom g;
     g.tiles_x = wp.g[0]; g.tiles_y = wp.g[1]; g.nimg = wp.g[2]; g.hwd = wp.g[3]; g.hrows = wp.g[4];
     g.nct = wp.g[5]; g.nnt = wp.g[6]; g.splits = wp.g[7]; g.tps = wp.g[8]; g.ptiles = wp.g[9];
+    g.nbias = wp.nbias;
     const dim3 grid((unsigned)wp.blocks), block(512);
     const bool small = g.hrows <= 4 * 64;     // 4 halo pieces -> 3 stages fit
+    if (g_wgrad_abl && wp.nt == 128) {
+        if (wp.bw == 32) {
+            if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 1>), grid, block, 0, s, p, g);
+            if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 2>), grid, block, 0, s, p, g);
+            if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 3>), grid, block, 0, s, p, g);
+        } else {
+            if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 1>), grid, block, 0, s, p, g);
+            if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 2>), grid, block, 0, s, p, g);
+            if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 3>), grid, block, 0, s, p, g);
+        }
+        return;
+    }
+    if (g_wgrad_la == 2 && wp.nt == 128 && wp.bw == 16) {
+        hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 2>), grid, block, 0, s, p, g);
+        return;
+    }
     if (wp.bw == 32) {
         if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4>), grid, block, 0, s, p, g);
         else if (small) hipLaunchKernelGGL((wgrad_halo<32, 64, 3, 4>), grid, block, 0, s, p, g);

@@ -142,20 +142,24 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                "wgrad-nbias4"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
     where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles,
     5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off in 2 so
-    igemm_tn2 stays covered for wide problems)."""
+    igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
+    BiasAddGrad spread over up to 4 channel blocks (extra slab rows)."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
-    ops.set_option("wgrad_halo", 1 if v in (3, 4) else 0)
-    ops.set_option("wgrad_nt", 128 if v == 4 else 64)
+    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6) else 0)
+    ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
+    ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
     yield v
     ops.set_option("tn3", 1)
+    ops.set_option("wgrad_nbias", 1)
     ops.set_option("igemm_tn_variant", 2)
     ops.set_option("wgrad_halo", 1)
     ops.set_option("wgrad_nt", 128)
