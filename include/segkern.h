@@ -107,6 +107,17 @@ int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hw
 int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy,
                           float* dw_f32, float* dbias, void* ws, size_t ws_bytes, void* stream);
 
+/* The same in two halves: _begin runs the filter-gradient kernel (and any
+ * BiasAddGrad it cannot fuse) and leaves its split-K reduction pending in ws,
+ * reporting pending[2] = {splits, slab rows}; _end (same d, dw, dbias, ws)
+ * performs that reduction -- on another stream if the caller orders it after
+ * _begin's (an event), so it overlaps the next layer's input gradient.
+ * pending[0] <= 1: nothing left to do. */
+int seg_conv2d_bwd_filter_begin(const seg_conv_desc* d, const void* x, const void* dy, float* dw_f32,
+                                float* dbias, void* ws, size_t ws_bytes, int* pending, void* stream);
+int seg_conv2d_bwd_filter_end(const seg_conv_desc* d, float* dw_f32, float* dbias, void* ws,
+                              const int* pending, void* stream);
+
 /* ---- conv2d_transpose (Network/model/FCN.py:155, :106; utils.py:272) ---- */
 /* w_rskc: packed filter [R][S][K][C] in `dtype` (TF layout, seg_pack_filter mode 2). */
 int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_rskc,

@@ -110,6 +110,8 @@ SIGNATURES = {
     "seg_conv_workspace": (_Z, [_DP, _I]),
     "seg_tconv_filter_apad": (_I, [_DP]),
     "seg_conv_wgrad_adam_fusable": (_I, [_DP]),
+    "seg_conv2d_bwd_filter_begin": (_I, [_DP, _P, _P, _P, _P, _P, _Z, ctypes.POINTER(_I), _P]),
+    "seg_conv2d_bwd_filter_end": (_I, [_DP, _P, _P, _P, ctypes.POINTER(_I), _P]),
     "seg_softmax": (_I, [_P, _I, _I, _L, _P, _I, _I, _P]),
     "seg_conv2d_bwd_filter_adam": (_I, [_DP, _P, _P, _P, _P, ctypes.POINTER(SegAdamFused), _P, _Z, _P]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),

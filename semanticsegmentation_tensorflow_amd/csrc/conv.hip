@@ -613,6 +613,48 @@ extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, cons
     return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
 }
 
+// Split form of seg_conv2d_bwd_filter: _begin runs the filter-gradient kernel
+// (and any BiasAddGrad it does not fuse) and leaves a split-K reduction
+// pending in `ws` (pending = {splits, slab rows}); _end performs it, on any
+// stream ordered after _begin's, so it can overlap the next layer's work.
+extern "C" int seg_conv2d_bwd_filter_begin(const seg_conv_desc* d, const void* x, const void* dy, float* dw,
+                                           float* dbias, void* ws, size_t ws_bytes, int* pending, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !dy || !dw || !pending) return SEG_EINVAL;
+    TNParams p = conv_bwd_filter_params(d);
+    p.x = x; p.b = dy; p.out = dw; p.dbias = dbias;
+    seg::WgradPlan wp;
+    const bool fuses_bias = seg::smallc_wgrad_ok(p, d->dtype) ||
+                            (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp));
+    if (dbias && !fuses_bias) {          // reduce it now, while the workspace is free
+        st = bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
+        if (st) return st;
+        p.dbias = nullptr;
+    }
+    pending[0] = 1;
+    pending[1] = 0;
+    p.defer = pending;
+    return seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_conv2d_bwd_filter_end(const seg_conv_desc* d, float* dw, float* dbias, void* ws,
+                                         const int* pending, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!dw || !pending) return SEG_EINVAL;
+    if (pending[0] <= 1) return SEG_OK;
+    TNParams p = conv_bwd_filter_params(d);
+    p.out = dw;
+    p.dbias = dbias;
+    p.partial = reinterpret_cast<float*>(ws);
+    p.Mp = pending[1];
+    if (!ws || p.Mp < p.M || (p.Mp > p.M && !dbias)) return SEG_EINVAL;
+    seg::tn_reduce(p, pending[0], (hipStream_t)stream);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
 static bool wgrad_adam_params(const seg_conv_desc* d, TNParams* out) {
     if (check_desc(d) || d->dtype != SEG_BF16 || seg::g_tn_variant != 2) return false;
     TNParams p = conv_bwd_filter_params(d);

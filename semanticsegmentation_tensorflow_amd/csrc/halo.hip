@@ -929,10 +929,10 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {
     }
     if (hp.bn == 256) {
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
-        if (g_nt2_ablate && hp.bw == 16) {
-            if (g_nt2_ablate == 1) hipLaunchKernelGGL((conv_halo2<16, true, 1>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 2) hipLaunchKernelGGL((conv_halo2<16, true, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 3) hipLaunchKernelGGL((conv_halo2<16, true, 3>), grid, dim3(512), 0, s, p, g);
+        if (g_nt2_ablate && hp.bw == 16) {   // diagnostics on the default two-phase schedule
+            if (g_nt2_ablate == 1) hipLaunchKernelGGL((conv_halo2<16, true, 1, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 2) hipLaunchKernelGGL((conv_halo2<16, true, 2, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 3) hipLaunchKernelGGL((conv_halo2<16, true, 3, 2>), grid, dim3(512), 0, s, p, g);
             return;
         }
         if (g_halo_phases == 2) {

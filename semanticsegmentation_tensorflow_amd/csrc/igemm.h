@@ -70,6 +70,9 @@ struct TNParams {
     // slabs then carry it as an extra row M, so slabs hold Mp = M + 1 rows.
     float* dbias;
     int Mp;
+    // non-null: leave a split-K reduction pending (slabs stay in the
+    // workspace) and report {splits, Mp} here instead of reducing
+    int* defer;
     // TF1 Adam fused into the filter-gradient epilogue (igemm_tn3 only; p == null: off)
     struct {
         float *p, *m, *v;      // fp32 master slices indexed like out
@@ -84,6 +87,7 @@ struct TNParams {
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
+void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
 size_t tn_workspace(int M, int N, int P, int dtype);
 void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits);

@@ -803,6 +803,25 @@ static void launch_tn_t(TNParams& p, int gridz, hipStream_t s) {
     hipLaunchKernelGGL((igemm_tn<T, BM, BN>), dim3(tiles, 1, gridz), dim3(256), 0, s, p);
 }
 
+// Split-K tail: reduce the slabs now, or leave them pending (p.defer).
+static void tn_finish(TNParams& p, int splits, hipStream_t s) {
+    if (p.defer) {
+        p.defer[0] = p.partial ? splits : 1;
+        p.defer[1] = p.Mp;
+        p.partial = nullptr;
+        return;
+    }
+    if (!p.partial) return;
+    const long total = (long)p.Mp * (p.N / 4);
+    hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+    p.partial = nullptr;
+}
+
+void tn_reduce(TNParams& p, int splits, hipStream_t s) {
+    const long total = (long)p.Mp * (p.N / 4);
+    hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+}
+
 template <typename T>
 static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
@@ -817,12 +836,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         }
         launch_smallc_wgrad(p, splits, s);
         SEG_CHECK_LAUNCH();
-        if (p.partial) {
-            const long total = (long)p.Mp * (p.N / 4);
-            hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
-            SEG_CHECK_LAUNCH();
-            p.partial = nullptr;
-        }
+        tn_finish(p, splits, s);
+        SEG_CHECK_LAUNCH();
         p.dbias = nullptr;
         return SEG_OK;
     }
@@ -835,12 +850,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         }
         launch_wgrad(p, wp, s);
         SEG_CHECK_LAUNCH();
-        if (p.partial) {
-            const long total = (long)p.Mp * (p.N / 4);
-            hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, wp.splits);
-            SEG_CHECK_LAUNCH();
-            p.partial = nullptr;
-        }
+        tn_finish(p, wp.splits, s);
+        SEG_CHECK_LAUNCH();
         p.dbias = nullptr;                    // done
         return SEG_OK;
     }
@@ -867,12 +878,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     else if (bn == 64) launch_tn_t<T, 128, 64>(p, gridz, s);
     else launch_tn_t<T, 128, 128>(p, gridz, s);
     SEG_CHECK_LAUNCH();
-    if (p.partial) {
-        const long total = (long)p.M * (p.N / 4);
-        hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
-        SEG_CHECK_LAUNCH();
-        p.partial = nullptr;
-    }
+    tn_finish(p, splits, s);
+    SEG_CHECK_LAUNCH();
     return SEG_OK;
 }
 

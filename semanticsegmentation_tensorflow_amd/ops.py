@@ -174,6 +174,29 @@ def conv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None, dbias=None):
     return dw
 
 
+def conv2d_bwd_filter_begin(desc, x, dy, dw, ws_buf, dbias=None, stream=None):
+    """First half of conv2d_bwd_filter: the kernel runs, a split-K reduction
+    is left pending in `ws_buf` (a uint8 device tensor owned by the caller).
+    Returns the token for conv2d_bwd_filter_end."""
+    d = _with_ld(desc, x, dy)
+    pend = (ctypes.c_int * 2)()
+    check(_lib.lib().seg_conv2d_bwd_filter_begin(ctypes.byref(d), ptr(x), ptr(dy), ptr(dw),
+                                                 None if dbias is None else ptr(dbias), ptr(ws_buf),
+                                                 ws_buf.numel(), pend, stream_ptr(stream)),
+          "conv2d_backprop_filter")
+    return d, pend
+
+
+def conv2d_bwd_filter_end(token, dw, ws_buf, dbias=None, stream=None):
+    """Second half: the pending split-K reduction (no-op when there is none)."""
+    d, pend = token
+    if pend[0] <= 1:
+        return dw
+    check(_lib.lib().seg_conv2d_bwd_filter_end(ctypes.byref(d), ptr(dw), None if dbias is None else ptr(dbias),
+                                               ptr(ws_buf), pend, stream_ptr(stream)), "conv2d_backprop_filter")
+    return dw
+
+
 def tconv2d_fwd(desc, x, w_rskc, y, epi=None, ws=None, stream=None):
     d = _with_ld(desc, x, y)
     wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_TFWD))

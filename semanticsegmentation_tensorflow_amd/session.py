@@ -126,6 +126,11 @@ class Session:
         self.fuse_adam = fuse_adam
         self.store_fused_grads = False   # tests: also write the fused layers' gradients
         self._fused = None               # names updated inside backward this step
+        # split-K reductions of filter gradients on a side stream, overlapping
+        # the next layer's input gradient (single process: DP all-reduces need
+        # the reduced gradient on the compute stream)
+        self.defer_wgrad_reduce = True
+        self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
@@ -513,9 +518,13 @@ class Session:
             if c.kind in ("conv", "tconv") or (c.kind == "MaxPool" and n.kp is None):
                 p.mask_fuse.add(id(n))
         p.adam_fusable = set()
+        p.wg_ws = {}                     # per-conv filter-gradient workspace (pending split-K slabs)
         for n in p.nodes:
             if n.kind == "conv" and ops.wgrad_adam_fusable(n.desc):
                 p.adam_fusable.add(id(n))
+            elif n.kind == "conv":
+                p.wg_ws[id(n)] = torch.empty(max(256, ops.conv_workspace(n.desc, ops.OP_BWD_FILTER)),
+                                             dtype=torch.uint8, device=self.device)
         p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
         p.uncovered = [v for v in p.var_names if v not in covered]
         for v in p.uncovered:            # no gradient path: keep the grad slice at 0
@@ -686,12 +695,21 @@ class Session:
             self._fused = None
             if self.fuse_adam and self.dp is None and not self.overlap_optimizer and fresh and p.adam_fusable:
                 self._fused = (opt, gs, set())
+            self._red = None
+            if self.defer_wgrad_reduce and self.dp is None and not self.overlap_optimizer and \
+                    self.device.type == "cuda":
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=self.device)
+                self._red = (self._side, torch.cuda.current_stream(self.device))
             if self.overlap_optimizer and self.device.type == "cuda":
                 # per-layer Adam on a side stream as soon as the layer's gradient is final
                 self._adam_ctx = _AdamOverlap(self, opt, gs)
                 if self.dp is not None:
                     self.dp.on_launch = self._adam_ctx.after_work
             self._backward(p, scal)
+            if self._red is not None:            # pending filter-gradient reductions done before Adam
+                self._red[1].wait_stream(self._red[0])
+                self._red = None
             if self.dp is not None:
                 self.dp.finish()
                 self.dp.on_launch = None
@@ -735,9 +753,10 @@ class Session:
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        fn(*args)
+        r = fn(*args)
         e.record()
         self.timer.append((desc, op, s, e))
+        return r
 
     def _relu_fwd(self, x, y):
         C = x.shape[-1]
@@ -847,6 +866,17 @@ class Session:
                                 store.packed.get((wn, ops.PACK_KRSC)),
                                 store.grad(wn) if self.store_fused_grads else None, fused_db, ws)
                     fdone.add(wn)
+                elif self._red is not None:
+                    # kernel now, its split-K reduction on the side stream
+                    side, main = self._red
+                    gw, wsb = store.grad(n.w.var_name), p.wg_ws[id(n)]
+                    tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc, buf[id(x)],
+                                      dz, gw, wsb, fused_db)
+                    if tok[1][0] > 1:
+                        ev = torch.cuda.Event()
+                        ev.record(main)
+                        side.wait_event(ev)
+                        ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db, stream=side)
                 else:
                     self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
                                 store.grad(n.w.var_name), ws, None, fused_db)

@@ -569,3 +569,40 @@ def test_conv2d_bwd_filter_adam_fused(dev, case):
     assert torch.equal(tk[:K, :, :C], pb.view(R * R, C, K).permute(2, 0, 1))
     if cp > C:
         assert (tk[:, :, C:] == 7.0).all()
+
+
+# (N, H, W, C, K, R): halo filter gradient (split-K, fused bias), first layer
+# (C = 3 -> 8, split-K), generic TN GEMMs (split-K, bias by the fallback)
+SPLIT_WGRAD_CASES = [
+    (2, 24, 40, 64, 128, 3),
+    (2, 19, 131, 3, 48, 3),
+    (1, 6, 9, 512, 264, 7),
+    (2, 6, 9, 40, 24, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", SPLIT_WGRAD_CASES)
+def test_conv2d_bwd_filter_begin_end(dev, case, dtype):
+    """seg_conv2d_bwd_filter_begin + _end (reduction on a second stream) ==
+    seg_conv2d_bwd_filter, gradient and BiasAddGrad bit-for-bit."""
+    N, H, W, C, K, R = case
+    d = ops.conv_desc(N, H, W, C, K, R, R, dtype=DT[dtype])
+    g = torch.Generator().manual_seed(31)
+    x = to_dev(torch.randn(N, H, W, C, generator=g, dtype=torch.float64), dtype, dev)
+    dy = to_dev(torch.randn(N, H, W, K, generator=g, dtype=torch.float64), dtype, dev)
+    ref, rdb = torch.empty(R, R, C, K, device=dev), torch.empty(K, device=dev)
+    ops.conv2d_bwd_filter(d, x, dy, ref, dbias=rdb)
+    out = torch.full((R, R, C, K), float("nan"), device=dev)
+    db = torch.full((K,), float("nan"), device=dev)
+    wsb = torch.empty(max(256, ops.conv_workspace(d, ops.OP_BWD_FILTER)), dtype=torch.uint8, device=dev)
+    tok = ops.conv2d_bwd_filter_begin(d, x, dy, out, wsb, dbias=db)
+    side = torch.cuda.Stream(device=dev)
+    ev = torch.cuda.Event()
+    ev.record()
+    side.wait_event(ev)
+    ops.conv2d_bwd_filter_end(tok, out, wsb, db, stream=side)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(db, rdb)
