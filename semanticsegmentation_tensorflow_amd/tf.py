@@ -6,6 +6,7 @@ else raises NotImplementedError instead of silently running elsewhere.
 """
 from types import SimpleNamespace
 
+from . import checkpoint as _ckpt
 from . import graph as _g
 from .session import Session  # noqa: F401
 
@@ -45,5 +46,7 @@ nn = SimpleNamespace(
 )
 layers = SimpleNamespace(batch_normalization=_g.batch_normalization)
 image = SimpleNamespace(resize_bilinear=_g.resize_bilinear)
-train = SimpleNamespace(AdamOptimizer=_g.AdamOptimizer)
+train = SimpleNamespace(AdamOptimizer=_g.AdamOptimizer, Saver=_ckpt.Saver,
+                        get_checkpoint_state=_ckpt.get_checkpoint_state,
+                        latest_checkpoint=_ckpt.latest_checkpoint)
 compat = SimpleNamespace(v1=SimpleNamespace(train=train, placeholder=placeholder))
