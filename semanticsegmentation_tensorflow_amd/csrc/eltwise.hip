@@ -363,17 +363,24 @@ __global__ void concat_bwd_k(const T* __restrict__ dy, int ldy, ConcatArgs a, co
 template <typename T>
 __global__ void prepare_input_k(const float* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
                                 int WP, int CP) {
-    const long total = (long)N * HP * WP * CP;
+    // one thread per output pixel: its cin fp32 values (contiguous) -> one
+    // 16-byte chunk per 8 channels (zeros in channel / spatial padding)
+    constexpr int EPC = dt_traits<T>::EPC;
+    const long total = (long)N * HP * WP;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % CP);
-        long t = i / CP;
-        const int w = (int)(t % WP);
-        t /= WP;
+        const int w = (int)(i % WP);
+        const long t = i / WP;
         const int h = (int)(t % HP);
         const int n = (int)(t / HP);
-        float v = 0.f;
-        if (c < cin && h < H && w < W) v = img[(((long)n * H + h) * W + w) * cin + c];
-        x[i] = from_f32<T>(v);
+        const bool in = h < H && w < W;
+        const float* src = img + (((long)n * H + (in ? h : 0)) * W + (in ? w : 0)) * cin;
+        T* dst = x + i * CP;
+        for (int c0 = 0; c0 < CP; c0 += EPC) {
+            float v[EPC];
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) v[e] = (in && c0 + e < cin) ? src[c0 + e] : 0.f;
+            *reinterpret_cast<uint4*>(dst + c0) = Chunk<T>::pack(v);
+        }
     }
 }
 
@@ -861,9 +868,9 @@ extern "C" int seg_concat_bwd(const void* dy, int ldy, const seg_concat_part* pa
 
 extern "C" int seg_prepare_input(const float* img, void* x, int N, int H, int W, int cin, int HP, int WP, int CP,
                                  int dtype, void* stream) {
-    if (!img || !x || HP < H || WP < W || CP < cin) return SEG_EINVAL;
+    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_BF16 ? 8 : 4)) return SEG_EINVAL;
     const long total = (long)N * HP * WP * CP;
-    DISPATCH_T(dtype, hipLaunchKernelGGL(prepare_input_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+    DISPATCH_T(dtype, hipLaunchKernelGGL(prepare_input_k<T>, dim3(seg_grid_1d(total / CP + 1, 256)), dim3(256), 0,
                                          (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));
     SEG_CHECK_LAUNCH();
     return SEG_OK;

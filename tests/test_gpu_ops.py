@@ -436,6 +436,20 @@ def test_bn_relu(dev, dtype):
     assert_close(dbt.double().cpu(), beta.grad, torch.float32, "dbeta", 1e-4)
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(2, 5, 7, 3, 8, 8, 8), (1, 4, 4, 8, 4, 6, 8), (1, 3, 5, 11, 4, 5, 16)])
+def test_prepare_input(dev, dtype, shape):
+    """fp32 NHWC image -> zero-padded compute tensor (bit-exact: a cast)."""
+    N, H, W, c, HP, WP, CP = shape
+    img = torch.randn(N, H, W, c, generator=torch.Generator().manual_seed(18))
+    ref = torch.zeros(N, HP, WP, CP)
+    ref[:, :H, :W, :c] = img
+    x = torch.full((N, HP, WP, CP), float("nan"), device=dev, dtype=dtype)
+    ops.prepare_input(img.to(dev), x)
+    torch.cuda.synchronize()
+    assert torch.equal(x.cpu(), ref.to(dtype))
+
+
 def test_resize_bilinear(dev):
     N, H, W, C, OH, OW = 1, 5, 7, 3, 9, 15
     g = torch.Generator().manual_seed(17)
