@@ -479,6 +479,16 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_abl = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "tn3_half")) {
+        if (value < 0 || value > 3) return SEG_EINVAL;
+        seg::g_tn3_half = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn3_adam_abl")) {
+        if (value < 0 || value > 31) return SEG_EINVAL;
+        seg::g_tn3_adam_abl = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "tn3_mfast")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_tn3_mfast = value;
@@ -686,6 +696,7 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.lr_t = (float)lr_t; p.adam.b1 = a->beta1; p.adam.b2 = a->beta2; p.adam.eps = a->eps;
     p.adam.gs = a->grad_scale;
     p.adam.store_grad = dw != nullptr;
+    p.adam.abl = seg::g_tn3_adam_abl;
     p.Mp = p.M;
     p.partial = nullptr;
     seg::launch_tn3(p, 1, (hipStream_t)stream);

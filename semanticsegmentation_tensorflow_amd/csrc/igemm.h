@@ -82,6 +82,7 @@ struct TNParams {
         int tr_ap, RS;
         float lr_t, b1, b2, eps, gs;
         int store_grad;        // also write the gradient to out
+        int abl;               // diagnostics (garbage results): g_tn3_adam_abl bits
     } adam;
 };
 
@@ -108,6 +109,8 @@ void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s);
 extern int g_tn3;
 extern int g_tn3_abl;
 extern int g_tn3_mfast;
+extern int g_tn3_adam_abl;
+extern int g_tn3_half;
 bool tn3_ok(const TNParams& p, int dtype);
 inline bool tn3_applies(int M, int N, int dtype) { return g_tn3 && dtype == SEG_BF16 && M >= 256 && N > 128; }
 void tn3_info(int M, int N, int P, int cus, int* splits);

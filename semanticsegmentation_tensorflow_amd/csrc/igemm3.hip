@@ -357,20 +357,33 @@ __device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((r
 
 int g_tn3 = 1;
 int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
-int g_tn3_mfast = 0;   // tile order: M fastest when the B (dy) panel is the larger operand
+int g_tn3_mfast = 0;
+int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam, 2 for plain single-split
+int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue   // tile order: M fastest when the B (dy) panel is the larger operand
 
 // ABL: see g_tn3_abl.  MFAST: consecutive tiles walk M (share the dy panel).
 // ADAM: TF1 Adam on the parameters of the tile (p.adam) instead of (or besides)
 // storing the gradient -- the filter gradient never round-trips through HBM.
-template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false>
-__global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int tiles_n, int splits) {
+// BN / BKP: 256 / 64 is the one-block-per-CU tile (8 waves, 160 KiB rings);
+// 128 / 32 is the half tile (4 waves, 64 KiB rings + 68 KiB epilogue staging)
+// that runs two blocks per CU, so one block's HBM-bound epilogue (the fused
+// Adam) overlaps the other block's MFMA main loop.
+template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false, int BN = 256, int BKP = 64>
+__global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, int tiles_n, int splits) {
     using T = bf16;
-    constexpr int NW = 8, BM = 256, BN = 256, BKP = 64;
-    constexpr int ROWB = 512, RPI = 1024 / ROWB, CPR = ROWB / 16;   // 2 rows / DMA piece, 32 chunks / row
-    constexpr int A_INS = BKP / RPI / NW, B_INS = BKP / RPI / NW;   // 4 + 4
-    constexpr int WTM = 128, WTN = 64, TN = WTN / 16;
-    constexpr int ABUF = BKP * ROWB, BBUF = BKP * ROWB;             // 32 KiB each
-    __shared__ __attribute__((aligned(16))) char smem[3 * ABUF + 2 * BBUF];
+    constexpr int BM = 256, WTM = 128, WTN = 64, TN = WTN / 16;
+    constexpr int NWN = BN / WTN, NW = 2 * NWN;                      // waves: 2 (M) x NWN (N)
+    constexpr int ROWB = BM * 2, RPI = 1024 / ROWB, CPR = ROWB / 16; // A: 2 rows / DMA piece, 32 chunks / row
+    constexpr int ROWBB = BN * 2, RPIB = 1024 / ROWBB, CPRB = ROWBB / 16;
+    constexpr int A_INS = BKP / RPI / NW, B_INS = BKP / RPIB / NW;
+    constexpr int KS = BKP / 32;
+    constexpr int ABUF = BKP * ROWB, BBUF = BKP * ROWBB;
+    constexpr int RING = 3 * ABUF + 2 * BBUF;
+    constexpr int EPI = ADAM ? NW * (32 * (WTN * 4 + 16) + WTN * (32 * 2 + 16)) : NW * 64 * (WTN * 4 + 16);
+    constexpr int SMEM = RING > EPI ? RING : EPI;
+    static_assert(A_INS * NW * RPI == BKP && B_INS * NW * RPIB == BKP, "DMA pieces must tile the stage");
+    static_assert(NW == 8 || (NW == 4 && BKP == 32), "A-piece row map");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
     typedef short s16x8 __attribute__((ext_vector_type(8)));
 
     const int ntile = tiles_m * tiles_n;
@@ -397,14 +410,20 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w >> 2, wn = w & 3;
+    const int wm = w / NWN, wn = w % NWN;
     const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
     const T* __restrict__ Bm = reinterpret_cast<const T*>(p.b);
     const void* zero = (const void*)g_nt3_zero;
 
-    // lane -> (row of the DMA piece, physical chunk) -> global chunk (swizzle is piece-independent)
+    // first stage row of A piece i (2 rows): the pieces of one wave differ
+    // only in row bits the swizzle ignores (bits 4+ for 8 waves; bits 2 and
+    // 4 for 4 waves), so one swizzled column serves all of them
+    auto arow = [&](int i) {
+        return NW == 8 ? (i * NW + w) * RPI : 2 * (w & 1) + 8 * (w >> 1) + 4 * (i & 1) + 16 * (i >> 1);
+    };
+    // lane -> (row of the DMA piece, physical chunk) -> global chunk
     const int rsub = lane / CPR, pc = lane % CPR;
-    const int row0 = w * RPI + rsub;
+    const int row0 = arow(0) + rsub;
     const int gc = (pc & ~15) | ((pc & 15) ^ tn3_swz(row0));
     // A: column m = m0 + gc*8 .. +7 -> (tap, channel)
     const int am = m0 + gc * 8;
@@ -417,7 +436,7 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
     const int hw = p.Ha * p.Wa;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-        const int pix = kt_begin * BKP + (i * NW) * RPI + row0;
+        const int pix = kt_begin * BKP + arow(i) + rsub;
         pp[i] = pix;
         const int q = pix < p.P ? pix : 0;
         pimg[i] = q / hw;
@@ -425,10 +444,13 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
         pa[i] = rem / p.Wa;
         pb[i] = rem - pa[i] * p.Wa;
     }
-    // B: column n = n0 + gc*8
-    const int bn = n0 + gc * 8;
+    // B: column n = n0 + gcb*8 (B pieces differ by 16 rows: swizzle-invariant)
+    const int rsubb = lane / CPRB, pcb = lane % CPRB;
+    const int rowb0 = w * RPIB + rsubb;
+    const int gcb = (pcb & ~15) | ((pcb & 15) ^ tn3_swz(rowb0));
+    const int bn = n0 + gcb * 8;
     const bool b_nok = bn < p.N;
-    int bpix = kt_begin * BKP + row0;
+    int bpix = kt_begin * BKP + rowb0;
 
     const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
     const unsigned ldsB = lds0 + 3 * ABUF;
@@ -438,7 +460,7 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
             const int ih = pa[i] * p.ish + hoff, iw = pb[i] * p.isw + woff;
             const bool ok = a_mok && pp[i] < p.P && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
             const void* src = ok ? (const void*)(X + (long)pimg[i] * p.x_img + ((long)ih * p.IW + iw) * p.ldx + ac) : zero;
-            glds16(src, lds0 + buf * ABUF + (i * NW + w) * 1024);
+            glds16(src, lds0 + buf * ABUF + arow(i) * ROWB);
             pp[i] += BKP;
             pb[i] += BKP;
             while (pb[i] >= p.Wa) {
@@ -450,7 +472,7 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
     auto issue_b = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {
-            const int pix = bpix + (i * NW) * RPI;
+            const int pix = bpix + (i * NW) * RPIB;
             const bool ok = b_nok && pix < p.P;
             const void* src = ok ? (const void*)(Bm + (long)pix * p.ldb + bn) : zero;
             glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
@@ -483,29 +505,29 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
     for (int it = 0; it < nk; ++it) {
         const char* As = smem + abuf * ABUF;
         const char* Bs = smem + 3 * ABUF + bbuf * BBUF;
-        bf16x8 af[2][4], bq[2][TN];
+        bf16x8 af[KS][4], bq[KS][TN];
         // 16 columns x 32 pixel rows fragment at column `col0`, k rows ks*32 ..
-        auto frag = [&](const char* base, int col0, int ks) {
+        auto frag = [&](const char* base, int rowb, int col0, int ks) {
             const int r1 = ks * 32 + 8 * fg + tq;
             const int chk = (col0 >> 3) + (tpp >> 1);
             const int c1 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1));
             const int c2 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1 + 4));
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + r1 * ROWB + 16 * c1 + 8 * (tpp & 1)));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + (r1 + 4) * ROWB + 16 * c2 + 8 * (tpp & 1)));
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + r1 * rowb + 16 * c1 + 8 * (tpp & 1)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + (r1 + 4) * rowb + 16 * c2 + 8 * (tpp & 1)));
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             return __builtin_bit_cast(bf16x8, v);
         };
         auto read_a = [&](int mh) {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
+            for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi) af[ks][mi] = frag(As, wm * WTM + mh * 64 + mi * 16, ks);
+                for (int mi = 0; mi < 4; ++mi) af[ks][mi] = frag(As, ROWB, wm * WTM + mh * 64 + mi * 16, ks);
         };
         auto mma = [&](int mh) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
+            for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -516,13 +538,13 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
         };
         read_a(0);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, wn * WTN + ni * 16, ks);
+            for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, ROWBB, wn * WTN + ni * 16, ks);
         if (ABL != 1 && it + 1 < nk) issue_b(bbuf ^ 1);
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(0);
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[1][3]), "v"(bq[0][0]), "v"(bq[1][3]) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]), "v"(bq[0][0]), "v"(bq[KS - 1][3]) : "memory");
         __builtin_amdgcn_s_barrier();
         read_a(1);
         const int anext = abuf == 0 ? 2 : abuf - 1;
@@ -534,7 +556,7 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
         }
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(1);
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[1][3]) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]) : "memory");
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
         bbuf ^= 1;
@@ -556,8 +578,13 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
         // epilogue is latency-, not DRAM-page-bound.)
         constexpr int QR = 32, SROWF = WTN * 4 + 16, SROWT = QR * 2 + 16;
         constexpr int WB = QR * SROWF + WTN * SROWT;
-        static_assert(NW * WB <= 3 * ABUF + 2 * BBUF, "fused epilogue staging must fit");
+        static_assert(NW * WB <= SMEM, "fused epilogue staging must fit");
         const auto& A = p.adam;
+        const int abl = A.abl;
+        if (abl & 16) {
+            if (acc[0][0][0] == 12345.f && acc[7][3][3] == 54321.f) p.out[tid] = acc[3][1][2];
+            return;
+        }
         const int fr = lane & 15;
         const int cch = lane & 7, esub = lane >> 3;          // 8 lanes x 8 columns per row, 8 rows per pass
         const int col0 = n0 + wn * WTN + cch * 8;
@@ -587,7 +614,10 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
                 cc[i] = m - tp[i] * p.Cg;
                 ok[i] = m < p.M && cc[i] < p.c_valid && col0 + 8 <= p.n_valid;
                 eo[i] = (long)tp[i] * p.o_tap + (long)cc[i] * p.o_c + col0;
-                if (ok[i]) {
+                if (ok[i] && (abl & 1)) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) pv[i][j] = mv[i][j] = vv[i][j] = 0.f;
+                } else if (ok[i]) {
                     *reinterpret_cast<float4*>(pv[i]) = *reinterpret_cast<const float4*>(A.p + eo[i]);
                     *reinterpret_cast<float4*>(pv[i] + 4) = *reinterpret_cast<const float4*>(A.p + eo[i] + 4);
                     *reinterpret_cast<float4*>(mv[i]) = *reinterpret_cast<const float4*>(A.m + eo[i]);
@@ -613,17 +643,19 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
                         mv[i][j] = mj;
                         vv[i][j] = vj;
                     }
-                    *reinterpret_cast<float4*>(A.p + eo[i]) = *reinterpret_cast<const float4*>(np);
-                    *reinterpret_cast<float4*>(A.p + eo[i] + 4) = *reinterpret_cast<const float4*>(np + 4);
-                    *reinterpret_cast<float4*>(A.m + eo[i]) = *reinterpret_cast<const float4*>(mv[i]);
-                    *reinterpret_cast<float4*>(A.m + eo[i] + 4) = *reinterpret_cast<const float4*>(mv[i] + 4);
-                    *reinterpret_cast<float4*>(A.v + eo[i]) = *reinterpret_cast<const float4*>(vv[i]);
-                    *reinterpret_cast<float4*>(A.v + eo[i] + 4) = *reinterpret_cast<const float4*>(vv[i] + 4);
+                    if (!(abl & 2)) {
+                        *reinterpret_cast<float4*>(A.p + eo[i]) = *reinterpret_cast<const float4*>(np);
+                        *reinterpret_cast<float4*>(A.p + eo[i] + 4) = *reinterpret_cast<const float4*>(np + 4);
+                        *reinterpret_cast<float4*>(A.m + eo[i]) = *reinterpret_cast<const float4*>(mv[i]);
+                        *reinterpret_cast<float4*>(A.m + eo[i] + 4) = *reinterpret_cast<const float4*>(mv[i] + 4);
+                        *reinterpret_cast<float4*>(A.v + eo[i]) = *reinterpret_cast<const float4*>(vv[i]);
+                        *reinterpret_cast<float4*>(A.v + eo[i] + 4) = *reinterpret_cast<const float4*>(vv[i] + 4);
+                    }
                     if (A.store_grad) {
                         *reinterpret_cast<float4*>(p.out + eo[i]) = g0;
                         *reinterpret_cast<float4*>(p.out + eo[i] + 4) = g1;
                     }
-                    if (A.rows)
+                    if (A.rows && !(abl & 4))
                         *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(A.rows) +
                                                   ((long)tp[i] * A.rows_ap + cc[i]) * A.rows_bp + col0) = Chunk<bf16>::pack(np);
                 }
@@ -631,7 +663,7 @@ __global__ __launch_bounds__(512) void igemm_tn3(TNParams p, int tiles_m, int ti
                 for (int j = 0; j < 8; ++j)
                     *reinterpret_cast<bf16*>(tbuf + (cch * 8 + j) * SROWT + rr * 2) = (bf16)np[j];
             }
-            if (A.tr) {
+            if (A.tr && !(abl & 8)) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 const int n = n0 + wn * WTN + lane;              // one transposed row per lane
 #pragma unroll
@@ -717,7 +749,24 @@ void tn3_info(int M, int N, int P, int cus, int* splits) {
 }
 
 void launch_tn3(TNParams& p, int splits, hipStream_t s) {
-    const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256;
+    const int tm = (p.M + 255) / 256;
+    if (splits == 1 && !g_tn3_abl && (g_tn3_half & (p.adam.p ? 1 : 2))) {
+        // 256 x 128 tiles, two blocks per CU
+        const int tn = (p.N + 127) / 128;
+        const dim3 g(tm * tn), b(256);
+        const bool mfast = g_tn3_mfast && tm > tn;
+#define TN3H(MF, AD) hipLaunchKernelGGL((igemm_tn3<true, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
+        if (p.adam.p) {
+            if (mfast) TN3H(true, true);
+            else TN3H(false, true);
+        } else {
+            if (mfast) TN3H(true, false);
+            else TN3H(false, false);
+        }
+#undef TN3H
+        return;
+    }
+    const int tn = (p.N + 255) / 256;
     const dim3 g(tm * tn * splits), b(512);
     const bool mfast = g_tn3_mfast && tm > tn;
 #define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<true, A, MF>), g, b, 0, s, p, tm, tn, splits)

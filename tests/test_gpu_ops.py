@@ -142,22 +142,25 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
-                                                "wgrad-nbias4"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                   "wgrad-nbias4", "tn3-half"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
     where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles,
     5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off in 2 so
     igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
-    BiasAddGrad spread over up to 4 channel blocks (extra slab rows)."""
+    BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5 with
+    the 256x128 two-blocks-per-CU tiles also for plain single-split launches."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
     ops.set_option("wgrad_halo", 1 if v in (3, 4, 6) else 0)
     ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
+    ops.set_option("tn3_half", 3 if v == 7 else 1)
     yield v
+    ops.set_option("tn3_half", 1)
     ops.set_option("tn3", 1)
     ops.set_option("wgrad_nbias", 1)
     ops.set_option("igemm_tn_variant", 2)
@@ -533,11 +536,19 @@ ADAM_FUSED_CASES = [
     (1, 5, 7, 40, 264, 7),      # conv6-like 7x7; K tail of the 256-wide tile
     (1, 5, 7, 36, 264, 7),      # c_valid = 36 < Cg = 40: padding rows of the packed copies untouched
     (2, 6, 9, 512, 512, 1),     # conv7-like 1x1
+    (2, 11, 13, 256, 392, 1),   # 9 pixel stages of 32, N tail of the 128-wide half tile
 ]
 
 
+@pytest.fixture(params=[1, 0], ids=["half-tiles", "full-tiles"])
+def adam_tiles(request, dev):
+    ops.set_option("tn3_half", request.param)
+    yield request.param
+    ops.set_option("tn3_half", 1)
+
+
 @pytest.mark.parametrize("case", ADAM_FUSED_CASES)
-def test_conv2d_bwd_filter_adam_fused(dev, case):
+def test_conv2d_bwd_filter_adam_fused(dev, case, adam_tiles):
     """seg_conv2d_bwd_filter_adam == Conv2DBackpropFilter, then TF1 Adam
     (FCN.py:338) on the filter, then repacking of the HWIO / KRSC copies."""
     N, H, W, C, K, R = case
