@@ -53,6 +53,7 @@ def parse():
                     help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-miou", action="store_true", help="skip the mIoU parity probe")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the KITTI data-pipeline rate probe")
     ap.add_argument("--no-fuse-adam", action="store_true",
                     help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
     ap.add_argument("--overlap-optimizer", action="store_true",
@@ -160,6 +161,59 @@ def miou_parity(sess, pred, image, keep, img, lab, H, W, model):
                 "image0_class_map_agreement": round(agree, 6),
                 "oracle": f"oracle FCN forward, float64 (bf16 rounding points), {dt:.1f} s"})
     return out
+
+
+def pipeline_rate(H, W, device, threads=16, seconds=2.0):
+    """KITTI input pipeline (gen_batch_function, FCN.py:235-307) rates on this
+    box: native PNG decode of 375x1242 RGBA merge + RGB gt files on `threads`
+    host threads, and the GPU augmentation (3 samples per file: bc_img
+    original, crop, flip; PIL-exact bilinear resize to HxW; labels)."""
+    import io
+    import random
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    import torch
+    from PIL import Image
+
+    from semanticsegmentation_tensorflow_amd import data
+    rng = np.random.default_rng(7)
+    yy, xx = np.mgrid[0:375, 0:1242]
+    img = np.stack([(xx * 0.2 + yy * 0.3) % 256, (xx * 0.1) % 256, (yy * 0.5) % 256, np.full_like(xx, 255)], -1)
+    img = (img + rng.integers(-8, 8, img.shape)).clip(0, 255).astype(np.uint8)
+    gt = np.zeros((375, 1242, 3), np.uint8)
+    gt[:] = (255, 0, 0)
+    gt[220:, 300:900] = (255, 0, 255)
+    pngs = []
+    for a, mode in ((img, "RGBA"), (gt, "RGB")):
+        b = io.BytesIO()
+        Image.fromarray(a, mode).save(b, "PNG")
+        pngs.append(b.getvalue())
+    pair = lambda _: (data.png_decode(pngs[0]), data.png_decode(pngs[1]))   # noqa: E731
+    n = 0
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(pair, range(threads)))
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(pair, range(4 * threads)))
+            n += 4 * threads
+        files_per_s = n / (time.perf_counter() - t0)
+    dec = [(torch.from_numpy(img).to(device), torch.from_numpy(gt).to(device)) for _ in range(4)]
+    r = random.Random(1)
+    data.augment_batch(dec, (H, W), r, device)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    s.record()
+    for _ in range(reps):
+        data.augment_batch(dec, (H, W), r, device)
+    e.record()
+    torch.cuda.synchronize()
+    aug = 12 * reps / (s.elapsed_time(e) * 1e-3)
+    return {"host_decode_files_per_s": round(files_per_s, 1), "host_threads": threads,
+            "gpu_augment_samples_per_s": round(aug, 1), "samples_per_file": 3,
+            "sustained_samples_per_s": round(min(3 * files_per_s, aug), 1),
+            "note": f"375x1242 RGBA merge + RGB gt PNG pairs -> {H}x{W} samples + labels"}
 
 
 def kernel_symbol(name):
@@ -389,10 +443,16 @@ def main():
         "loss_after": round(loss_val, 5),
         "miou_parity": miou,
     }
+    if rank == 0 and world == 1 and not args.no_pipeline and args.model == "fcn":
+        try:
+            result["data_pipeline"] = pipeline_rate(H, W, device)
+        except Exception as exc:  # report, never crash the headline line
+            result["data_pipeline"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_traffic:
         try:
             argv = [a for a in sys.argv[1:] if a not in ("--kernel-table",)]
-            argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-miou"]
+            argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-miou",
+                           "--no-pipeline"]
             t = pmc_traffic(argv, kernel_symbol(dname), os.path.join(ROOT, "gpurun_out", "bench_pmc"))
             result["roofline"]["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
             result["roofline"]["traffic_detail"] = {

@@ -236,6 +236,44 @@ int seg_copy_channels(const void* x, int ldx, void* y, int ldy, long P, int C, i
  * to [N, HP, WP, CP] with zeros (SURVEY.md 0-3 pad policy). */
 int seg_prepare_input(const float* img, void* x, int N, int H, int W, int c_in, int HP, int WP,
                       int CP, int dtype, void* stream);
+/* Same from uint8 images (the decoded / augmented batch as the reference
+ * feeds it: feed_dict uint8 arrays into the float32 placeholder). */
+int seg_prepare_input_u8(const uint8_t* img, void* x, int N, int H, int W, int c_in, int HP, int WP,
+                         int CP, int dtype, void* stream);
+
+/* ---- host PNG decode (scipy.misc.imread of merge/ and gt_image_2/ PNGs,
+ * FCN.py:267-268).  8-bit grey / grey+alpha / RGB / RGBA, non-interlaced;
+ * other PNGs return SEG_EINVAL (decode those another way).  Host memory
+ * only; thread-safe, no GPU work. */
+int seg_png_info(const void* png, size_t n, int* h, int* w, int* channels);
+/* out = uint8 [h][w][channels] (out_bytes >= h * w * channels). */
+int seg_png_decode(const void* png, size_t n, void* out, size_t out_bytes);
+
+/* ---- training-data augmentation (gen_batch_function, FCN.py:235-307) ----
+ * One view = one training sample cut from a decoded uint8 image in device
+ * memory: the window [y0, y0+h) x [x0, x0+w) of src [H0][W0][C]
+ * (crop_image, FCN.py:176-182; the whole image otherwise), optionally
+ * mirrored along x (flip_image, :184-185), resized to OH x OW exactly as
+ * scipy.misc.imresize(..., 'bilinear') = PIL Image.resize(BILINEAR) does
+ * (antialiased two-pass 8-bit resample; RGBA premultiplied), then, if bc,
+ * bc_img(img, contrast, bright) (:187-193). */
+typedef struct seg_aug_view {
+    const void* src;
+    int H0, W0;
+    int x0, y0, w, h;
+    int flip;
+    int bc;
+    int bright;
+    double contrast;
+} seg_aug_view;
+/* labels = 0: out = uint8 [nviews][OH][OW][C] images (C = 3 RGB or 4 RGBA).
+ * labels = 1: src are ground-truth colour images (C = 3); out = uint8
+ * [nviews][OH][OW] class index of process_gt_image (:195-201): 0 where the
+ * resized pixel is exactly (255, 0, 0) (background), else 1.
+ * Downscale factors up to 8 per axis; a window outside its source or a larger
+ * downscale returns SEG_ESHAPE. */
+int seg_augment(const seg_aug_view* views, int nviews, int C, int OH, int OW, int labels, void* out,
+                void* stream);
 
 /* ---- loss / prediction (FCN.py:334, :111) ------------------------------- */
 /* Per pixel over the valid region (h < valid_h, w < valid_w) of

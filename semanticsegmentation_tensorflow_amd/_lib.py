@@ -18,7 +18,9 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip"]
+HOST_SOURCES = ["pngdec.cpp"]          # host-only C++ (g++), linked into the same library
+HOST_LIBS = ["-lz"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
@@ -42,22 +44,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src):
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        o = os.path.join(BUILD_DIR, os.path.splitext(src)[0] + ".o")
         if (not force and _newer(s, o) and os.path.getmtime(o) >= newest_header):
             return o
-        cmd = [HIPCC, *CFLAGS, "-c", s, "-o", o]
+        if src in HOST_SOURCES:
+            cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o]
+        else:
+            cmd = [HIPCC, *CFLAGS, "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise SegKernelError(f"hipcc failed for {src}:\n{r.stderr}")
+            raise SegKernelError(f"{cmd[0]} failed for {src}:\n{r.stderr}")
         return o
 
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
+        objs = list(ex.map(compile_one, SOURCES + HOST_SOURCES))
     if force or not os.path.exists(LIB_PATH) or any(
             os.path.getmtime(o) > os.path.getmtime(LIB_PATH) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs, *HOST_LIBS]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise SegKernelError(f"link failed:\n{r.stderr}")
@@ -79,6 +84,12 @@ class SegEpilogue(ctypes.Structure):
                 ("residual", ctypes.c_void_p), ("ld_residual", ctypes.c_int), ("relu", ctypes.c_int),
                 ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64), ("relu_mask", ctypes.c_void_p),
                 ("ld_relu_mask", ctypes.c_int), ("mask_scale", ctypes.c_float)]
+
+
+class SegAugView(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("H0", ctypes.c_int), ("W0", ctypes.c_int), ("x0", ctypes.c_int),
+                ("y0", ctypes.c_int), ("w", ctypes.c_int), ("h", ctypes.c_int), ("flip", ctypes.c_int),
+                ("bc", ctypes.c_int), ("bright", ctypes.c_int), ("contrast", ctypes.c_double)]
 
 
 class SegAdamFused(ctypes.Structure):
@@ -134,6 +145,10 @@ SIGNATURES = {
     "seg_resize_bilinear_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_copy_channels": (_I, [_P, _I, _P, _I, _L, _I, _I, _P]),
     "seg_prepare_input": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_prepare_input_u8": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_png_info": (_I, [_P, _Z, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "seg_png_decode": (_I, [_P, _Z, _P, _Z]),
+    "seg_augment": (_I, [ctypes.POINTER(SegAugView), _I, _I, _I, _I, _I, _P, _P]),
     "seg_softmax_xent_fwd_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I, _P,
                                       _Z, _P]),
     "seg_xent_workspace": (_Z, [_I, _I, _I]),

@@ -360,8 +360,8 @@ __global__ void concat_bwd_k(const T* __restrict__ dy, int ldy, ConcatArgs a, co
     }
 }
 
-template <typename T>
-__global__ void prepare_input_k(const float* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
+template <typename T, typename S = float>
+__global__ void prepare_input_k(const S* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
                                 int WP, int CP) {
     // one thread per output pixel: its cin fp32 values (contiguous) -> one
     // 16-byte chunk per 8 channels (zeros in channel / spatial padding)
@@ -373,12 +373,12 @@ __global__ void prepare_input_k(const float* __restrict__ img, T* __restrict__ x
         const int h = (int)(t % HP);
         const int n = (int)(t / HP);
         const bool in = h < H && w < W;
-        const float* src = img + (((long)n * H + (in ? h : 0)) * W + (in ? w : 0)) * cin;
+        const S* src = img + (((long)n * H + (in ? h : 0)) * W + (in ? w : 0)) * cin;
         T* dst = x + i * CP;
         for (int c0 = 0; c0 < CP; c0 += EPC) {
             float v[EPC];
 #pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] = (in && c0 + e < cin) ? src[c0 + e] : 0.f;
+            for (int e = 0; e < EPC; ++e) v[e] = (in && c0 + e < cin) ? (float)src[c0 + e] : 0.f;
             *reinterpret_cast<uint4*>(dst + c0) = Chunk<T>::pack(v);
         }
     }
@@ -872,6 +872,16 @@ extern "C" int seg_prepare_input(const float* img, void* x, int N, int H, int W,
     const long total = (long)N * HP * WP * CP;
     DISPATCH_T(dtype, hipLaunchKernelGGL(prepare_input_k<T>, dim3(seg_grid_1d(total / CP + 1, 256)), dim3(256), 0,
                                          (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_prepare_input_u8(const uint8_t* img, void* x, int N, int H, int W, int cin, int HP, int WP, int CP,
+                                    int dtype, void* stream) {
+    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_BF16 ? 8 : 4)) return SEG_EINVAL;
+    const long total = (long)N * HP * WP * CP;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((prepare_input_k<T, uint8_t>), dim3(seg_grid_1d(total / CP + 1, 256)),
+                                         dim3(256), 0, (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

@@ -415,13 +415,34 @@ def copy_channels(x, y, stream=None):
     return y
 
 
-def prepare_input(img_f32, x, stream=None):
-    """fp32 [N,H,W,c] -> padded compute tensor x [N,HP,WP,CP] (zeros outside)."""
-    N, H, W, c = img_f32.shape
+def prepare_input(img, x, stream=None):
+    """fp32 or uint8 [N,H,W,c] -> padded compute tensor x [N,HP,WP,CP] (zeros outside)."""
+    N, H, W, c = img.shape
     _, HP, WP, CP = x.shape
-    check(_lib.lib().seg_prepare_input(ptr(img_f32), ptr(x), N, H, W, c, HP, WP, CP, seg_dtype(x),
-                                       stream_ptr(stream)), "prepare_input")
+    fn = _lib.lib().seg_prepare_input_u8 if img.dtype == torch.uint8 else _lib.lib().seg_prepare_input
+    if img.dtype not in (torch.uint8, torch.float32):
+        raise ValueError(f"prepare_input: unsupported image dtype {img.dtype}")
+    check(fn(ptr(img), ptr(x), N, H, W, c, HP, WP, CP, seg_dtype(x), stream_ptr(stream)), "prepare_input")
     return x
+
+
+def augment(views, C, OH, OW, out, labels=False, stream=None):
+    """seg_augment: `views` = [(src uint8 [H0,W0,C] device tensor, (y0, x0, h, w),
+    flip, bc, contrast, bright)], out uint8 [n,OH,OW,C] (or [n,OH,OW] labels)."""
+    n = len(views)
+    arr = (_lib.SegAugView * max(n, 1))()
+    for i, (src, (y0, x0, h, w), flip, bc, contrast, bright) in enumerate(views):
+        if src.dtype != torch.uint8 or src.dim() != 3 or src.shape[2] != C or not src.is_contiguous():
+            raise ValueError("augment: sources must be contiguous uint8 [H, W, C]")
+        a = arr[i]
+        a.src, a.H0, a.W0 = src.data_ptr(), src.shape[0], src.shape[1]
+        a.x0, a.y0, a.w, a.h = x0, y0, w, h
+        a.flip, a.bc, a.contrast, a.bright = int(flip), int(bc), float(contrast), int(bright)
+    want = (n, OH, OW) if labels else (n, OH, OW, C)
+    if tuple(out.shape) != want or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError(f"augment: out must be contiguous uint8 {want}")
+    check(_lib.lib().seg_augment(arr, n, C, OH, OW, int(labels), ptr(out), stream_ptr(stream)), "augment")
+    return out
 
 
 def softmax_xent(logits, labels, dlogits, loss_sum, num_classes, valid_hw=None, grad_scale=1.0,

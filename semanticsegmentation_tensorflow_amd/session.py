@@ -595,6 +595,10 @@ class Session:
                 scal[tid] = float(v)
                 continue
             src = _np(v)
+            if kind == "image" and src.is_cuda and src.dtype == torch.uint8 and src.is_contiguous() \
+                    and src.shape == stage.shape:
+                ops.prepare_input(src, p.buf[tid])   # augmented uint8 batch resident in HBM
+                continue
             if src.is_cuda and src.dtype == stage.dtype and src.is_contiguous() and src.shape == stage.shape:
                 src_dev = src                      # resident in HBM: no copy
             else:
