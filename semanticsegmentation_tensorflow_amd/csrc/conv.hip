@@ -479,6 +479,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_abl = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "tn3_stagger_us")) {
+        if (value < 0 || value > 1000) return SEG_EINVAL;
+        seg::g_tn3_stagger_us = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "tn3_half")) {
         if (value < 0 || value > 3) return SEG_EINVAL;
         seg::g_tn3_half = value;

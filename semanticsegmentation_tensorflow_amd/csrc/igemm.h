@@ -83,6 +83,9 @@ struct TNParams {
         float lr_t, b1, b2, eps, gs;
         int store_grad;        // also write the gradient to out
         int abl;               // diagnostics (garbage results): g_tn3_adam_abl bits
+        int stagger;           // half tiles: second block per CU starts this many 10 ns ticks late
+        int first_round;       // blocks of the first dispatch round (2 per CU)
+        int* cu_slots;         // per-CU arrival counters (zeroed per launch)
     } adam;
 };
 
@@ -111,6 +114,7 @@ extern int g_tn3_abl;
 extern int g_tn3_mfast;
 extern int g_tn3_adam_abl;
 extern int g_tn3_half;
+extern int g_tn3_stagger_us;
 bool tn3_ok(const TNParams& p, int dtype);
 inline bool tn3_applies(int M, int N, int dtype) { return g_tn3 && dtype == SEG_BF16 && M >= 256 && N > 128; }
 void tn3_info(int M, int N, int P, int cus, int* splits);

@@ -359,6 +359,8 @@ int g_tn3 = 1;
 int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
 int g_tn3_mfast = 0;
 int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam, 2 for plain single-split
+int g_tn3_stagger_us = 40;  // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
+__device__ int g_tn3_cu_slots[4096];
 int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue   // tile order: M fastest when the B (dy) panel is the larger operand
 
 // ABL: see g_tn3_abl.  MFAST: consecutive tiles walk M (share the dy panel).
@@ -386,6 +388,26 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     typedef short s16x8 __attribute__((ext_vector_type(8)));
 
+    if constexpr (ADAM && BN == 128) {
+        // The two blocks resident on a CU start together and would stay in
+        // lock step (both in the MFMA loop, then both in the HBM-bound
+        // update).  The second arrival on each CU in the first round starts
+        // late, seeding the alternation main loop <-> update across the pair.
+        if (p.adam.stagger > 0 && (int)blockIdx.x < p.adam.first_round) {
+            __shared__ int late;
+            if (threadIdx.x == 0) {
+                const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_ID
+                const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // XCC_ID
+                const int cu = (int)(((xcc & 15u) << 8) | ((hw >> 8) & 255u));
+                late = atomicAdd(&p.adam.cu_slots[cu], 1) & 1;
+            }
+            __syncthreads();
+            if (late) {
+                const unsigned long long t0 = wall_clock64();
+                while (wall_clock64() - t0 < (unsigned long long)p.adam.stagger) __builtin_amdgcn_s_sleep(16);
+            }
+        }
+    }
     const int ntile = tiles_m * tiles_n;
     const int wg = xcd_remap2(blockIdx.x, gridDim.x);
     const int split = wg / ntile;
@@ -755,6 +777,16 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s) {
         const int tn = (p.N + 127) / 128;
         const dim3 g(tm * tn), b(256);
         const bool mfast = g_tn3_mfast && tm > tn;
+        if (p.adam.p && g_tn3_stagger_us > 0 && tm * tn > 4 * device_cus()) {
+            static int* slots = nullptr;
+            if (!slots) (void)hipGetSymbolAddress((void**)&slots, HIP_SYMBOL(g_tn3_cu_slots));
+            (void)hipMemsetAsync(slots, 0, sizeof(int) * 4096, s);
+            p.adam.cu_slots = slots;
+            p.adam.stagger = g_tn3_stagger_us * 100;
+            p.adam.first_round = 2 * device_cus();
+        } else {
+            p.adam.stagger = 0;
+        }
 #define TN3H(MF, AD) hipLaunchKernelGGL((igemm_tn3<true, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
         if (p.adam.p) {
             if (mfast) TN3H(true, true);

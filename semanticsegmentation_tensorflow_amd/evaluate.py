@@ -3,9 +3,10 @@ mask, Network/utils/utils.py:43-92) plus the mIoU evaluator the reference
 lacks, computed on the GPU from the model's class map.
 
 The reference reads PNGs from data_road/ and resizes them on the host
-(scipy.misc, Network/utils/utils.py:71-83); file I/O is out of scope here, so
-the helpers take decoded image arrays already shaped like the graph's image
-placeholder."""
+(scipy.misc, Network/model/FCN.py:213-233, Network/utils/utils.py:71-83);
+`gen_test_output_files` does the same from a data folder with the native
+PNG decoder and the PIL-exact GPU resize (data.py); `gen_test_output` takes
+decoded arrays already shaped like the graph's image placeholder."""
 from __future__ import annotations
 
 import time
@@ -41,6 +42,28 @@ def gen_test_output(sess, softmax, keep_prob, image_pl, images, image_shape):
         sm = sess.run(softmax, feed_dict=_feed(image_pl, np.asarray(img, np.float32)[None], keep_prob))
         processing_time = time.time() - start
         yield i, paste_mask(sm[0], image_shape), sm[0], processing_time
+
+
+def gen_test_output_files(sess, softmax, keep_prob, image_pl, data_folder, image_shape):
+    """Network/model/FCN.py:213-233: for each `merge/*.png` of data_folder,
+    imread + imresize(image, image_shape) (on the GPU, bit-exact with
+    scipy.misc/PIL), softmax, road mask; yields (basename, RGBA mask,
+    resized image uint8 [h,w,C], processing seconds)."""
+    import glob
+    import os
+
+    from . import data
+    oh, ow = image_shape
+    for path in sorted(glob.glob(os.path.join(data_folder, "merge", "*.png"))):
+        start = time.time()
+        img = data.imread(path)
+        src = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+        C = img.shape[2]
+        out = torch.empty((1, oh, ow, C), dtype=torch.uint8, device=src.device)
+        ops.augment([(src, (0, 0, img.shape[0], img.shape[1]), False, False, 1.0, 0)], C, oh, ow, out)
+        sm = sess.run(softmax, feed_dict=_feed(image_pl, out, keep_prob))
+        processing_time = time.time() - start
+        yield os.path.basename(path), paste_mask(sm[0], image_shape), out[0].cpu().numpy(), processing_time
 
 
 def confusion_to_iou(conf):

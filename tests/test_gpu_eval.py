@@ -90,3 +90,35 @@ def test_resize_bilinear_in_training_graph(dev):
         gg = sess.store.grad(k).cpu().numpy()
         ref = v.grad.numpy()
         assert np.abs(gg - ref).max() <= 2e-3 * np.abs(ref).max(), k
+
+
+def test_gen_test_output_files_and_uint8_feed(dev, tmp_path):
+    """FCN.py:213-233 from a data folder: PNG -> GPU imresize (PIL-exact) ->
+    softmax mask; the uint8 device batch feeds the float32 image placeholder
+    exactly like the same values fed as float32."""
+    from PIL import Image
+    from oracle import augment as A
+    H, W = 64, 96
+    rng = np.random.default_rng(12)
+    (tmp_path / "merge").mkdir()
+    srcs = []
+    for i in range(2):
+        a = rng.integers(0, 256, (75, 124, 3), dtype=np.uint8)
+        Image.fromarray(a, "RGB").save(tmp_path / "merge" / f"um_00000{i}.png")
+        srcs.append(a)
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, H, W, 3], name="input_image")
+    keep = tf.placeholder(tf.float32, name="keep_probability")
+    pred, logits = FCN(image, keep, 2).create()
+    sm = tf.nn.softmax(logits)
+    sess = tf.Session(compute_dtype="f32")
+    sess.run(tf.global_variables_initializer())
+    outs = list(E.gen_test_output_files(sess, sm, keep, image, str(tmp_path), (H, W)))
+    assert [o[0] for o in outs] == ["um_000000.png", "um_000001.png"]
+    for (name, mask, resized, _), a in zip(outs, srcs):
+        want = A.imresize(a, (H, W))
+        assert np.array_equal(resized, want)
+        p32 = sess.run(sm, feed_dict={image: want[None].astype(np.float32), keep: 1.0})
+        assert np.array_equal(mask[..., 1] == 255, p32[0, ..., 1] > 0.5)
+        p8 = sess.run(sm, feed_dict={image: torch.from_numpy(want[None].copy()).to(dev), keep: 1.0})
+        assert np.array_equal(p8, p32)

@@ -12,6 +12,7 @@ dev = torch.device("cuda:0")
 ws = ops.Workspace(dev)
 SHAPES = [("conv6", 12, 39, 512, 4096, 7), ("conv7", 12, 39, 4096, 4096, 1)]
 HALF = [int(h) for h in os.environ.get("PROBE_HALF", "1").split(",")]
+STAG = [int(h) for h in os.environ.get("PROBE_STAGGER", "0").split(",")]
 ABL = [0, 1, 2, 3, 4, 8, 12, 16]
 ABL = [int(a) for a in os.environ.get("PROBE_ABL", ",".join(map(str, ABL))).split(",")]
 
@@ -44,11 +45,14 @@ for name, H, W, C, K, R in SHAPES:
         t = min(timeit(lambda: ops.conv2d_bwd_filter(d, x, dy, dw, ws)) for _ in range(3))
         print(f"{name} half={h} grad-only  {t * 1e3:8.1f} us {gf / t:7.1f} TF/s", flush=True)
         for a in ABL:
-            ops.set_option("tn3_adam_abl", a)
-            t = min(timeit(lambda: ops.conv2d_bwd_filter_adam(d, x, dy, p, m, v, 1e-4, 3, rows=(rows, cp, kp),
-                                                              tr=(tr, cp, kp), ws=ws)) for _ in range(3))
-            print(f"{name} half={h} adam abl={a:2d} {t * 1e3:8.1f} us  ({28 * n / t / 1e9:6.2f} TB/s at 28 B/param)",
-                  flush=True)
+            for sg in STAG:
+                ops.set_option("tn3_adam_abl", a)
+                ops.set_option("tn3_stagger_us", sg)
+                t = min(timeit(lambda: ops.conv2d_bwd_filter_adam(d, x, dy, p, m, v, 1e-4, 3, rows=(rows, cp, kp),
+                                                                  tr=(tr, cp, kp), ws=ws)) for _ in range(3))
+                print(f"{name} half={h} adam abl={a:2d} stagger={sg:3d}us {t * 1e3:8.1f} us "
+                      f"({28 * n / t / 1e9:6.2f} TB/s at 28 B/param)", flush=True)
+        ops.set_option("tn3_stagger_us", 0)
     ops.set_option("tn3_adam_abl", 0)
     big = torch.empty(n * 6, device=dev)
     t = min(timeit(lambda: big[: n * 3].copy_(big[n * 3:])) for _ in range(3))
