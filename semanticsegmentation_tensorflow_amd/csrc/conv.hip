@@ -479,13 +479,18 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_abl = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "nt3_fill")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_nt3_fill = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "tn3_stagger_us")) {
         if (value < 0 || value > 1000) return SEG_EINVAL;
         seg::g_tn3_stagger_us = value;
         return SEG_OK;
     }
     if (!strcmp(name, "tn3_half")) {
-        if (value < 0 || value > 3) return SEG_EINVAL;
+        if (value < 0 || value > 7) return SEG_EINVAL;
         seg::g_tn3_half = value;
         return SEG_OK;
     }

@@ -661,6 +661,21 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
+int g_nt3_fill = 1;
+
+// 256x256 tiles only when the launch (tiles x splits x phases) fills at least
+// half the CUs; narrow problems (phased conv2d_transpose, K <= 6 k-tiles) run
+// more, smaller blocks on igemm_nt2 instead.
+static bool nt3_pick(const NTParams& p, int nphases, int max_m) {
+    if (!nt3_ok(p, SEG_BF16)) return false;
+    if (!g_nt3_fill) return true;
+    int s3;
+    nt3_info(max_m, p.N, p.K, num_cus(), &s3);
+    if (nphases > 1) s3 = 1;
+    const long blocks = (long)((max_m + 255) / 256) * ((p.N + 255) / 256) * s3 * nphases;
+    return blocks * 2 >= num_cus();
+}
+
 template <typename T, int BM, int BN>
 static void launch_nt_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -696,7 +711,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         }
         return SEG_OK;
     }
-    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_ok(p, SEG_BF16);
+    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m);
     if (nt3) {
         nt3_info(max_m, p.N, p.K, num_cus(), &splits);
         if (nphases > 1) splits = 1;
@@ -739,7 +754,7 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
         *bm = 256; *bn = hp.bn; *splits = hp.splits;
         return "conv_halo";
     }
-    if (dtype == SEG_BF16 && g_nt_variant == 2 && nt3_ok(p, SEG_BF16)) {
+    if (dtype == SEG_BF16 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m)) {
         nt3_info(max_m, p.N, p.K, num_cus(), splits);
         if (nphases > 1) *splits = 1;
         *bm = *bn = 256;

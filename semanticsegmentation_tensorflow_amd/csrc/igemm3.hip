@@ -358,7 +358,7 @@ __device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((r
 int g_tn3 = 1;
 int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
 int g_tn3_mfast = 0;
-int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam, 2 for plain single-split
+int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split
 int g_tn3_stagger_us = 40;  // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
 __device__ int g_tn3_cu_slots[4096];
 int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue   // tile order: M fastest when the B (dy) panel is the larger operand
@@ -772,7 +772,8 @@ void tn3_info(int M, int N, int P, int cus, int* splits) {
 
 void launch_tn3(TNParams& p, int splits, hipStream_t s) {
     const int tm = (p.M + 255) / 256;
-    if (splits == 1 && !g_tn3_abl && (g_tn3_half & (p.adam.p ? 1 : 2))) {
+    const bool multi_round = (long)tm * ((p.N + 255) / 256) > device_cus();
+    if (splits == 1 && !g_tn3_abl && (g_tn3_half & (p.adam.p ? 1 : 2)) && (multi_round || !p.adam.p || (g_tn3_half & 4))) {
         // 256 x 128 tiles, two blocks per CU
         const int tn = (p.N + 127) / 128;
         const dim3 g(tm * tn), b(256);

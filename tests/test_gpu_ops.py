@@ -26,8 +26,9 @@ def ntv(request, dev):
     4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
     stagger (two-phase schedule), 6 = 3 with four phases per iteration,
     7 = 3 with the two-phase kernel also for N <= 128 (off by default),
-    8 = 2 with the 256x256-tile GEMM (igemm_nt3) for N > 128 (on by default;
-    variant 2 keeps it off so igemm_nt2 stays covered for wide N)."""
+    8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
+    (by default only where its grid fills half the CUs; variant 2 keeps it
+    off so igemm_nt2 stays covered for wide N)."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
     ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
@@ -36,7 +37,9 @@ def ntv(request, dev):
     ops.set_option("halo_stagger", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
+    ops.set_option("nt3_fill", 0 if v == 8 else 1)   # small test problems: force the 256x256 tiles
     yield v
+    ops.set_option("nt3_fill", 1)
     ops.set_option("igemm_nt_variant", 2)
     ops.set_option("nt_halo", 1)
     ops.set_option("nt3", 1)
@@ -158,7 +161,7 @@ def tnv(request, dev):
     ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
-    ops.set_option("tn3_half", 3 if v == 7 else 1)
+    ops.set_option("tn3_half", 7 if v == 7 else 1)
     yield v
     ops.set_option("tn3_half", 1)
     ops.set_option("tn3", 1)
@@ -540,7 +543,7 @@ ADAM_FUSED_CASES = [
 ]
 
 
-@pytest.fixture(params=[1, 0], ids=["half-tiles", "full-tiles"])
+@pytest.fixture(params=[5, 0], ids=["half-tiles", "full-tiles"])
 def adam_tiles(request, dev):
     ops.set_option("tn3_half", request.param)
     yield request.param
