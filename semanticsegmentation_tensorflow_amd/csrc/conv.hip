@@ -545,7 +545,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "wgrad_la")) {
-        if (value != 1 && value != 2) return SEG_EINVAL;
+        if (value < 1 || value > 3) return SEG_EINVAL;
         seg::g_wgrad_la = value;
         return SEG_OK;
     }

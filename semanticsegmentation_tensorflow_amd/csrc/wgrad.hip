@@ -32,7 +32,7 @@ static __device__ uint4 wg_zero_page[4];
 
 int g_wgrad_halo = 1;
 int g_wgrad_nt = 128;
-int g_wgrad_la = 1;
+int g_wgrad_la = 3;   // 1: per-read index arithmetic, 2: flat 36-step pipeline (spills), 3: packed per-lane offsets
 int g_wgrad_abl = 0;
 int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
 
@@ -175,6 +175,32 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             b_hi[ni] = (kk + 4) * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d2)) + 8 * (tpp & 1);
         }
     }
+    // LA == 3: the same per-lane offsets packed two per register (rows kk and
+    // kk + 4 as lo | hi << 16; BW = 16, hwd % 8 == 0 so substeps only add a
+    // wave-uniform base): one VALU op per fragment read instead of the
+    // index / swizzle arithmetic, at 13 VGPRs
+    unsigned a_pk[9], b_pk[NF];
+    if constexpr (LA == 3) {
+        static_assert(BW == 16, "packed offsets need 16-pixel tile rows");
+        const int kk = 8 * fg + tq;
+        const int py = kk / BW, px = kk - (kk / BW) * BW;
+        const int achk = cf * 2 + (tpp >> 1);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int r1 = py * g.hwd + px + tapoff[t];
+            const unsigned lo = r1 * 128 + 16 * (achk ^ wg_swz<128>(r1)) + 8 * (tpp & 1);
+            const unsigned hi = (r1 + 4) * 128 + 16 * (achk ^ wg_swz<128>(r1 + 4)) + 8 * (tpp & 1);
+            a_pk[t] = lo | (hi << 16);
+        }
+        const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
+#pragma unroll
+        for (int ni = 0; ni < NF; ++ni) {
+            const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
+            const unsigned lo = kk * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d1)) + 8 * (tpp & 1);
+            const unsigned hi = (kk + 4) * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d2)) + 8 * (tpp & 1);
+            b_pk[ni] = lo | (hi << 16);
+        }
+    }
     // per-wave DMA instructions per tile (wave-uniform, tile-independent)
     const int per_tile = h_n + D_INS;
     for (int i = 0; i < NST - 1; ++i)
@@ -216,10 +242,17 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
 #pragma unroll
             for (int ni = 0; ni < NF; ++ni) {
-                const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
-                const int q1 = (chk & ~15) | ((chk & 15) ^ d1), q2 = (chk & ~15) | ((chk & 15) ^ d2);
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * q1 + 8 * (tpp & 1)));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
+                s16x4 lo, hi;
+                if constexpr (LA == 3) {
+                    SEG_LDS char* dbs = (SEG_LDS char*)smem + buf * STAGE + HBUF + ss * 32 * DROWB;
+                    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] & 0xffffu)));
+                    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] >> 16)));
+                } else {
+                    const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
+                    const int q1 = (chk & ~15) | ((chk & 15) ^ d1), q2 = (chk & ~15) | ((chk & 15) ^ d2);
+                    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * q1 + 8 * (tpp & 1)));
+                    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
+                }
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 bo[ni] = __builtin_bit_cast(bf16x8, v);
                 if (do_bias && ni == cf && ss % g.nbias == ct) {
@@ -230,6 +263,13 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             }
         };
         auto read_a = [&](int ss, int tap) {
+            if constexpr (LA == 3) {
+                SEG_LDS char* hb = (SEG_LDS char*)smem + buf * STAGE + ss * (32 / BW) * g.hwd * 128;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] & 0xffffu)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] >> 16)));
+                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                return __builtin_bit_cast(bf16x8, v);
+            }
             if constexpr (ABL == 3) {
                 s16x8 v = {(short)ss, (short)tap, 1, 2, 3, 4, 5, (short)lane};
                 return __builtin_bit_cast(bf16x8, v);
@@ -374,10 +414,10 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     const int nimg = p.P / (p.Ha * p.Wa);
     long best = -1;
     for (int bw : {32, 16}) {
-        if (g_wgrad_la == 2 && bw != 16) continue;
+        if (g_wgrad_la >= 2 && bw != 16) continue;
         const int bh = 128 / bw;
         int hwd = bw + 2 * p.tsw;
-        if (g_wgrad_la == 2) hwd = (hwd + 7) & ~7;          // substep row shifts keep the swizzle
+        if (g_wgrad_la >= 2) hwd = (hwd + 7) & ~7;          // substep row shifts keep the swizzle
         const int hrows = hwd * (bh + 2 * p.tsh);
         if (hrows > 5 * 64) continue;
         const int tx = (p.Wa + bw - 1) / bw, ty = (p.Ha + bh - 1) / bh;
@@ -431,6 +471,12 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s) {
     }
     if (g_wgrad_la == 2 && wp.nt == 128 && wp.bw == 16) {
         hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 2>), grid, block, 0, s, p, g);
+        return;
+    }
+    if (g_wgrad_la == 3 && wp.bw == 16) {
+        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 3>), grid, block, 0, s, p, g);
+        else if (small) hipLaunchKernelGGL((wgrad_halo<16, 64, 3, 4, 3>), grid, block, 0, s, p, g);
+        else hipLaunchKernelGGL((wgrad_halo<16, 64, 2, 5, 3>), grid, block, 0, s, p, g);
         return;
     }
     if (wp.bw == 32) {

@@ -145,8 +145,8 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
-                                                   "wgrad-nbias4", "tn3-half"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                      "wgrad-nbias4", "tn3-half", "wgrad-la1"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
@@ -154,15 +154,19 @@ def tnv(request, dev):
     5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off in 2 so
     igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
     BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5 with
-    the 256x128 two-blocks-per-CU tiles also for plain single-split launches."""
+    the 256x128 two-blocks-per-CU tiles also for plain single-split launches,
+    8 = 4 with the per-fragment index arithmetic instead of packed per-lane
+    LDS offsets (wgrad_la 1 vs the default 3)."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
-    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6) else 0)
-    ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
+    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6, 8) else 0)
+    ops.set_option("wgrad_la", 1 if v == 8 else 3)
+    ops.set_option("wgrad_nt", 128 if v in (4, 6, 8) else 64)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
     ops.set_option("tn3_half", 7 if v == 7 else 1)
     yield v
+    ops.set_option("wgrad_la", 3)
     ops.set_option("tn3_half", 1)
     ops.set_option("tn3", 1)
     ops.set_option("wgrad_nbias", 1)
