@@ -16,7 +16,10 @@
 //    iteration issues at most B_INS + 1 DMA instructions per wave and one
 //    counted `s_waitcnt vmcnt` + barrier per iteration suffices.
 //  * A fragment = 16 consecutive output px of one tile row = 16 consecutive
-//    halo rows: the (row>>1)&7 chunk XOR stays conflict-free for any offset.
+//    halo rows starting at ANY row (taps shift it): the chunk XOR (row & 6)
+//    keeps every ds_read_b128 lane group (gfx950: lanes {0-3,12-15,20-27},
+//    ...) on 16 distinct 16-byte slots for every start row -- the
+//    (row >> 1) & 7 XOR is 2-way conflicted whenever start row % 4 != 0.
 //  * output: same LDS-staged 16-byte epilogue as igemm_nt2 (bias / BN-affine /
 //    ReLU / dropout / residual), or fp32 split-K slabs over channel chunks.
 //
@@ -79,8 +82,8 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     const int wm = w / WN, wn = w - (w / WN) * WN;
     const int lr = lane >> 3;
     // physical 16-byte chunk (lane & 7) of LDS row (q*8 + lr) holds global
-    // chunk c; with NW even the swizzle (row>>1)&7 depends on w, lr only.
-    const int c = (lane & 7) ^ ((((w & 1) << 2) + (lr >> 1)) & 7);
+    // chunk c; the swizzle row & 6 depends on lr only.
+    const int c = (lane & 7) ^ (lr & 6);   // halo row (h*NW + w)*8 + lr: swizzle row & 6
 
     const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
     const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
@@ -178,12 +181,12 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 const int row = rowbase[mi] + toff;
-                af[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+                af[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ (row & 6)));
             }
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const int row = wn * WTN + ni * 16 + fr;
-                bfr[ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+                bfr[ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * (chunk ^ (row & 6)));
             }
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi)
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = w >> 2, wn = w & 3;
     const int lr = lane >> 3;
-    const int c = (lane & 7) ^ ((((w & 1) << 2) + (lr >> 1)) & 7);
+    const int c = (lane & 7) ^ (lr & 6);   // halo row (h*NW + w)*8 + lr: swizzle row & 6
 
     const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
     const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 for (int mi = 0; mi < 4; ++mi) {
                     const int row = rowbase[mh * 4 + mi] + toff;
                     if constexpr (ABL == 3) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
-                    else af[ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                    else af[ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
         auto read_b = [&](int nh) {
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 for (int ni = 0; ni < NFH; ++ni) {
                     const int row = wn * WTN + nh * (WTN / 2) + ni * 16 + fr;
                     if constexpr (ABL == 3) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
-                    else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                    else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
         auto mma = [&](int mh, int nh) {
@@ -638,7 +641,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
             v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col +
                                                 (long)((p.rb + p.rstep * j) * p.Sfull + (p.sb + p.sstep * ii)) * p.w_tap +
                                                 c8 * 8);
-        *reinterpret_cast<uint4*>(Bs + (tap * 64 + n) * 128 + 16 * (c8 ^ ((n >> 1) & 7))) = v;
+        *reinterpret_cast<uint4*>(Bs + (tap * 64 + n) * 128 + 16 * (c8 ^ (n & 6))) = v;
     }
     // ---- halo fetch into registers: slot q -> (row q / 8, chunk q % 8)
     uint4 hv[R64_PER];
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
         for (int k = 0; k < R64_PER; ++k) {
             const int q = tid + k * 512;
             const int hr = q >> 3, c8 = q & 7;
-            if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 128 + 16 * (c8 ^ ((hr >> 1) & 7))) = hv[k];
+            if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 128 + 16 * (c8 ^ (hr & 6))) = hv[k];
         }
     };
 
@@ -724,12 +727,12 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 const int row = rowbase[mi] + toff[tap];
-                a[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+                a[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ (row & 6)));
             }
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const int row = wn * WTN + ni * 16 + fr;
-                b[ni] = *reinterpret_cast<const uint4*>(Bt + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+                b[ni] = *reinterpret_cast<const uint4*>(Bt + row * 128 + 16 * (chunk ^ (row & 6)));
             }
         };
         load_step(0, fa[0], fb[0]);

@@ -523,19 +523,31 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
 
     const int fg = lane >> 4;
     const int tq = (lane & 15) >> 2, tpp = lane & 3;
+    // Per-lane LDS byte offsets of the fragment reads, hoisted out of the
+    // loop: row r1 = 8 fg + tq has bit 2 clear, so rows r1 + 4 and
+    // r1 + 32 ks share its swizzle and are immediate offsets of one address.
+    const int fr1 = 8 * fg + tq, fsw = tn3_swz(fr1);
+    auto lane_off = [&](int col0, int rowb) {
+        const int chk = (col0 >> 3) + (tpp >> 1);
+        return (unsigned)(fr1 * rowb + 16 * ((chk & ~15) | ((chk & 15) ^ fsw)) + 8 * (tpp & 1));
+    };
+    unsigned aoff[2][4], boff[TN];
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) aoff[mh][mi] = lane_off(wm * WTM + mh * 64 + mi * 16, ROWB);
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) boff[ni] = lane_off(wn * WTN + ni * 16, ROWBB);
     int abuf = 0, bbuf = 0;
     for (int it = 0; it < nk; ++it) {
-        const char* As = smem + abuf * ABUF;
-        const char* Bs = smem + 3 * ABUF + bbuf * BBUF;
+        SEG_LDS char* As = (SEG_LDS char*)smem + abuf * ABUF;
+        SEG_LDS char* Bs = (SEG_LDS char*)smem + 3 * ABUF + bbuf * BBUF;
         bf16x8 af[KS][4], bq[KS][TN];
-        // 16 columns x 32 pixel rows fragment at column `col0`, k rows ks*32 ..
-        auto frag = [&](const char* base, int rowb, int col0, int ks) {
-            const int r1 = ks * 32 + 8 * fg + tq;
-            const int chk = (col0 >> 3) + (tpp >> 1);
-            const int c1 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1));
-            const int c2 = (chk & ~15) | ((chk & 15) ^ tn3_swz(r1 + 4));
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + r1 * rowb + 16 * c1 + 8 * (tpp & 1)));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(base + (r1 + 4) * rowb + 16 * c2 + 8 * (tpp & 1)));
+        // 16 columns x 32 pixel rows fragment at lane offset `off`, k rows ks*32 ..
+        auto frag = [&](SEG_LDS char* base, int rowb, unsigned off, int ks) {
+            SEG_LDS char* a = base + off + ks * 32 * rowb;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)a);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(a + 4 * rowb));
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             return __builtin_bit_cast(bf16x8, v);
         };
@@ -543,7 +555,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi) af[ks][mi] = frag(As, ROWB, wm * WTM + mh * 64 + mi * 16, ks);
+                for (int mi = 0; mi < 4; ++mi) af[ks][mi] = frag(As, ROWB, aoff[mh][mi], ks);
         };
         auto mma = [&](int mh) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -562,7 +574,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, ROWBB, wn * WTN + ni * 16, ks);
+            for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, ROWBB, boff[ni], ks);
         if (ABL != 1 && it + 1 < nk) issue_b(bbuf ^ 1);
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(0);
