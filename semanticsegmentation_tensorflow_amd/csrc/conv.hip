@@ -462,6 +462,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
     return SEG_OK;
 }
 
+int g_adam_tr_fused = 0;   // 1: the fused epilogue also writes the KRSC copy (transposed 16-byte stores)
+
 extern "C" int seg_set_option(const char* name, int value) {
     if (!name) return SEG_EINVAL;
     if (!strcmp(name, "igemm_nt_variant")) {
@@ -477,6 +479,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "tn3_abl")) {   // diagnostic builds only: results are garbage
         if (value < 0 || value > 3) return SEG_EINVAL;
         seg::g_tn3_abl = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "adam_tr_fused")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        g_adam_tr_fused = value;
         return SEG_OK;
     }
     if (!strcmp(name, "nt3_fill")) {
@@ -691,6 +698,41 @@ extern "C" int seg_conv_wgrad_adam_fusable(const seg_conv_desc* d) {
     return wgrad_adam_params(d, &p) ? 1 : 0;
 }
 
+// KRSC copy from the HWIO copy the fused-Adam epilogue wrote: tr[n][rs][c] =
+// rows[rs][c][n] for c < C, n < K (padding untouched).  64 x 64 tiles staged
+// through LDS so both sides move 128-byte runs (the epilogue's own transposed
+// 16-byte stores, strided by RS * tr_ap, cost more than this pass).
+__global__ __launch_bounds__(256) void rows_to_tr_k(const bf16* __restrict__ rows, bf16* __restrict__ tr, int RS,
+                                                    int C, int K, int rows_ap, int rows_bp, int tr_ap, int ctiles) {
+    __shared__ bf16 t[64][64 + 8];
+    const int rs = blockIdx.y, c0 = (blockIdx.x % ctiles) * 64, n0 = (blockIdx.x / ctiles) * 64;
+    const int tid = threadIdx.x;
+    // load: 64 rows (c) x 64 n, 8 bf16 per thread-chunk: 512 chunks / 256 threads
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int q = tid + k * 256, cr = q >> 3, nc = (q & 7) * 8;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (c0 + cr < C && n0 + nc < rows_bp)
+            v = *reinterpret_cast<const uint4*>(rows + ((long)rs * rows_ap + c0 + cr) * rows_bp + n0 + nc);
+        const bf16* e = reinterpret_cast<const bf16*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[nc + j][cr] = e[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int q = tid + k * 256, nr = q >> 3, cc = (q & 7) * 8;
+        const int n = n0 + nr, c = c0 + cc;
+        if (n >= K || c >= C) continue;
+        bf16* dst = tr + ((long)n * RS + rs) * tr_ap + c;
+        if (c + 8 <= C) {
+            *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(&t[nr][cc]);
+        } else {
+            for (int j = 0; j < 8 && c + j < C; ++j) dst[j] = t[nr][cc + j];
+        }
+    }
+}
+
 extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void* dy, float* dw,
                                           float* dbias, const seg_adam_fused* a, void* ws, size_t ws_bytes,
                                           void* stream) {
@@ -702,7 +744,8 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     const double lr_t = (double)a->lr * sqrt(1.0 - pow((double)a->beta2, a->t)) / (1.0 - pow((double)a->beta1, a->t));
     p.adam.p = a->p; p.adam.m = a->m; p.adam.v = a->v;
     p.adam.rows = a->rows_dst; p.adam.rows_ap = a->rows_ap; p.adam.rows_bp = a->rows_bp;
-    p.adam.tr = a->tr_dst; p.adam.tr_ap = a->tr_ap; p.adam.RS = d->R * d->S;
+    const bool tr_after = a->tr_dst && a->rows_dst && !g_adam_tr_fused;
+    p.adam.tr = tr_after ? nullptr : a->tr_dst; p.adam.tr_ap = a->tr_ap; p.adam.RS = d->R * d->S;
     p.adam.lr_t = (float)lr_t; p.adam.b1 = a->beta1; p.adam.b2 = a->beta2; p.adam.eps = a->eps;
     p.adam.gs = a->grad_scale;
     p.adam.store_grad = dw != nullptr;
@@ -711,6 +754,14 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.partial = nullptr;
     seg::launch_tn3(p, 1, (hipStream_t)stream);
     SEG_CHECK_LAUNCH();
+    if (tr_after) {
+        const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;
+        const int ctiles = (C + 63) / 64, ntiles = (K + 63) / 64;
+        hipLaunchKernelGGL(rows_to_tr_k, dim3(ctiles * ntiles, RS), dim3(256), 0, (hipStream_t)stream,
+                           (const bf16*)a->rows_dst, (bf16*)a->tr_dst, RS, C, K, a->rows_ap, a->rows_bp, a->tr_ap,
+                           ctiles);
+        SEG_CHECK_LAUNCH();
+    }
     if (!dbias) return SEG_OK;
     return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
 }

@@ -547,11 +547,14 @@ ADAM_FUSED_CASES = [
 ]
 
 
-@pytest.fixture(params=[5, 0], ids=["half-tiles", "full-tiles"])
+@pytest.fixture(params=[(5, 0), (0, 0), (0, 1)], ids=["half-tiles", "full-tiles", "full-tiles-tr-fused"])
 def adam_tiles(request, dev):
-    ops.set_option("tn3_half", request.param)
+    half, trf = request.param
+    ops.set_option("tn3_half", half)
+    ops.set_option("adam_tr_fused", trf)
     yield request.param
     ops.set_option("tn3_half", 1)
+    ops.set_option("adam_tr_fused", 0)
 
 
 @pytest.mark.parametrize("case", ADAM_FUSED_CASES)
