@@ -654,9 +654,10 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     int bm, bn, splits;
     choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, bm, bn, splits);
     if (g_nt_variant == 2 && nt3_applies(N, dtype)) {
-        int s3;
+        int s3, s4;
         nt3_info(M, N, K, num_cus(), &s3);
-        splits = std::max(splits, s3);
+        nt4_info(M, N, K, num_cus(), &s4);
+        splits = std::max(splits, std::max(s3, s4));
     }
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
@@ -712,13 +713,18 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         return SEG_OK;
     }
     const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m);
-    if (nt3) {
+    const bool nt4 = nt3 && nt4_ok(p, SEG_BF16);
+    if (nt4) {
+        nt4_info(max_m, p.N, p.K, num_cus(), &splits);
+        if (nphases > 1) splits = 1;
+    } else if (nt3) {
         nt3_info(max_m, p.N, p.K, num_cus(), &splits);
         if (nphases > 1) splits = 1;
     }
     int gridz = nphases;
     if (splits > 1) {
-        const int kt = (p.K + BK - 1) / BK;
+        const int bk = nt4 ? 32 : BK;
+        const int kt = (p.K + bk - 1) / bk;
         p.kt_per_split = (kt + splits - 1) / splits;
         splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
         const size_t need = (size_t)splits * p.M * p.N * sizeof(float);
@@ -726,7 +732,8 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (nt3) launch_nt3(p, gridz, max_m, s);
+    if (nt4) launch_nt4(p, gridz, max_m, s);
+    else if (nt3) launch_nt3(p, gridz, max_m, s);
     else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
@@ -755,10 +762,12 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
         return "conv_halo";
     }
     if (dtype == SEG_BF16 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m)) {
-        nt3_info(max_m, p.N, p.K, num_cus(), splits);
+        const bool nt4 = nt4_ok(p, SEG_BF16);
+        if (nt4) nt4_info(max_m, p.N, p.K, num_cus(), splits);
+        else nt3_info(max_m, p.N, p.K, num_cus(), splits);
         if (nphases > 1) *splits = 1;
         *bm = *bn = 256;
-        return "igemm_nt3";
+        return nt4 ? "igemm_nt4" : "igemm_nt3";
     }
     return *bm == 256 ? "igemm_nt2" : "igemm_nt";
 }

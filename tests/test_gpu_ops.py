@@ -17,8 +17,8 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8],
-                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9],
+                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3", "nt4"])
 def ntv(request, dev):
     """Run NT tests on every kernel generation: 1 = register-staged GEMM,
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
@@ -28,7 +28,8 @@ def ntv(request, dev):
     7 = 3 with the two-phase kernel also for N <= 128 (off by default),
     8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
     (by default only where its grid fills half the CUs; variant 2 keeps it
-    off so igemm_nt2 stays covered for wide N)."""
+    off so igemm_nt2 stays covered for wide N), 9 = 8 with the four-wave
+    128x128-per-wave GEMM (igemm_nt4) in place of igemm_nt3."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
     ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
@@ -37,8 +38,10 @@ def ntv(request, dev):
     ops.set_option("halo_stagger", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
-    ops.set_option("nt3_fill", 0 if v == 8 else 1)   # small test problems: force the 256x256 tiles
+    ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
+    ops.set_option("nt4", 1 if v == 9 else 0)
     yield v
+    ops.set_option("nt4", 0)
     ops.set_option("nt3_fill", 1)
     ops.set_option("igemm_nt_variant", 2)
     ops.set_option("nt_halo", 1)
