@@ -473,17 +473,32 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
     }
 }
 
-__global__ void bn_finish_k(const float* __restrict__ part, int nrows, int C, int cv, float inv, float* dgamma,
-                            float* dbeta) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= cv) return;
+// dgamma / dbeta from the per-block partial rows: 8 channels per block, the
+// rows split over 32 thread groups (a thread per channel looping over all
+// rows serialised ~2k dependent loads: 170 us per BN layer)
+__global__ __launch_bounds__(256) void bn_finish_k(const float* __restrict__ part, int nrows, int C, int cv,
+                                                   float inv, float* dgamma, float* dbeta) {
+    __shared__ float sg[32][9], sb[32][9];
+    const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    const int k = blockIdx.x * 8 + cl;
     float g = 0.f, b = 0.f;
-    for (int r = 0; r < nrows; ++r) {
-        g += part[(long)r * 2 * C + k];
-        b += part[(long)r * 2 * C + C + k];
+    if (k < cv)
+        for (int r = rg; r < nrows; r += 32) {
+            g += part[(long)r * 2 * C + k];
+            b += part[(long)r * 2 * C + C + k];
+        }
+    sg[rg][cl] = g;
+    sb[rg][cl] = b;
+    __syncthreads();
+    if (threadIdx.x < 8 && k < cv) {
+        float tg = 0.f, tb = 0.f;
+        for (int r = 0; r < 32; ++r) {
+            tg += sg[r][cl];
+            tb += sb[r][cl];
+        }
+        dgamma[k] = tg * inv;
+        dbeta[k] = tb;
     }
-    dgamma[k] = g * inv;
-    dbeta[k] = b;
 }
 
 // ---------------------------------------------------------------------------
@@ -913,7 +928,7 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
     DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)x, ldx, (const T*)y,
                                          ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, inv, (float*)ws, P, C, cv, relu));
     SEG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bn_finish_k, dim3((cv + 255) / 256), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
+    hipLaunchKernelGGL(bn_finish_k, dim3((cv + 7) / 8), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }
