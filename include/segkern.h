@@ -197,6 +197,12 @@ int seg_dropout_fwd(const void* x, void* y, long n, float keep_prob, uint64_t se
                     void* stream);
 int seg_dropout_bwd(const void* dy, void* dx, long n, float keep_prob, uint64_t seed, int dtype,
                     void* stream);
+/* Gradient of a dropout fused into a conv epilogue without ReLU (the
+ * epilogue draws element (pixel p, channel c) with counter p * c_valid + c):
+ * dz = dy / keep_prob * floor(keep_prob + U), padding channels zeroed.
+ * NHWC with pixel strides ldy / ldz, C % 8 == 0. */
+int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C, int c_valid,
+                       float keep_prob, uint64_t seed, int dtype, void* stream);
 /* Frozen-stat BatchNorm (+ReLU): y = relu?(x*scale[c] + shift[c])
  * (Network/utils/utils.py:300-301).  scale = gamma/sqrt(1+eps). */
 int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const float* gamma,

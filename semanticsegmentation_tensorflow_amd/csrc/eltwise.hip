@@ -266,6 +266,29 @@ __global__ void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n, fl
     }
 }
 
+// TF1 dropout gradient of a conv whose forward epilogue applied the dropout
+// (no ReLU after it): element (pixel p, channel c < cv) uses the epilogue's
+// counter index p * cv + c; padding channels are zeroed.
+template <typename T>
+__global__ void dropout_ch_k(const T* __restrict__ dy, int ldy, T* __restrict__ dz, int ldz, long P, int C, int cv,
+                             float kp, uint64_t seed) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int chunks = C / EPC;
+    const long total = P * chunks;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / chunks;
+        const int c0 = (int)(i - p * chunks) * EPC;
+        float v[EPC];
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(dy + p * ldy + c0), v);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            const int c = c0 + e;
+            v[e] = c < cv ? (v[e] / kp) * floorf(kp + seg_uniform(seed, (uint64_t)p * cv + c)) : 0.f;
+        }
+        *reinterpret_cast<uint4*>(dz + p * ldz + c0) = Chunk<T>::pack(v);
+    }
+}
+
 template <typename T>
 __global__ void fill_k(T* y, long n, float v) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -807,6 +830,16 @@ extern "C" int seg_dropout_fwd(const void* x, void* y, long n, float kp, uint64_
 extern "C" int seg_dropout_bwd(const void* dy, void* dx, long n, float kp, uint64_t seed, int dtype, void* stream) {
     // the same mask and 1/kp scale: dx = dy / kp * floor(kp + U)
     return seg_dropout_fwd(dy, dx, n, kp, seed, dtype, stream);
+}
+
+extern "C" int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C, int cv, float kp,
+                                  uint64_t seed, int dtype, void* stream) {
+    if (!dy || !dz || !(kp > 0.f) || kp > 1.f || (C & 7) || cv > C || ldy < C || ldz < C) return SEG_EINVAL;
+    const long total = P * (C / epc_of(dtype));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)dy, ldy, (T*)dz, ldz, P, C, cv, kp, seed));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
 }
 
 extern "C" int seg_fill(void* y, long n, float v, int dtype, void* stream) {

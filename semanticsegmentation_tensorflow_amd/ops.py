@@ -339,6 +339,16 @@ def dropout_fwd(x, y, keep_prob, seed, stream=None):
     return y
 
 
+def dropout_bwd_ch(dy, dz, c_valid, keep_prob, seed, stream=None):
+    """Gradient of a conv-epilogue dropout (counter p * c_valid + c)."""
+    C = dy.shape[-1]
+    P = dy.numel() // C
+    check(_lib.lib().seg_dropout_bwd_ch(ptr(dy), pixel_stride(dy), ptr(dz), pixel_stride(dz), P, C, int(c_valid),
+                                        float(keep_prob), int(seed), seg_dtype(dy), stream_ptr(stream)),
+          "dropout_grad")
+    return dz
+
+
 def bn_relu_fwd(x, y, gamma, beta, c_valid, relu=True, eps=1e-3, stream=None):
     N, H, W, C = x.shape
     check(_lib.lib().seg_bn_relu_fwd(ptr(x), pixel_stride(x), ptr(y), pixel_stride(y), ptr(gamma),

@@ -130,6 +130,9 @@ class Session:
         # the next layer's input gradient (single process: DP all-reduces need
         # the reduced gradient on the compute stream)
         self.defer_wgrad_reduce = True
+        # Dropout right after a bias-free / ReLU-free conv (FC-DenseNet's
+        # Conv2D_Block + dropout) applied in the conv epilogue
+        self.fuse_dropout = True
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -261,6 +264,9 @@ class Session:
                     relu = True
                     chain.append(nxt)
                     cur = nxt.outputs[0]
+                if relu or self.fuse_dropout:
+                    # Conv [+BiasAdd] [+Relu] + Dropout: applied in the epilogue (without
+                    # a ReLU the gradient re-draws the mask: seg_dropout_bwd_ch)
                     nxt = single_consumer(cur, "Dropout")
                     if nxt is not None:
                         kp = nxt.attrs["keep_prob"]
@@ -840,7 +846,16 @@ class Session:
                 yb = buf[id(n.output)]
                 dz = dy
                 fused_db = None
-                if id(n) in p.mask_fuse or (n.bias is not None and not n.relu):
+                if not n.relu and n.kp_val is not None and n.kp_val < 1.0:
+                    # dropout applied in the forward epilogue, no ReLU: re-draw its mask
+                    dz = p.tmp.get(("dz", id(n.output)))
+                    if dz is None:
+                        dz = torch.zeros_like(yb)
+                        p.tmp[("dz", id(n.output))] = dz
+                    ops.dropout_bwd_ch(dy, dz, n.desc.k_valid, n.kp_val, n.seed_val)
+                    if n.bias is not None:
+                        fused_db = store.grad(n.bias.var_name)
+                elif id(n) in p.mask_fuse or (n.bias is not None and not n.relu):
                     # gradient arrives masked (or there is no ReLU): BiasAddGrad is
                     # summed by the filter-gradient launch below
                     if n.bias is not None:
