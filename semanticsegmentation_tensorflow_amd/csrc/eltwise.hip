@@ -383,6 +383,63 @@ __global__ void concat_bwd_k(const T* __restrict__ dy, int ldy, ConcatArgs a, co
     }
 }
 
+// bf16 fast paths when every part starts on an 8-channel boundary: a lane owns
+// one output chunk (its source part found once), pixels are walked with
+// 16-byte loads / stores (the element loops above run at a fraction of HBM)
+__global__ __launch_bounds__(256) void concat_fwd_fast_k(ConcatArgs a, bf16* __restrict__ y, int ldy, int yc8,
+                                                         long P) {
+    const RedGeom g = red_geom(yc8 * 8, 8);
+    const int t = threadIdx.x;
+    const int c8 = t % g.LPP, prow = t / g.LPP;
+    if (prow >= g.rows) return;
+    const long step = (long)gridDim.x * g.rows;
+    for (int j = 0; j < g.iters; ++j) {
+        const int k = c8 + j * g.LPP;
+        if (k >= yc8) break;
+        int src = 0;
+        while (src < a.n && k * 8 >= a.off[src + 1]) ++src;
+        const bf16* xp = src < a.n ? reinterpret_cast<const bf16*>(a.part[src].ptr) + (k * 8 - a.off[src]) : nullptr;
+        const int ld = src < a.n ? a.part[src].ld : 0;
+        for (long p = (long)blockIdx.x * g.rows + prow; p < P; p += step) {
+            const uint4 v = xp ? *reinterpret_cast<const uint4*>(xp + p * ld) : uint4{0u, 0u, 0u, 0u};
+            *reinterpret_cast<uint4*>(y + p * ldy + k * 8) = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void concat_bwd_fast_k(const bf16* __restrict__ dy, int ldy, ConcatArgs a,
+                                                         int chunks, long P) {
+    const RedGeom g = red_geom(chunks * 8, 8);
+    const int t = threadIdx.x;
+    const int c8 = t % g.LPP, prow = t / g.LPP;
+    if (prow >= g.rows) return;
+    const long step = (long)gridDim.x * g.rows;
+    for (int j = 0; j < g.iters; ++j) {
+        int k = c8 + j * g.LPP;
+        if (k >= chunks) break;
+        int d = 0;
+        while (d < a.n && k >= (a.part[d].channels + 7) / 8) { k -= (a.part[d].channels + 7) / 8; ++d; }
+        if (d >= a.n) break;
+        const seg_concat_part& pt = a.part[d];
+        bf16* xp = reinterpret_cast<bf16*>(const_cast<void*>(pt.ptr)) + k * 8;
+        const bf16* sp = dy + a.off[d] + k * 8;
+        const int nv = min(8, pt.channels - k * 8);   // valid channels of this chunk
+        for (long p = (long)blockIdx.x * g.rows + prow; p < P; p += step) {
+            float v[8], d8[8];
+            Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(sp + p * ldy), d8);
+            if (pt.accumulate) {
+                Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(xp + p * pt.ld), v);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += e < nv ? d8[e] : 0.f;
+            *reinterpret_cast<uint4*>(xp + p * pt.ld) = Chunk<bf16>::pack(v);
+        }
+    }
+}
+
 template <typename T, typename S = float>
 __global__ void prepare_input_k(const S* __restrict__ img, T* __restrict__ x, int N, int H, int W, int cin, int HP,
                                 int WP, int CP) {
@@ -910,6 +967,16 @@ extern "C" int seg_concat_fwd(const seg_concat_part* parts, int nparts, void* y,
     int st = concat_args(parts, nparts, &a);
     if (st) return st;
     if (!y || (ldy & 7) || (ychannels & 7) || ychannels < a.off[nparts] || ldy < ychannels) return SEG_EINVAL;
+    bool aligned = dtype == SEG_BF16;
+    for (int i = 0; i < nparts; ++i) aligned = aligned && (a.off[i] & 7) == 0;
+    if (aligned) {
+        const RedGeom g = red_geom(ychannels, 8);
+        const long blocks = std::max<long>(1, std::min<long>((P + g.rows - 1) / g.rows, 16384));
+        hipLaunchKernelGGL(concat_fwd_fast_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, (bf16*)y,
+                           ldy, ychannels / 8, P);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     const long total = P * (ychannels / 8);
     DISPATCH_T(dtype, hipLaunchKernelGGL(concat_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
                                          (hipStream_t)stream, a, (T*)y, ldy, ychannels / 8, P));
@@ -925,6 +992,16 @@ extern "C" int seg_concat_bwd(const void* dy, int ldy, const seg_concat_part* pa
     if (!dy || ldy < a.off[nparts]) return SEG_EINVAL;
     int chunks = 0;
     for (int i = 0; i < nparts; ++i) chunks += (parts[i].channels + 7) / 8;
+    bool aligned = dtype == SEG_BF16 && (ldy & 7) == 0;
+    for (int i = 0; i < nparts; ++i) aligned = aligned && (a.off[i] & 7) == 0;
+    if (aligned) {
+        const RedGeom g = red_geom(chunks * 8, 8);
+        const long blocks = std::max<long>(1, std::min<long>((P + g.rows - 1) / g.rows, 16384));
+        hipLaunchKernelGGL(concat_bwd_fast_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                           (const bf16*)dy, ldy, a, chunks, P);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     const long total = P * chunks;
     DISPATCH_T(dtype, hipLaunchKernelGGL(concat_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
                                          (hipStream_t)stream, (const T*)dy, ldy, a, (const int*)nullptr, P, chunks));

@@ -644,3 +644,35 @@ def test_conv2d_bwd_filter_begin_end(dev, case, dtype):
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     assert torch.equal(db, rdb)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("chans", [(16, 48, 8), (24, 40, 12), (5, 11), (64, 16, 16, 16, 430)],
+                         ids=["aligned", "aligned-tail", "unaligned", "densenet"])
+def test_concat_fwd_bwd(dev, dtype, chans):
+    """tf.concat(axis=-1) forward and its gradient split (write and
+    accumulate), channel-padded NHWC parts; bit-exact (copies / one add)."""
+    N, H, W = 2, 5, 7
+    g = torch.Generator().manual_seed(19)
+    xs = [torch.randn(N, H, W, c, generator=g) for c in chans]
+    parts = [(to_dev(x.double(), dtype, dev), c) for x, c in zip(xs, chans)]
+    tot = sum(chans)
+    y = torch.full((N, H, W, ops.round8(tot)), float("nan"), dtype=dtype, device=dev)
+    ops.concat_fwd(parts, y, tot)
+    torch.cuda.synchronize()
+    want = torch.cat([x.to(dtype) for x in xs], dim=-1)
+    assert torch.equal(y[..., :tot].cpu(), want)
+    if y.shape[-1] > tot:
+        assert y[..., tot:].abs().max().item() == 0
+    dy = to_dev(torch.randn(N, H, W, tot, generator=g, dtype=torch.float64), dtype, dev)
+    olds = [to_dev(torch.randn(N, H, W, c, generator=g, dtype=torch.float64), dtype, dev) for c in chans]
+    dsts = [o.clone() for o in olds]
+    acc = [i % 2 == 1 for i in range(len(chans))]
+    ops.concat_bwd(dy, [(d, c, a) for d, c, a in zip(dsts, chans, acc)])
+    torch.cuda.synchronize()
+    off = 0
+    for d, o, c, a in zip(dsts, olds, chans, acc):
+        sl = dy[..., off:off + c].float().cpu()
+        ref = (o[..., :c].float().cpu() + sl).to(dtype) if a else sl.to(dtype)
+        assert torch.equal(d[..., :c].cpu(), ref), (c, a)
+        off += c
