@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true", help="skip the KITTI data-pipeline rate probe")
     ap.add_argument("--no-fuse-adam", action="store_true",
                     help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="seg_set_option kernel knob (A/B runs; repeatable)")
     ap.add_argument("--overlap-optimizer", action="store_true",
                     help="per-layer Adam on a side stream as gradients become final (measured slower: the "
                          "HBM-bound update steals CUs from the MFMA-bound backward)")
@@ -315,6 +317,9 @@ def main():
     from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
     from semanticsegmentation_tensorflow_amd.fcn import FCN
 
+    for kv in args.option:
+        name, val = kv.split("=")
+        ops.set_option(name, int(val))
     H = args.height or (1024 if args.model == "deeplab" else 375)
     W = args.width or (2048 if args.model == "deeplab" else 1242)
     HP, WP = pad32(H), pad32(W)

@@ -495,6 +495,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         g_adam_tr_fused = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "nt2_short")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_nt2_short = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "nt3_fill")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt3_fill = value;

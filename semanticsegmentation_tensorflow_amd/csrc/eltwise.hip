@@ -262,7 +262,7 @@ template <typename T>
 __global__ void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n, float kp, uint64_t seed) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const float u = seg_uniform(seed, (uint64_t)i);
-        y[i] = from_f32<T>((to_f32(x[i]) / kp) * floorf(kp + u));
+        y[i] = from_f32<T>((to_f32(x[i]) * (1.f / kp)) * floorf(kp + u));
     }
 }
 
@@ -283,7 +283,7 @@ __global__ void dropout_ch_k(const T* __restrict__ dy, int ldy, T* __restrict__ 
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
             const int c = c0 + e;
-            v[e] = c < cv ? (v[e] / kp) * floorf(kp + seg_uniform(seed, (uint64_t)p * cv + c)) : 0.f;
+            v[e] = c < cv ? seg_dropout(v[e], kp, seed, (uint64_t)p * cv + c) : 0.f;
         }
         *reinterpret_cast<uint4*>(dz + p * ldz + c0) = Chunk<T>::pack(v);
     }

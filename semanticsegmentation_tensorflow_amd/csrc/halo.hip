@@ -278,7 +278,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             const int col = col0 + j;
             float x = v[j] * scl[j] + shf[j] + bias[j];
             if (e.relu) x = fmaxf(x, 0.f);
-            if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
             if (e.residual) x += res[j];
             if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = col < e.n_valid ? x : 0.f;
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 const int col = col0 + j;
                 float x = v[j] * scl[j] + shf[j] + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                 if (e.residual) x += res[j];
                 if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
                         const int col = col0 + j;
                         float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
                         if (e.relu) x = fmaxf(x, 0.f);
-                        if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+                        if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                         x += res[j];
                         if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                         o[j] = (bf16)(col < e.n_valid ? x : 0.f);

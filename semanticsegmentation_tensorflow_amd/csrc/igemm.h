@@ -98,6 +98,8 @@ void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* s
 const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits);
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
+extern int g_nt2_short;
+bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
 extern int g_tn_variant;
 extern int g_nt2_ablate;

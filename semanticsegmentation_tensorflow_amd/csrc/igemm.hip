@@ -65,7 +65,7 @@ __device__ __forceinline__ float nt_apply(const EpiParams& e, const NtRow& r, in
     if (e.shift) v += e.shift[col];
     if (e.bias) v += e.bias[col];
     if (e.relu) v = fmaxf(v, 0.f);
-    if (e.keep_prob < 1.f) v = (v / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, r.gidx + col));
+    if (e.keep_prob < 1.f) v = seg_dropout(v, e.keep_prob, e.seed, r.gidx + col);
     v += res;
     if (e.mask) v = mk > 0.f ? v * e.mask_scale : 0.f;
     return v;

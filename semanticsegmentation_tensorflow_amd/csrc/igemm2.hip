@@ -37,7 +37,7 @@ template <typename T>
         if (e.relu) v = fmaxf(v, 0.f);
         if (e.keep_prob < 1.f) {
             const uint64_t idx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid + col;
-            v = (v / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, idx));
+            v = seg_dropout(v, e.keep_prob, e.seed, idx);
         }
         if (e.residual)
             v += to_f32(reinterpret_cast<const T*>(e.residual)[img * e.res_img + pix * e.ld_res + col]);
@@ -47,8 +47,12 @@ template <typename T>
 
 // ABL (diagnostic builds only, results are garbage): 1 = no LDS-DMA in the
 // main loop, 2 = no MFMA, 3 = trivial (row-constant) source addresses.
-template <typename T, int BM, int BN, int WM, int WN, int ABL = 0>
-__global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
+// NSTG = ring depth.  3 for long K; 2 for short-K problems (1x1 convs over
+// <= 128 channels: one or two k tiles per block), where the smaller LDS
+// footprint lets two blocks share a CU so one block's loads overlap the
+// other's epilogue -- with one block per CU those blocks are pure latency.
+template <typename T, int BM, int BN, int WM, int WN, int ABL = 0, int NSTG = 3>
+__global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTParams p) {
     constexpr int NW = WM * WN;
     constexpr int EPC = dt_traits<T>::EPC;
     constexpr int BK = 128 / sizeof(T);
@@ -59,7 +63,10 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
     static_assert(NW % 2 == 0, "swizzle assumes an even wave count");
     constexpr int NI = A_INS + B_INS;
     constexpr int STAGE = (BM + BN) * 128;
-    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+    constexpr int SROW = WTN * 4 + 16;               // epilogue: padded fp32 row (bytes)
+    constexpr int SMEM = NSTG * STAGE > NW * WTM * SROW ? NSTG * STAGE : NW * WTM * SROW;
+    static_assert(NSTG == 2 || NSTG == 3, "ring depth");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
     int Ha = p.Ha, Wa = p.Wa, ioh = p.ioh, iow = p.iow, ooh = p.ooh, oow = p.oow;
     int rb = p.rb, sb = p.sb, M = p.M;
@@ -182,15 +189,15 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (kt_begin < kt_end) load_stage(0);
-    if (kt_begin + 1 < kt_end) load_stage(1);
+    if (NSTG == 3 && kt_begin + 1 < kt_end) load_stage(1);
 
     const int fr = lane & 15, fg = lane >> 4;
     int stage = 0;
     for (int kt = kt_begin; kt < kt_end; ++kt) {
-        if (kt + 1 < kt_end) wait_vmcnt<NI>();
+        if (NSTG == 3 && kt + 1 < kt_end) wait_vmcnt<NI>();
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (kt + 2 < kt_end) load_stage(stage == 0 ? 2 : stage - 1);
+        if (kt + NSTG - 1 < kt_end) load_stage(NSTG == 3 ? (stage == 0 ? 2 : stage - 1) : stage ^ 1);
         const char* As = smem + stage * STAGE;
         const char* Bs = As + BM * 128;
 #pragma unroll
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
                     }
                 }
         }
-        stage = stage == 2 ? 0 : stage + 1;
+        stage = stage == NSTG - 1 ? 0 : stage + 1;
     }
 
     if (p.partial) {
@@ -248,8 +255,6 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
     // ---- epilogue: stage the wave's fp32 tile in LDS, then each lane
     // finishes 8 consecutive columns of a row (one pixel decomposition per
     // row, 16-byte bf16 / 32-byte fp32 stores).
-    constexpr int SROW = WTN * 4 + 16;               // padded fp32 row (bytes)
-    static_assert(NW * WTM * SROW <= 3 * STAGE, "epilogue staging must fit the ring");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     char* wbuf = smem + w * WTM * SROW;
 #pragma unroll
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_nt2(NTParams p) {
             const int col = col0 + j;
             float x = v[j] * scl[j] + shf[j] + bias[j];
             if (e.relu) x = fmaxf(x, 0.f);
-            if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
             if (e.residual) x += res[j];
             if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = col < e.n_valid ? x : 0.f;
@@ -533,9 +538,20 @@ void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), g, b, 0, s, p);
 }
 
+// Short-K bf16 problems (<= 2 k tiles, no split-K) on the 2-stage ring with
+// 64-column tiles: two blocks per CU.  Runtime toggle for tests / A-B runs.
+int g_nt2_short = 1;
+
+bool nt2_short(const NTParams& p, int dtype) {
+    return g_nt2_short && dtype == SEG_BF16 && !p.partial && p.K <= 128 && g_nt2_ablate == 0;
+}
+
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s) {
     if (dtype == SEG_BF16) {
-        if (bn == 64) launch_nt2_t<bf16, 256, 64, 4, 2>(p, gridz, max_m, s);
+        if (nt2_short(p, dtype)) {
+            const int tiles = ((max_m + 255) / 256) * ((p.N + 63) / 64);
+            hipLaunchKernelGGL((igemm_nt2<bf16, 256, 64, 4, 2, 0, 2>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+        } else if (bn == 64) launch_nt2_t<bf16, 256, 64, 4, 2>(p, gridz, max_m, s);
         else launch_nt2_t<bf16, 256, 128, 4, 2>(p, gridz, max_m, s);
     } else {
         if (bn == 64) launch_nt2_t<float, 256, 64, 4, 2>(p, gridz, max_m, s);

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void igemm_nt4(NTParams p, int abl) {
                 const int col = col0 + j;
                 float x = v[j] * scl[j] + shf[j] + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = (x / e.keep_prob) * floorf(e.keep_prob + seg_uniform(e.seed, gidx + col));
+                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                 if (e.residual) x += res[j];
                 if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;

@@ -29,7 +29,9 @@ def ntv(request, dev):
     8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
     (by default only where its grid fills half the CUs; variant 2 keeps it
     off so igemm_nt2 stays covered for wide N), 9 = 8 with the four-wave
-    128x128-per-wave GEMM (igemm_nt4) in place of igemm_nt3."""
+    128x128-per-wave GEMM (igemm_nt4) in place of igemm_nt3.  Variant 8 also
+    turns off the 2-stage short-K igemm_nt2 (K <= 128), so the 3-stage ring
+    stays covered for those problems."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
     ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
@@ -40,7 +42,9 @@ def ntv(request, dev):
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
     ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
     ops.set_option("nt4", 1 if v == 9 else 0)
+    ops.set_option("nt2_short", 0 if v == 8 else 1)
     yield v
+    ops.set_option("nt2_short", 1)
     ops.set_option("nt4", 0)
     ops.set_option("nt3_fill", 1)
     ops.set_option("igemm_nt_variant", 2)
@@ -402,12 +406,17 @@ def test_adam_tf1(dev):
 
 
 def _np_uniform(seed, idx):
-    M = (1 << 64) - 1
-    z = (seed * 0x9E3779B97F4A7C15 + idx + 0x632BE59BD9B4E019) & M
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
-    z = z ^ (z >> 31)
-    return (z >> 40) / 16777216.0
+    """seg_uniform (csrc/common.h): lowbias32 of the counter plus a seed key."""
+    M = 0xFFFFFFFF
+    key = (((seed ^ (seed >> 32)) & M) * 0x9E3779B9 + 0x632BE59B) & M
+    x = ((idx & M) + key) & M
+    x ^= ((idx >> 32) * 0x85EBCA6B) & M
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M
+    x ^= x >> 16
+    return (x >> 8) / 16777216.0
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
