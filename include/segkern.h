@@ -208,10 +208,12 @@ int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C
 int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const float* gamma,
                     const float* beta, float eps, long P, int C, int c_valid, int relu,
                     int dtype, void* stream);
-/* dx = dy*(y>0)*scale; dgamma = sum(dy*(y>0)*x)/sqrt(1+eps); dbeta = sum(dy*(y>0)). */
+/* dx = dy*(y>0)*scale; dgamma = sum(dy*(y>0)*x)/sqrt(1+eps); dbeta = sum(dy*(y>0)).
+   flags: bit 0 = the forward had the ReLU (mask by y > 0), bit 1 = accumulate
+   (dx += ..., for gradients landing in a shared concat buffer). */
 int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy,
                     void* dx, int lddx, const float* gamma, float eps, float* dgamma,
-                    float* dbeta, long P, int C, int c_valid, int relu, int dtype, void* ws,
+                    float* dbeta, long P, int C, int c_valid, int flags, int dtype, void* ws,
                     size_t ws_bytes, void* stream);
 /* resize_bilinear(align_corners=True) (Network/utils/utils.py:329-330). */
 int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW,

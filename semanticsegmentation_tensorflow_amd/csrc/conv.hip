@@ -495,8 +495,8 @@ extern "C" int seg_set_option(const char* name, int value) {
         g_adam_tr_fused = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "nt2_short")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
+    if (!strcmp(name, "nt2_short")) {   // max k tiles (64 deep) of the 2-stage igemm_nt2; 0 = off
+        if (value < 0 || value > 64) return SEG_EINVAL;
         seg::g_nt2_short = value;
         return SEG_OK;
     }

@@ -514,8 +514,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, int ldx, const T* __restrict__ y, int ldy,
                                                      const T* __restrict__ dy, int lddy, T* __restrict__ dx, int lddx,
                                                      const float* __restrict__ gamma, float inv,
-                                                     float* __restrict__ part, long P, int C, int cv, int relu) {
+                                                     float* __restrict__ part, long P, int C, int cv, int flags) {
     constexpr int EPC = dt_traits<T>::EPC;
+    const bool relu = flags & 1, acc = flags & 2;
     extern __shared__ __attribute__((aligned(16))) float red[];
     const RedGeom g = red_geom(C, EPC);
     const int t = threadIdx.x;
@@ -536,10 +537,11 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                 if (j >= g.iters) break;
                 const int cc = c8 + j * g.LPP;
                 if (cc >= g.CK) break;
-                float xv[EPC], yv[EPC], d[EPC];
+                float xv[EPC], yv[EPC], d[EPC], old[EPC];
                 Chunk<T>::unpack(ldc(x + pix * ldx + cc * EPC), xv);
                 Chunk<T>::unpack(ldc(y + pix * ldy + cc * EPC), yv);
                 Chunk<T>::unpack(ldc(dy + pix * lddy + cc * EPC), d);
+                if (acc) Chunk<T>::unpack(ldc(dx + pix * lddx + cc * EPC), old);
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) {
                     const int c = cc * EPC + e;
@@ -548,6 +550,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                     sb[j][e] += dz;
                     sg[j][e] += dz * xv[e];
                     d[e] = c < cv ? dz * (gamma[c] * inv) : 0.f;
+                    if (acc) d[e] += old[e];
                 }
                 stc(dx + pix * lddx + cc * EPC, Chunk<T>::pack(d));
             }
@@ -1044,8 +1047,8 @@ extern "C" int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const f
 
 extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
                                int lddx, const float* gamma, float eps, float* dgamma, float* dbeta, long P, int C,
-                               int cv, int relu, int dtype, void* ws, size_t ws_bytes, void* stream) {
-    if (!x || !y || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7)) return SEG_EINVAL;
+                               int cv, int flags, int dtype, void* ws, size_t ws_bytes, void* stream) {
+    if (!x || !y || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7) || (flags & ~3)) return SEG_EINVAL;
     if (C > 4096) return SEG_EINVAL;
     const int nb = red_blocks(P, C, epc_of(dtype));
     if (!ws || ws_bytes < (size_t)nb * 2 * C * sizeof(float)) return SEG_EWORKSPACE;
@@ -1055,7 +1058,7 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
     if (shm > 64 * 1024) return SEG_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)x, ldx, (const T*)y,
-                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, inv, (float*)ws, P, C, cv, relu));
+                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, inv, (float*)ws, P, C, cv, flags));
     SEG_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_finish_k, dim3((cv + 7) / 8), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
     SEG_CHECK_LAUNCH();

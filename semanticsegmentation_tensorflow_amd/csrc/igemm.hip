@@ -669,6 +669,8 @@ int g_nt3_fill = 1;
 // more, smaller blocks on igemm_nt2 instead.
 static bool nt3_pick(const NTParams& p, int nphases, int max_m) {
     if (!nt3_ok(p, SEG_BF16)) return false;
+    // one or two k tiles: the 2-stage igemm_nt2 (two blocks per CU) wins
+    if (g_nt3_fill && g_nt2_short >= 2 && p.K <= 128) return false;
     if (!g_nt3_fill) return true;
     int s3;
     nt3_info(max_m, p.N, p.K, num_cus(), &s3);

@@ -538,12 +538,12 @@ void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), g, b, 0, s, p);
 }
 
-// Short-K bf16 problems (<= 2 k tiles, no split-K) on the 2-stage ring with
-// 64-column tiles: two blocks per CU.  Runtime toggle for tests / A-B runs.
-int g_nt2_short = 1;
+// Short-K bf16 problems (<= g_nt2_short 64-deep k tiles, no split-K) on the
+// 2-stage ring with 64-column tiles: two blocks per CU.  0 = off (tests / A-B).
+int g_nt2_short = 8;
 
 bool nt2_short(const NTParams& p, int dtype) {
-    return g_nt2_short && dtype == SEG_BF16 && !p.partial && p.K <= 128 && g_nt2_ablate == 0;
+    return dtype == SEG_BF16 && !p.partial && p.K <= 64 * g_nt2_short && g_nt2_ablate == 0;
 }
 
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s) {

@@ -133,6 +133,8 @@ class Session:
         # Dropout right after a bias-free / ReLU-free conv (FC-DenseNet's
         # Conv2D_Block + dropout) applied in the conv epilogue
         self.fuse_dropout = True
+        # DenseBlock concatenations as channel views of one block buffer
+        self.alias_concat = True
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -383,11 +385,69 @@ class Session:
         N, H, W, C = shape
         return torch.zeros(N, H, W, round8(C), dtype=self.tdt, device=self.device)
 
+    def _plan_concat_alias(self, p):
+        """Zero-copy concatenation for FC-DenseNet's DenseBlock
+        (Network/model/FCDenseNet.py:48-61), where concat i is
+        [x0, h0, ..., h_i]: every concat of the block is a channel prefix of the
+        last one.  That last concat (the root) gets one buffer; its parts are
+        channel slices of it (their producers write there through the row
+        stride) and the earlier concats are prefix views, so no concat copies
+        data.  Gradients mirror this: one buffer per root, the consumers' input
+        gradients accumulate into their slice (BatchNorm backward in
+        accumulate mode, or a copying concat's split) and the parts' producers
+        read theirs from it.
+
+        A root qualifies when every part has a multiple of 8 channels (slices
+        start on 16-byte chunks and carry no padding), is produced by a node
+        that writes through a row stride (conv, pooling, BatchNorm) and is not
+        already a slice, and every other reader of the group is a BatchNorm or
+        a (copying) concat -- the consumers whose input gradient can land in a
+        shared buffer in place."""
+        p.alias = {}          # tensor id -> (root tensor id, channel offset)
+        p.alias_nodes = set()  # ConcatV2 node ids that became views
+        if not self.alias_concat:
+            return
+        shp = p.shapes
+        producer = {id(n.output): n for n in p.nodes}
+        users = {}
+        for n in p.nodes:
+            for t in list(n.inputs) + [getattr(n, "residual", None)]:
+                if t is not None:
+                    users.setdefault(id(t), []).append(n)
+        fetched = {id(f) for f in p.fetches if isinstance(f, G.Tensor)}
+        concats = [n for n in p.nodes if n.kind == "ConcatV2"]
+        for root in reversed(concats):
+            if id(root.output) in p.alias:
+                continue
+            ids = [id(t) for t in root.inputs]
+            if len(set(ids)) != len(ids):
+                continue
+            prefixes = [c for c in concats if c is not root and id(c.output) not in p.alias and
+                        len(c.inputs) < len(ids) and [id(t) for t in c.inputs] == ids[:len(c.inputs)]]
+            ok = all(shp[i][3] % 8 == 0 and i not in p.alias and i not in fetched and
+                     producer.get(i) is not None and producer[i].kind in ("conv", "AvgPool", "MaxPool", "bn")
+                     for i in ids)
+            views = {root} | set(prefixes)
+            group = {id(c.output) for c in views} | set(ids)
+            if ok:
+                ok = all(u in views or u.kind in ("bn", "ConcatV2") for g in group for u in users.get(g, []))
+            if not ok:
+                continue
+            r, off = id(root.output), 0
+            for t in root.inputs:
+                p.alias[id(t)] = (r, off)
+                off += shp[id(t)][3]
+            for c in views:
+                p.alias[id(c.output)] = (r, 0)
+                p.alias_nodes.add(id(c))
+
     def _allocate(self, p, consumers, feeds):
         dev = self.device
         shp = p.shapes
         buf = {}            # tensor id -> device tensor (padded)
         p.buf = buf
+        self._plan_concat_alias(p)
+        roots = {r: self._act(shp[r]) for r, _ in set(p.alias.values())}
         p.feed_slots = {}   # tensor id -> (kind, staging)
         store = self.store
         ws_need = 0
@@ -433,7 +493,11 @@ class Session:
                 buf[id(y)] = src.unsqueeze(-1)
                 continue
             s = shp[id(y)]
-            buf[id(y)] = self._act(s)
+            if id(y) in p.alias:
+                r, off = p.alias[id(y)]
+                buf[id(y)] = roots[r][..., off:off + s[3]]
+            else:
+                buf[id(y)] = self._act(s)
             if n.kind == "conv":
                 x = n.inputs[0]
                 N, H, W, C = shp[id(x)]
@@ -681,8 +745,9 @@ class Session:
                 ops.softmax_xent(lg, labels, n.dlogits, n.loss_sum, n.num_classes, n.valid_hw,
                                  grad_scale=1.0 / n.count, ws=self.ws)
             elif k == "ConcatV2":
-                ops.concat_fwd([(buf[id(t)], p.shapes[id(t)][3]) for t in n.inputs], y,
-                               p.shapes[id(n.output)][3])
+                if id(n) not in p.alias_nodes:      # aliased: the parts already sit in place
+                    ops.concat_fwd([(buf[id(t)], p.shapes[id(t)][3]) for t in n.inputs], y,
+                                   p.shapes[id(n.output)][3])
             elif k == "ArgMax":
                 x = buf[id(n.inputs[0])]
                 C = p.shapes[id(n.inputs[0])][3]
@@ -823,6 +888,27 @@ class Session:
             if acc is not None:
                 ops.add(acc, dst, acc)
 
+        ginit = set()      # aliased-concat roots whose gradient buffer holds data this step
+
+        def adest(t):
+            """Slice of the root's gradient buffer for aliased t, and whether the
+            kernel must accumulate into it (False only for the first write
+            when it covers the whole root)."""
+            r, off = p.alias[id(t)]
+            dB = p.tmp.get(("ga", r))
+            if dB is None:
+                dB = torch.zeros_like(buf[r])
+                p.tmp[("ga", r)] = dB
+            C = p.shapes[id(t)][3]
+            view = dB[..., off:off + C]
+            grad[id(t)] = view
+            if r not in ginit:
+                ginit.add(r)
+                if off == 0 and C == p.shapes[r][3]:
+                    return view, False
+                dB.zero_()
+            return view, True
+
         def contribute_alias(t, g):
             if id(t) not in ng:
                 return
@@ -834,6 +920,17 @@ class Session:
         for n in reversed(p.nodes):
             k = n.kind
             if k == "input" or id(n.output) not in ng:
+                continue
+            if id(n) in p.alias_nodes:
+                # concat as a view: its parts' gradients are slices of the
+                # root's buffer, which the consumers accumulated into
+                r = p.alias[id(n.output)][0]
+                if r in ginit:
+                    dB = p.tmp[("ga", r)]
+                    for t in n.inputs:
+                        if id(t) in ng and id(t) not in grad:
+                            off = p.alias[id(t)][1]
+                            grad[id(t)] = dB[..., off:off + p.shapes[id(t)][3]]
                 continue
             if k == "xent":
                 contribute_alias(n.inputs[0], n.dlogits)
@@ -943,7 +1040,10 @@ class Session:
                             p.tmp[("cz", id(t))] = g
                         parts.append((g, p.shapes[id(t)][3], False))
                         continue
-                    if id(t) in grad:
+                    if id(t) in p.alias:
+                        v, accf = adest(t)
+                        parts.append((v, p.shapes[id(t)][3], accf))
+                    elif id(t) in grad:
                         parts.append((grad[id(t)], p.shapes[id(t)][3], True))
                     else:
                         g = p.tmp.get(("g", id(t)))
@@ -956,10 +1056,14 @@ class Session:
             elif k == "bn":
                 x = n.inputs[0]
                 C = p.shapes[id(x)][3]
-                dx, acc = dest(x)
+                if id(x) in p.alias:
+                    dx, accf = adest(x)
+                    acc = None
+                else:
+                    (dx, acc), accf = dest(x), False
                 ops.bn_relu_bwd(buf[id(x)], buf[id(n.output)], dy, dx, store.param(n.gamma.var_name),
                                 store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
-                                n.eps, ws)
+                                n.eps, ws, accumulate=accf)
                 done(dx, acc)
                 self._grad_ready([n.gamma.var_name, n.beta.var_name])
             elif k == "Relu":

@@ -32,7 +32,10 @@ def build(H, W):
     return image, labels, keep, pred, logits, loss, train_step
 
 
-def test_fcdensenet_logits_grads_adam_f32(dev):
+@pytest.mark.parametrize("alias", [True, False], ids=["concat-views", "concat-copies"])
+def test_fcdensenet_logits_grads_adam_f32(dev, alias):
+    """alias: DenseBlock concats as channel views of one buffer (default) or
+    as copies."""
     N, H, W = 1, 64, 96
     image, labels, keep, pred, logits, loss, train_step = build(H, W)
     shapes = M.fcdensenet_param_shapes(3, 2)
@@ -47,6 +50,7 @@ def test_fcdensenet_logits_grads_adam_f32(dev):
     r_logits = r_logits.detach().numpy()
 
     sess = tf.Session(compute_dtype="f32")
+    sess.alias_concat = alias
     sess.run(tf.global_variables_initializer())
     for k, v in weights.items():
         sess.assign(k, v)

@@ -42,9 +42,9 @@ def ntv(request, dev):
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
     ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
     ops.set_option("nt4", 1 if v == 9 else 0)
-    ops.set_option("nt2_short", 0 if v == 8 else 1)
+    ops.set_option("nt2_short", 0 if v == 8 else 8)
     yield v
-    ops.set_option("nt2_short", 1)
+    ops.set_option("nt2_short", 8)
     ops.set_option("nt4", 0)
     ops.set_option("nt3_fill", 1)
     ops.set_option("igemm_nt_variant", 2)
