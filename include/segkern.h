@@ -210,9 +210,11 @@ int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const float* gamma
                     int dtype, void* stream);
 /* dx = dy*(y>0)*scale; dgamma = sum(dy*(y>0)*x)/sqrt(1+eps); dbeta = sum(dy*(y>0)).
    flags: bit 0 = the forward had the ReLU (mask by y > 0), bit 1 = accumulate
-   (dx += ..., for gradients landing in a shared concat buffer). */
+   (dx += ..., for gradients landing in a shared concat buffer).  y may be
+   NULL when beta is given: the mask is then re-derived from x with the
+   forward's arithmetic (x*gamma/sqrt(1+eps) + beta > 0) and y is not read. */
 int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy,
-                    void* dx, int lddx, const float* gamma, float eps, float* dgamma,
+                    void* dx, int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
                     float* dbeta, long P, int C, int c_valid, int flags, int dtype, void* ws,
                     size_t ws_bytes, void* stream);
 /* resize_bilinear(align_corners=True) (Network/utils/utils.py:329-330). */

@@ -144,7 +144,7 @@ SIGNATURES = {
     "seg_dropout_bwd": (_I, [_P, _P, _L, _F, ctypes.c_uint64, _I, _P]),
     "seg_dropout_bwd_ch": (_I, [_P, _I, _P, _I, _L, _I, _I, _F, ctypes.c_uint64, _I, _P]),
     "seg_bn_relu_fwd": (_I, [_P, _I, _P, _I, _P, _P, _F, _L, _I, _I, _I, _I, _P]),
-    "seg_bn_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _P, _F, _P, _P, _L, _I, _I, _I, _I,
+    "seg_bn_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _F, _P, _P, _L, _I, _I, _I, _I,
                              _P, _Z, _P]),
     "seg_resize_bilinear_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_resize_bilinear_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

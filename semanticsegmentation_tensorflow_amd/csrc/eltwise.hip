@@ -513,10 +513,13 @@ __global__ __launch_bounds__(256) void bn_relu_fwd_k(const T* __restrict__ x, in
 template <typename T>
 __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, int ldx, const T* __restrict__ y, int ldy,
                                                      const T* __restrict__ dy, int lddy, T* __restrict__ dx, int lddx,
-                                                     const float* __restrict__ gamma, float inv,
-                                                     float* __restrict__ part, long P, int C, int cv, int flags) {
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float inv, float* __restrict__ part, long P, int C, int cv,
+                                                     int flags) {
+    // ReLU mask from y, or (y == null) re-derived from x with the forward's
+    // own arithmetic (x * gamma*inv + beta > 0): 2 bytes per element less
     constexpr int EPC = dt_traits<T>::EPC;
-    const bool relu = flags & 1, acc = flags & 2;
+    const bool relu = flags & 1, acc = flags & 2, remask = relu && !y;
     extern __shared__ __attribute__((aligned(16))) float red[];
     const RedGeom g = red_geom(C, EPC);
     const int t = threadIdx.x;
@@ -525,11 +528,18 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
     const long per = (P + gridDim.x - 1) / gridDim.x;
     const long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
     constexpr int MAXIT = 16 / EPC;
-    float sg[MAXIT][EPC], sb[MAXIT][EPC];
+    float sg[MAXIT][EPC], sb[MAXIT][EPC], sc[MAXIT][EPC], sh[MAXIT][EPC];
 #pragma unroll
     for (int j = 0; j < MAXIT; ++j)
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) sg[j][e] = sb[j][e] = 0.f;
+        for (int e = 0; e < EPC; ++e) {
+            sg[j][e] = sb[j][e] = 0.f;
+            // the per-lane affine, loaded once (channels >= cv: scale 0)
+            const int c = (c8 + j * g.LPP) * EPC + e;
+            const bool ok = j < g.iters && c < cv;
+            sc[j][e] = ok ? gamma[c] * inv : 0.f;
+            sh[j][e] = ok && remask ? beta[c] : 0.f;
+        }
     if (active) {
         for (long pix = p0 + prow; pix < p1; pix += g.rows) {
 #pragma unroll
@@ -539,17 +549,18 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                 if (cc >= g.CK) break;
                 float xv[EPC], yv[EPC], d[EPC], old[EPC];
                 Chunk<T>::unpack(ldc(x + pix * ldx + cc * EPC), xv);
-                Chunk<T>::unpack(ldc(y + pix * ldy + cc * EPC), yv);
+                if (relu && !remask) Chunk<T>::unpack(ldc(y + pix * ldy + cc * EPC), yv);
                 Chunk<T>::unpack(ldc(dy + pix * lddy + cc * EPC), d);
                 if (acc) Chunk<T>::unpack(ldc(dx + pix * lddx + cc * EPC), old);
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) {
                     const int c = cc * EPC + e;
+                    if (remask) yv[e] = xv[e] * sc[j][e] + sh[j][e];
                     float dz = (relu && !(yv[e] > 0.f)) ? 0.f : d[e];
                     if (c >= cv) dz = 0.f;
                     sb[j][e] += dz;
                     sg[j][e] += dz * xv[e];
-                    d[e] = c < cv ? dz * (gamma[c] * inv) : 0.f;
+                    d[e] = dz * sc[j][e];
                     if (acc) d[e] += old[e];
                 }
                 stc(dx + pix * lddx + cc * EPC, Chunk<T>::pack(d));
@@ -1046,9 +1057,11 @@ extern "C" int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const f
 }
 
 extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
-                               int lddx, const float* gamma, float eps, float* dgamma, float* dbeta, long P, int C,
-                               int cv, int flags, int dtype, void* ws, size_t ws_bytes, void* stream) {
-    if (!x || !y || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7) || (flags & ~3)) return SEG_EINVAL;
+                               int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
+                               float* dbeta, long P, int C, int cv, int flags, int dtype, void* ws, size_t ws_bytes,
+                               void* stream) {
+    if (!x || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7) || (flags & ~3)) return SEG_EINVAL;
+    if ((flags & 1) && !y && !beta) return SEG_EINVAL;
     if (C > 4096) return SEG_EINVAL;
     const int nb = red_blocks(P, C, epc_of(dtype));
     if (!ws || ws_bytes < (size_t)nb * 2 * C * sizeof(float)) return SEG_EWORKSPACE;
@@ -1058,7 +1071,7 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
     if (shm > 64 * 1024) return SEG_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)x, ldx, (const T*)y,
-                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, inv, (float*)ws, P, C, cv, flags));
+                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, beta, inv, (float*)ws, P, C, cv, flags));
     SEG_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_finish_k, dim3((cv + 7) / 8), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
     SEG_CHECK_LAUNCH();

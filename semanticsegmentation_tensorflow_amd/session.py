@@ -1063,7 +1063,7 @@ class Session:
                     (dx, acc), accf = dest(x), False
                 ops.bn_relu_bwd(buf[id(x)], buf[id(n.output)], dy, dx, store.param(n.gamma.var_name),
                                 store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
-                                n.eps, ws, accumulate=accf)
+                                n.eps, ws, accumulate=accf, beta=store.param(n.beta.var_name))
                 done(dx, acc)
                 self._grad_ready([n.gamma.var_name, n.beta.var_name])
             elif k == "Relu":

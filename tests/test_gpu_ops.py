@@ -456,6 +456,21 @@ def test_bn_relu(dev, dtype):
     assert_close(from_dev(dxd), x.grad, dtype, "bn dx")
     assert_close(dg.double().cpu(), gamma.grad, torch.float32, "dgamma", 1e-4)
     assert_close(dbt.double().cpu(), beta.grad, torch.float32, "dbeta", 1e-4)
+    # ReLU mask re-derived from x (y not read): bit-identical to the y-masked kernel
+    dx2 = torch.full_like(xd, float("nan"))
+    dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    ops.bn_relu_bwd(xd, None, to_dev(dy, dtype, dev), dx2, gd, dg2, db2, C, beta=bd)
+    # accumulate mode into a channel slice of a wider buffer (shared concat gradient)
+    wide = rnd(torch.randn(N, H, W, C + 16, generator=g, dtype=torch.float64), dtype)
+    wd = to_dev(wide, dtype, dev)
+    dg3, db3 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    ops.bn_relu_bwd(xd, None, to_dev(dy, dtype, dev), wd[..., 8:8 + C], gd, dg3, db3, C, beta=bd, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dxd) and torch.equal(dg2, dg) and torch.equal(db2, dbt)
+    ref = wide.clone()
+    ref[..., 8:8 + C] += x.grad
+    assert_close(from_dev(wd), ref, dtype, "bn dx accumulate")
+    assert torch.equal(dg3, dg)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
