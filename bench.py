@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "train images/sec on KITTI 375×1242 2-class at 1/2/4/8 MI355X; mIoU parity"
 PEAK = {"bf16": 2.5e15, "f32": 157.3e12}          # dense MFMA peaks (MI355X_MICROARCH.md)
+HBM_PEAK = 8.0e12                                  # HBM3E bytes/s (MI355X_MICROARCH.md)
 FCN_TRAIN_FLOP_PER_IMG = 1348.97e9                 # SURVEY.md 8d at 384x1248, C_in=3
 
 
@@ -380,25 +381,33 @@ def main():
     per = {}
     step_conv_flops = 0.0
     rows = []
+    esz = 2 if args.dtype == "bf16" else 4
     for desc, op, s, e in sess.timer:
         name, splits, flops = ops.conv_kernel_info(desc, op)
         ms = s.elapsed_time(e)
         step_conv_flops += flops
+        # algorithmic HBM bytes: input + output activations once, the filter once
+        # (fp32 filter gradient for the wgrad ops)
+        nbytes = esz * (desc.N * desc.H * desc.W * desc.c_valid + desc.N * desc.OH * desc.OW * desc.k_valid) \
+            + (4 if op in (ops.OP_BWD_FILTER, ops.OP_TBWD_FILTER) else esz) * desc.R * desc.S * desc.c_valid * desc.k_valid
         rows.append((name, op, splits, flops, ms, desc.N, desc.H, desc.W, desc.c_valid, desc.k_valid, desc.R))
-        a = per.setdefault(name, [0, 0.0, 0.0])
+        a = per.setdefault(name, [0, 0.0, 0.0, 0.0])
         a[0] += 1
         a[1] += flops
         a[2] += ms
+        a[3] += nbytes
     sess.timer = None
     dom = max(per.items(), key=lambda kv: kv[1][2])
-    dname, (dn, dflops, dms) = dom
+    dname, (dn, dflops, dms, dbytes) = dom
     achieved = (dflops / dn) / (dms / dn * 1e-3)
+    # roofline bound of the dominant kernel group from its arithmetic intensity
+    hbm_bound = dflops / dbytes < PEAK[args.dtype] / HBM_PEAK
     if args.kernel_table and rank == 0:
         for r in rows:
             print("KERNEL %-26s op=%d split=%-3d GF=%8.2f ms=%8.3f TF/s=%7.1f N=%d %dx%d C=%d K=%d R=%d"
                   % (r[0], r[1], r[2], r[3] / 1e9, r[4], r[3] / r[4] / 1e9, *r[5:]), file=sys.stderr)
-        for k, (n, f, m) in sorted(per.items(), key=lambda kv: -kv[1][2]):
-            print(f"GROUP {k}: launches={n} ms={m:.3f} TF/s={f / m / 1e9:.1f}", file=sys.stderr)
+        for k, (n, f, m, b) in sorted(per.items(), key=lambda kv: -kv[1][2]):
+            print(f"GROUP {k}: launches={n} ms={m:.3f} TF/s={f / m / 1e9:.1f} GB/s={b / m / 1e6:.0f}", file=sys.stderr)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = B * world * args.steps / elapsed
@@ -439,6 +448,20 @@ def main():
             "traffic": None,
             "launches_per_step": dn,
             "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
+            "algorithmic_bytes_per_launch": round(dbytes / dn),
+            "avg_launch_ms": round(dms / dn, 4),
+        } if not hbm_bound else {
+            "bound": "hbm",
+            "kernel": dname,
+            "achieved": round(dbytes / dn / (dms / dn * 1e-3) / 1e9, 1),
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": round(dbytes / (dms * 1e-3) / HBM_PEAK, 4),
+            "traffic": None,
+            "launches_per_step": dn,
+            "algorithmic_bytes_per_launch": round(dbytes / dn),
+            "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
+            "mfma_frac": round(achieved / peak, 4),
             "avg_launch_ms": round(dms / dn, 4),
         },
         "step_mfma_frac": round((FCN_TRAIN_FLOP_PER_IMG * B if args.model == "fcn" else step_conv_flops)
