@@ -268,24 +268,36 @@ __global__ void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n, fl
 
 // TF1 dropout gradient of a conv whose forward epilogue applied the dropout
 // (no ReLU after it): element (pixel p, channel c < cv) uses the epilogue's
-// counter index p * cv + c; padding channels are zeroed.
+// counter index p * cv + c; padding channels are zeroed.  Lanes own fixed
+// 8-channel chunks and walk pixels (bn_relu_fwd_k's geometry): the flat
+// element loop paid a 64-bit division per 16-byte chunk.
 template <typename T>
-__global__ void dropout_ch_k(const T* __restrict__ dy, int ldy, T* __restrict__ dz, int ldz, long P, int C, int cv,
-                             float kp, uint64_t seed) {
+__global__ __launch_bounds__(256) void dropout_ch_k(const T* __restrict__ dy, int ldy, T* __restrict__ dz, int ldz,
+                                                    long P, int C, int cv, float kp, uint64_t seed) {
     constexpr int EPC = dt_traits<T>::EPC;
-    const int chunks = C / EPC;
-    const long total = P * chunks;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long p = i / chunks;
-        const int c0 = (int)(i - p * chunks) * EPC;
-        float v[EPC];
-        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(dy + p * ldy + c0), v);
+    constexpr int MAXIT = 16 / EPC;
+    const RedGeom g = red_geom(C, EPC);
+    const int t = threadIdx.x;
+    const int c8 = t % g.LPP, prow = t / g.LPP;
+    if (prow >= g.rows) return;
+    const float rkp = 1.f / kp;
+    const long step = (long)gridDim.x * g.rows;
+    for (long pix = (long)blockIdx.x * g.rows + prow; pix < P; pix += step) {
+        const uint64_t base = (uint64_t)pix * cv;
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) {
-            const int c = c0 + e;
-            v[e] = c < cv ? seg_dropout(v[e], kp, seed, (uint64_t)p * cv + c) : 0.f;
+        for (int j = 0; j < MAXIT; ++j) {
+            if (j >= g.iters) break;
+            const int cc = c8 + j * g.LPP;
+            if (cc >= g.CK) break;
+            float v[EPC];
+            Chunk<T>::unpack(ldc(dy + pix * ldy + cc * EPC), v);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                const int c = cc * EPC + e;
+                v[e] = c < cv ? (v[e] * rkp) * floorf(kp + seg_uniform(seed, base + c)) : 0.f;
+            }
+            stc(dz + pix * ldz + cc * EPC, Chunk<T>::pack(v));
         }
-        *reinterpret_cast<uint4*>(dz + p * ldz + c0) = Chunk<T>::pack(v);
     }
 }
 
@@ -924,8 +936,10 @@ extern "C" int seg_dropout_bwd(const void* dy, void* dx, long n, float kp, uint6
 extern "C" int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C, int cv, float kp,
                                   uint64_t seed, int dtype, void* stream) {
     if (!dy || !dz || !(kp > 0.f) || kp > 1.f || (C & 7) || cv > C || ldy < C || ldz < C) return SEG_EINVAL;
-    const long total = P * (C / epc_of(dtype));
-    DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+    if (C > 4096) return SEG_EINVAL;
+    const RedGeom g = red_geom(C, epc_of(dtype));
+    const long blocks = std::max<long>(1, std::min<long>((P + g.rows - 1) / g.rows, 16384));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_k<T>, dim3((unsigned)blocks), dim3(256), 0,
                                          (hipStream_t)stream, (const T*)dy, ldy, (T*)dz, ldz, P, C, cv, kp, seed));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
