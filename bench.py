@@ -48,7 +48,9 @@ def parse():
                     help="fcn 0.8 (FCN.py:395), fcdensenet 0.2 (FCDenseNet.py:13)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 side lines")
+    ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--kernel-table", action="store_true", help="print per-launch timings to stderr")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
@@ -95,7 +97,9 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
     import torch
     from oracle import models as M
     from oracle import tf1_ops as T
-    threads = min(16, os.cpu_count() or 1)
+    # every core this job is allotted: the GPU box gives one GPU's job 16 CPUs
+    # (OMP_NUM_THREADS=16 there; nproc / os.cpu_count() report the whole host)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
     shapes = {"fcn": M.fcn_param_shapes, "fcdensenet": M.fcdensenet_param_shapes,
@@ -296,6 +300,138 @@ def pmc_traffic(argv, symbol, out_dir):
     return res
 
 
+DEFAULTS = {  # per model: (H, W, batch per GPU, keep_prob)
+    "fcn": (375, 1242, 4, 0.8),            # C2 (C4 under torchrun); FCN.py:395 keep_prob 0.8
+    "fcdensenet": (375, 1242, 8, 0.2),     # C3; FCDenseNet.py KEEP_PROB
+    "deeplab": (1024, 2048, 2, 0.9),       # C5, Cityscapes-shaped
+}
+WORKLOAD = {"fcn": "FCN (reference Network/model/FCN.py topology)",
+            "fcdensenet": "FC-DenseNet 'U-Net' (reference Network/model/FCDenseNet.py topology)",
+            "deeplab": "DeepLab-style atrous VGG16 + ASPP (rates 6/12/18, image pooling) + bilinear x8 "
+                       "(semanticsegmentation_tensorflow_amd/deeplab.py; config C5)"}
+
+
+def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, fuse_adam=True,
+            overlap_optimizer=False, want_miou=False):
+    """Build `model`'s training graph, run `warmup` + `steps` timed train steps
+    on a synthetic batch resident in HBM, then one more step with HIP events
+    around every conv launch (on its launch stream) for the per-kernel
+    roofline.  Returns the measurement dict (no printing)."""
+    import torch
+    import torch.distributed as dist
+    from semanticsegmentation_tensorflow_amd import graph as G
+    from semanticsegmentation_tensorflow_amd import ops, tf
+    from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
+    from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
+    from semanticsegmentation_tensorflow_amd.fcn import FCN
+
+    world = dp.world if dp is not None else 1
+    HP, WP = pad32(H), pad32(W)
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
+    labels = tf.placeholder(tf.uint8, [None, HP, WP], name="annotation")
+    keep = tf.placeholder(tf.float32, name="keep_probability")
+    if model == "fcn":
+        pred, logits = FCN(image, keep, 2).create()
+    elif model == "deeplab":
+        pred, logits = DeepLabASPP(image, keep, 2)
+    else:
+        pred, logits = FCDenseNet(image, keep, 2)
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
+                                                                   valid_hw=(H, W)))
+    train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = tf.Session(compute_dtype=dtype, seed=0, data_parallel=dp, overlap_optimizer=overlap_optimizer,
+                      fuse_adam=fuse_adam)
+    sess.run(tf.global_variables_initializer())
+    img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
+    feed = {image: img, labels: lab, keep: kp}
+
+    for _ in range(warmup):
+        sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    if dp:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    if dp:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dp:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    out = {"elapsed": elapsed, "loss": float(sess.run(loss, feed_dict=feed)), "HP": HP, "WP": WP}
+    if want_miou:
+        try:
+            out["miou"] = miou_parity(sess, pred, image, keep, img, lab, H, W, model)
+        except Exception as exc:  # report, never crash the headline line
+            out["miou"] = {"error": repr(exc)}
+
+    # ---- per-kernel timing (HIP events on the launch stream) for the roofline
+    sess.timer = []
+    sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    per = {}
+    step_conv_flops = 0.0
+    rows = []
+    esz = 2 if dtype == "bf16" else 4
+    for desc, op, s_ev, e_ev in sess.timer:
+        name, splits, flops = ops.conv_kernel_info(desc, op)
+        ms = s_ev.elapsed_time(e_ev)
+        step_conv_flops += flops
+        # algorithmic HBM bytes: input + output activations once, the filter once
+        # (fp32 filter gradient for the wgrad ops)
+        nbytes = esz * (desc.N * desc.H * desc.W * desc.c_valid + desc.N * desc.OH * desc.OW * desc.k_valid) \
+            + (4 if op in (ops.OP_BWD_FILTER, ops.OP_TBWD_FILTER) else esz) * desc.R * desc.S * desc.c_valid * desc.k_valid
+        rows.append((name, op, splits, flops, ms, desc.N, desc.H, desc.W, desc.c_valid, desc.k_valid, desc.R))
+        a = per.setdefault(name, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += flops
+        a[2] += ms
+        a[3] += nbytes
+    sess.timer = None
+    dname, (dn, dflops, dms, dbytes) = max(per.items(), key=lambda kv: kv[1][2])
+    achieved = (dflops / dn) / (dms / dn * 1e-3)
+    peak = PEAK[dtype]
+    # roofline bound of the dominant kernel group from its arithmetic intensity
+    hbm_bound = dflops / dbytes < peak / HBM_PEAK
+    if hbm_bound:
+        roof = {"bound": "hbm", "kernel": dname, "achieved": round(dbytes / dn / (dms / dn * 1e-3) / 1e9, 1),
+                "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(dbytes / (dms * 1e-3) / HBM_PEAK, 4),
+                "traffic": None, "launches_per_step": dn, "algorithmic_bytes_per_launch": round(dbytes / dn),
+                "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3), "mfma_frac": round(achieved / peak, 4),
+                "avg_launch_ms": round(dms / dn, 4)}
+    else:
+        roof = {"bound": "mfma", "kernel": dname, "achieved": round(achieved / 1e12, 2),
+                "peak": round(peak / 1e12, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": None, "launches_per_step": dn, "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
+                "algorithmic_bytes_per_launch": round(dbytes / dn), "avg_launch_ms": round(dms / dn, 4)}
+    ms_per_step = elapsed / steps * 1e3
+    step_flops = FCN_TRAIN_FLOP_PER_IMG * B if (model == "fcn" and (HP, WP) == (384, 1248)) else step_conv_flops
+    out.update({"value": B * world * steps / elapsed, "ms_per_step": ms_per_step, "roofline": roof,
+                "step_mfma_frac": step_flops / (ms_per_step * 1e-3) / peak,
+                "conv_gflop_per_step": step_conv_flops / 1e9, "rows": rows, "groups": per})
+    del sess
+    torch.cuda.empty_cache()
+    return out
+
+
+def extra_config(model, dtype, device, steps, warmup):
+    """C3 / C5 measured in the same run as the headline (a reported side line;
+    the headline metric stays C2)."""
+    H, W, B, kp = DEFAULTS[model]
+    m = measure(model, B, H, W, kp, steps, warmup, dtype, device)
+    return {"config": {"workload": WORKLOAD[model], "batch": B, "image": f"{H}x{W} -> {m['HP']}x{m['WP']}",
+                       "keep_prob": kp},
+            "value": round(m["value"], 3), "unit": "images/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(m["ms_per_step"], 3), "dtype": dtype,
+            "step_mfma_frac": round(m["step_mfma_frac"], 4), "roofline": m["roofline"]}
+
+
 def main():
     args = parse()
     import torch
@@ -312,125 +448,43 @@ def main():
         from semanticsegmentation_tensorflow_amd.dp import DataParallel
         dp = DataParallel(bucket_mb=args.bucket_mb)
 
-    from semanticsegmentation_tensorflow_amd import graph as G
-    from semanticsegmentation_tensorflow_amd import ops, tf
-    from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
-    from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
-    from semanticsegmentation_tensorflow_amd.fcn import FCN
-
+    from semanticsegmentation_tensorflow_amd import ops
     for kv in args.option:
         name, val = kv.split("=")
         ops.set_option(name, int(val))
-    H = args.height or (1024 if args.model == "deeplab" else 375)
-    W = args.width or (2048 if args.model == "deeplab" else 1242)
-    HP, WP = pad32(H), pad32(W)
-    B = args.batch or {"fcn": 4, "fcdensenet": 8, "deeplab": 2}[args.model]
-    kp = args.keep_prob if args.keep_prob is not None else {"fcn": 0.8, "fcdensenet": 0.2, "deeplab": 0.9}[args.model]
-    G.reset_default_graph()
-    image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
-    labels = tf.placeholder(tf.uint8, [None, HP, WP], name="annotation")
-    keep = tf.placeholder(tf.float32, name="keep_probability")
-    if args.model == "fcn":
-        pred, logits = FCN(image, keep, 2).create()
-    elif args.model == "deeplab":
-        pred, logits = DeepLabASPP(image, keep, 2)
-    else:
-        pred, logits = FCDenseNet(image, keep, 2)
-    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels,
-                                                                   valid_hw=(H, W)))
-    train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
-    sess = tf.Session(compute_dtype=args.dtype, seed=0, data_parallel=dp,
-                      overlap_optimizer=args.overlap_optimizer,
-                      fuse_adam=not args.no_fuse_adam)
-    sess.run(tf.global_variables_initializer())
-    img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
-    feed = {image: img, labels: lab, keep: kp}
-
-    for _ in range(args.warmup):
-        sess.run(train_step, feed_dict=feed)
-    torch.cuda.synchronize()
-    if dp:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sess.run(train_step, feed_dict=feed)
-    torch.cuda.synchronize()
-    if dp:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    dH, dW, dB, dkp = DEFAULTS[args.model]
+    H, W = args.height or dH, args.width or dW
+    B = args.batch or dB
+    kp = args.keep_prob if args.keep_prob is not None else dkp
+    m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, rank,
+                fuse_adam=not args.no_fuse_adam, overlap_optimizer=args.overlap_optimizer,
+                want_miou=rank == 0 and not args.no_miou and not args.pmc_child)
     if args.pmc_child:
         return
-    if dp:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    loss_val = float(sess.run(loss, feed_dict=feed))
-    miou = None
-    if rank == 0 and not args.no_miou:
-        try:
-            miou = miou_parity(sess, pred, image, keep, img, lab, H, W, args.model)
-        except Exception as exc:  # report, never crash the headline line
-            miou = {"error": repr(exc)}
-
-    # ---- per-kernel timing (HIP events on the launch stream) for the roofline
-    sess.timer = []
-    sess.run(train_step, feed_dict=feed)
-    torch.cuda.synchronize()
-    per = {}
-    step_conv_flops = 0.0
-    rows = []
-    esz = 2 if args.dtype == "bf16" else 4
-    for desc, op, s, e in sess.timer:
-        name, splits, flops = ops.conv_kernel_info(desc, op)
-        ms = s.elapsed_time(e)
-        step_conv_flops += flops
-        # algorithmic HBM bytes: input + output activations once, the filter once
-        # (fp32 filter gradient for the wgrad ops)
-        nbytes = esz * (desc.N * desc.H * desc.W * desc.c_valid + desc.N * desc.OH * desc.OW * desc.k_valid) \
-            + (4 if op in (ops.OP_BWD_FILTER, ops.OP_TBWD_FILTER) else esz) * desc.R * desc.S * desc.c_valid * desc.k_valid
-        rows.append((name, op, splits, flops, ms, desc.N, desc.H, desc.W, desc.c_valid, desc.k_valid, desc.R))
-        a = per.setdefault(name, [0, 0.0, 0.0, 0.0])
-        a[0] += 1
-        a[1] += flops
-        a[2] += ms
-        a[3] += nbytes
-    sess.timer = None
-    dom = max(per.items(), key=lambda kv: kv[1][2])
-    dname, (dn, dflops, dms, dbytes) = dom
-    achieved = (dflops / dn) / (dms / dn * 1e-3)
-    # roofline bound of the dominant kernel group from its arithmetic intensity
-    hbm_bound = dflops / dbytes < PEAK[args.dtype] / HBM_PEAK
+    HP, WP = m["HP"], m["WP"]
     if args.kernel_table and rank == 0:
-        for r in rows:
+        for r in m["rows"]:
             print("KERNEL %-26s op=%d split=%-3d GF=%8.2f ms=%8.3f TF/s=%7.1f N=%d %dx%d C=%d K=%d R=%d"
                   % (r[0], r[1], r[2], r[3] / 1e9, r[4], r[3] / r[4] / 1e9, *r[5:]), file=sys.stderr)
-        for k, (n, f, m, b) in sorted(per.items(), key=lambda kv: -kv[1][2]):
-            print(f"GROUP {k}: launches={n} ms={m:.3f} TF/s={f / m / 1e9:.1f} GB/s={b / m / 1e6:.0f}", file=sys.stderr)
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
-    peak = PEAK[args.dtype]
+        for k, (n, f, ms, b) in sorted(m["groups"].items(), key=lambda kv: -kv[1][2]):
+            print(f"GROUP {k}: launches={n} ms={ms:.3f} TF/s={f / ms / 1e9:.1f} GB/s={b / ms / 1e6:.0f}",
+                  file=sys.stderr)
+    dname = m["roofline"]["kernel"]
     result = {
         "metric": METRIC,
-        "value": round(value, 3),
+        "value": round(m["value"], 3),
         "unit": "images/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": round(m["ms_per_step"], 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic",
         "config": {
-            "workload": {"fcn": "FCN (reference Network/model/FCN.py topology)",
-                         "fcdensenet": "FC-DenseNet 'U-Net' (reference Network/model/FCDenseNet.py topology)",
-                         "deeplab": "DeepLab-style atrous VGG16 + ASPP (rates 6/12/18) + bilinear x8 "
-                                    "(semanticsegmentation_tensorflow_amd/deeplab.py; config C5)"}[args.model]
-                        + f" train step: fwd + softmax-xent + bwd + TF1 Adam, {H}x{W}x3"
+            "workload": WORKLOAD[args.model] + f" train step: fwd + softmax-xent + bwd + TF1 Adam, {H}x{W}x3"
                         + (f" zero-padded to {HP}x{WP}" if (HP, WP) != (H, W) else ""),
             "global_batch": B * world,
             "batch_per_gpu": B,
@@ -438,38 +492,11 @@ def main():
             "parallelism": f"dp{world}",
             "keep_prob": kp,
         },
-        "roofline": {
-            "bound": "mfma",
-            "kernel": dname,
-            "achieved": round(achieved / 1e12, 2),
-            "peak": round(peak / 1e12, 1),
-            "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4),
-            "traffic": None,
-            "launches_per_step": dn,
-            "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
-            "algorithmic_bytes_per_launch": round(dbytes / dn),
-            "avg_launch_ms": round(dms / dn, 4),
-        } if not hbm_bound else {
-            "bound": "hbm",
-            "kernel": dname,
-            "achieved": round(dbytes / dn / (dms / dn * 1e-3) / 1e9, 1),
-            "peak": HBM_PEAK / 1e9,
-            "unit": "GB/s",
-            "frac": round(dbytes / (dms * 1e-3) / HBM_PEAK, 4),
-            "traffic": None,
-            "launches_per_step": dn,
-            "algorithmic_bytes_per_launch": round(dbytes / dn),
-            "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
-            "mfma_frac": round(achieved / peak, 4),
-            "avg_launch_ms": round(dms / dn, 4),
-        },
-        "step_mfma_frac": round((FCN_TRAIN_FLOP_PER_IMG * B if args.model == "fcn" else step_conv_flops)
-                                / (ms_per_step * 1e-3) / peak, 4)
-        if (HP, WP) == (384, 1248) or args.model != "fcn" else None,
-        "conv_gflop_per_step_measured": round(step_conv_flops / 1e9, 2),
-        "loss_after": round(loss_val, 5),
-        "miou_parity": miou,
+        "roofline": m["roofline"],
+        "step_mfma_frac": round(m["step_mfma_frac"], 4),
+        "conv_gflop_per_step_measured": round(m["conv_gflop_per_step"], 2),
+        "loss_after": round(m["loss"], 5),
+        "miou_parity": m.get("miou"),
     }
     if rank == 0 and world == 1 and not args.no_pipeline and args.model == "fcn":
         try:
@@ -480,7 +507,7 @@ def main():
         try:
             argv = [a for a in sys.argv[1:] if a not in ("--kernel-table",)]
             argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-miou",
-                           "--no-pipeline"]
+                           "--no-pipeline", "--no-extra"]
             t = pmc_traffic(argv, kernel_symbol(dname), os.path.join(ROOT, "gpurun_out", "bench_pmc"))
             result["roofline"]["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
             result["roofline"]["traffic_detail"] = {
@@ -489,9 +516,19 @@ def main():
                 "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes; FETCH_SIZE doubled (gfx950)"}
         except Exception as exc:  # report, never crash the headline line
             result["roofline"]["traffic_error"] = repr(exc)
+    if rank == 0 and world == 1 and args.model == "fcn" and not args.no_extra:
+        # C3 and C5 in the same run (side lines; the headline stays C2)
+        for key, model in (("c3_fcdensenet", "fcdensenet"), ("c5_deeplab", "deeplab")):
+            try:
+                result[key] = extra_config(model, args.dtype, device, args.extra_steps, 3)
+            except Exception as exc:  # report, never crash the headline line
+                result[key] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps, args.model)
+            if args.model == "fcn":
+                # the FCN driver's own default training shape (Network/model/FCN.py:24)
+                result["cpu_baseline_160x576"] = cpu_baseline(160, 576, 160, 576, args.cpu_steps, "fcn")
         except Exception as exc:  # report, never crash the headline line
             result["cpu_baseline"] = {"value": None, "error": repr(exc)}
     if rank == 0:

@@ -334,7 +334,9 @@ typedef struct seg_adam_segment {
     void* tr_dst;
     int tr_ap, tr_bp;
 } seg_adam_segment;
-/* Host-side: fills tile_begin; returns the total tile count (< 0 on error). */
+/* Host-side: fills tile_begin.  The one entry point that returns a count:
+ * the total tile count (>= 0), or -SEG_EINVAL (the negated status code) when a
+ * segment is malformed. */
 int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs);
 /* dev_segs: the planned table copied to device memory. */
 int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_adam_segment* dev_segs,
@@ -371,6 +373,10 @@ int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void
 
 /* ---- misc ---------------------------------------------------------------- */
 int seg_fill(void* y, long n, float value, int dtype, void* stream);
+/* y += alpha * x over n fp32 elements: the accumulate-then-apply template's
+ * `accum.assign_add(tf.scalar_mul(const, grad))` (Network/main.py:92-95,
+ * Network/model/FCDenseNet.py:213). */
+int seg_axpy(float* y, const float* x, float alpha, long n, void* stream);
 int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);
 const char* seg_status_string(int status);
 int seg_version(void);

@@ -155,7 +155,10 @@ def fcdensenet_param_shapes(in_channels=3, num_classes=2):
     return shapes
 
 
-def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
+def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
+    """`quant` as in fcn_forward: applied where the device stores an activation
+    (conv / BN+ReLU / avg-pool / transposed-conv outputs; concats copy)."""
+    q = quant or (lambda t: t)
     bn = _BNCounter()
 
     def BN(h):
@@ -163,12 +166,12 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
         return tf.batch_norm_frozen(h, p[f"{n}/gamma"], p[f"{n}/beta"])
 
     def conv(h, name):
-        return tf.conv2d(h, p[f"{name}/weights"])
+        return q(tf.conv2d(h, p[f"{name}/weights"]))
 
     def bottleneck(h, name):                       # FCDenseNet.py:23-35
-        h = conv(tf.relu(BN(h)), f"{name}_conv1")
+        h = conv(q(tf.relu(BN(h))), f"{name}_conv1")
         h = tf.dropout(h, keep_prob)
-        h = conv(tf.relu(BN(h)), f"{name}_conv2")
+        h = conv(q(tf.relu(BN(h))), f"{name}_conv2")
         return tf.dropout(h, keep_prob)
 
     def dense_block(h, nl, name):                  # FCDenseNet.py:48-61
@@ -182,9 +185,9 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
         return tf.concat(feats)
 
     def transition(h, name):                       # FCDenseNet.py:37-46
-        h = tf.relu(BN(h))
+        h = q(tf.relu(BN(h)))
         h = conv(h, f"{name}_conv")
-        return tf.avg_pool2x2(h)
+        return q(tf.avg_pool2x2(h))
 
     h = conv(x, "dense_init")
     dbs = []
@@ -195,7 +198,7 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2):
             h = transition(h, f"transition_layer{b + 1}")
     for u in range(5):                              # FCDenseNet.py:141-154
         skip = dbs[4 - u]
-        t = tf.conv2d_transpose(h, p[f"transition_up{u + 1}/weights"], tuple(skip.shape), 2)
+        t = q(tf.conv2d_transpose(h, p[f"transition_up{u + 1}/weights"], tuple(skip.shape), 2))
         h = tf.concat([t, skip])
     logits = conv(h, "final_conv")
     pred = tf.argmax(logits).unsqueeze(-1)

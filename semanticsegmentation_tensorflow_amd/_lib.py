@@ -168,6 +168,7 @@ SIGNATURES = {
     "seg_adam_tf1_pack": (_I, [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _I, _F, _I, _P]),
     "seg_fill": (_I, [_P, _L, _F, _I, _P]),
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
+    "seg_axpy": (_I, [_P, _P, _F, _L, _P]),
     "seg_status_string": (ctypes.c_char_p, [_I]),
     "seg_version": (_I, []),
 }

@@ -307,6 +307,12 @@ __global__ void fill_k(T* y, long n, float v) {
         y[i] = from_f32<T>(v);
 }
 
+// y += alpha * x, fp32 (accumulate template: accum.assign_add(const * g), Network/main.py:92-95)
+__global__ void axpy_k(float* __restrict__ y, const float* __restrict__ x, float alpha, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = fmaf(alpha, x[i], y[i]);
+}
+
 template <typename A, typename B>
 __global__ void cast_k(const A* __restrict__ x, B* __restrict__ y, long n) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -949,6 +955,14 @@ extern "C" int seg_fill(void* y, long n, float v, int dtype, void* stream) {
     if (!y) return SEG_EINVAL;
     DISPATCH_T(dtype, hipLaunchKernelGGL(fill_k<T>, dim3(seg_grid_1d(n, 256)), dim3(256), 0, (hipStream_t)stream,
                                          (T*)y, n, v));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_axpy(float* y, const float* x, float alpha, long n, void* stream) {
+    if (!y || !x || n < 0) return SEG_EINVAL;
+    if (n == 0) return SEG_OK;
+    hipLaunchKernelGGL(axpy_k, dim3(seg_grid_1d(n, 256)), dim3(256), 0, (hipStream_t)stream, y, x, alpha, n);
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

@@ -27,44 +27,59 @@ class DataParallel:
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.buckets = []
         self.var_bucket = {}
+        self.var_buckets = {}
         self.store = None
-        # optional hook (work_or_None, var_names) called as each bucket's
-        # all-reduce is issued: the Session runs that bucket's Adam update on a
-        # side stream once the collective completes
+        # optional hook (works, var_names) called as each bucket's all-reduce
+        # is issued, with the variables whose last piece it carries and the
+        # collectives covering them: the Session runs their Adam update on a
+        # side stream once those complete
         self.on_launch = None
 
     def prepare(self, store):
-        """Cut the flat gradient buffer into contiguous buckets (backward order)."""
+        """Cut the flat gradient buffer into contiguous buckets of at most
+        bucket_bytes (backward order).  A variable larger than a bucket is
+        chunked (conv6's 411 MB filter gradient -> 64 MB all-reduces), so its
+        first bytes leave while the rest are still queued; a bucket is ready
+        once every variable with a piece in it is."""
         if self.store is store and self.buckets:
             return
         self.store = store
-        self.buckets = []
-        self.var_bucket = {}
-        cur, start, nbytes = [], None, 0
-        for v in store.order:
-            name = v.var_name
-            off = store.offset[name]
-            n = 1
-            for s in v.shape:
-                n *= int(s)
-            if cur and nbytes + 4 * n > self.bucket_bytes:
-                self.buckets.append((start, off, cur))
-                cur, start, nbytes = [], None, 0
-            if start is None:
-                start = off
-            cur.append(name)
-            nbytes += 4 * n
+        cap = max(1, self.bucket_bytes // 4)              # fp32 elements per bucket
+        spans = []                                        # (name, start, end) in backward order
+        order = list(store.order)
+        for i, v in enumerate(order):
+            s0 = store.offset[v.var_name]
+            e0 = store.offset[order[i + 1].var_name] if i + 1 < len(order) else store.numel
+            spans.append((v.var_name, s0, e0))
+        self.buckets = []                                 # (start, end, [names with a piece here])
+        cur, start, fill = [], None, 0
+        for name, s0, e0 in spans:
+            pos = s0
+            while pos < e0:
+                if start is None:
+                    start = pos
+                take = min(e0 - pos, cap - fill)
+                if not cur or cur[-1] != name:
+                    cur.append(name)
+                pos += take
+                fill += take
+                if fill >= cap:
+                    self.buckets.append((start, pos, cur))
+                    cur, start, fill = [], None, 0
         if cur:
             self.buckets.append((start, store.numel, cur))
+        self.var_buckets = {}
         for i, (_, _, names) in enumerate(self.buckets):
             for nm in names:
-                self.var_bucket[nm] = i
+                self.var_buckets.setdefault(nm, []).append(i)
+        self.var_bucket = {nm: b[-1] for nm, b in self.var_buckets.items()}   # bucket holding its last piece
         self._reset()
 
     def _reset(self):
         self.remaining = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
+        self.bucket_work = [None] * len(self.buckets)
 
     def _launch(self, i):
         s, e, names = self.buckets[i]
@@ -73,24 +88,25 @@ class DataParallel:
             w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
                                 async_op=True)
             self.works.append(w)
+        self.bucket_work[i] = w
         self.launched[i] = True
         if self.on_launch is not None:
-            self.on_launch(w, names)
+            done = [nm for nm in names if self.var_bucket[nm] == i]     # variables complete with this bucket
+            if done:
+                works = [self.bucket_work[j] for nm in done for j in self.var_buckets[nm]]
+                self.on_launch([x for x in works if x is not None], done)
 
     def ready(self, names):
         for nm in names:
-            i = self.var_bucket.get(nm)
-            if i is None:
-                continue
-            self.remaining[i] -= 1
-            # launch strictly in bucket order so every rank issues the same sequence
-            if self.remaining[i] == 0:
-                j = 0
-                while j < len(self.buckets) and self.launched[j]:
-                    j += 1
-                while j < len(self.buckets) and self.remaining[j] <= 0 and not self.launched[j]:
-                    self._launch(j)
-                    j += 1
+            for i in self.var_buckets.get(nm, ()):
+                self.remaining[i] -= 1
+        # launch strictly in bucket order so every rank issues the same sequence
+        j = 0
+        while j < len(self.buckets) and self.launched[j]:
+            j += 1
+        while j < len(self.buckets) and self.remaining[j] <= 0 and not self.launched[j]:
+            self._launch(j)
+            j += 1
 
     def finish(self):
         for i in range(len(self.buckets)):

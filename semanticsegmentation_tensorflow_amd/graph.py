@@ -138,6 +138,24 @@ class Variable(Tensor):
     def __repr__(self):
         return f"<Variable {self.var_name} {self.shape}>"
 
+    # --- the tf.Variable methods the accumulate-then-apply template uses
+    # (Network/main.py:78-95, Network/model/FCDenseNet.py:204-213)
+    def initialized_value(self):
+        return self
+
+    def value(self):
+        return self
+
+    def assign(self, value, name=None):
+        """`var.assign(value)`: value a tf.zeros_like / tf.constant / number."""
+        ins = [self] + ([value] if isinstance(value, Tensor) else [])
+        return Op("Assign", ins, {"var": self, "value": value}, name or "Assign")
+
+    def assign_add(self, value, name=None):
+        """`var.assign_add(value)`: value a gradient from compute_gradients,
+        optionally through tf.scalar_mul."""
+        return Op("AssignAdd", [self, value], {"var": self, "value": value}, name or "AssignAdd")
+
 
 # ---------------------------------------------------------------------------
 # initializers (Network/model/FCN.py:125-127)
@@ -196,6 +214,72 @@ def get_variable(name, shape, initializer=None, trainable=True):
                  trainable)
     g.variables[full] = v
     return v
+
+
+def Variable_(initial_value=0, trainable=True, name=None, dtype=None):
+    """tf.Variable(initial_value, trainable=..., name=...): the reference's
+    gradient accumulators `tf.Variable(tf.zeros_like(v.initialized_value()),
+    trainable=False)` (Network/main.py:78-81) and `global_step =
+    tf.Variable(0, trainable=False, name='global_step')`
+    (Network/model/FCDenseNet.py:247).  Created at the root scope."""
+    g = get_default_graph()
+    if isinstance(initial_value, Tensor):
+        if initial_value.op.type not in ("ZerosLike", "Const"):
+            raise NotImplementedError("tf.Variable initial_value must be tf.zeros_like(...), a "
+                                      "tf.constant or a number")
+        shape = tuple(initial_value.shape or ())
+        if initial_value.op.type == "ZerosLike":
+            init = constant_initializer(0.0)
+        else:
+            val = initial_value.op.attrs["value"]
+            init = lambda s, _v=val: _np_full(s, _v)  # noqa: E731
+    else:
+        import numpy as _np
+        arr = _np.asarray(initial_value, dtype=_np.float64)
+        shape = arr.shape
+        init = lambda s, _v=arr: _np_full(s, _v)  # noqa: E731
+    full = g.unique(name or "Variable")
+    v = Variable(full, shape, init, trainable)
+    v.dtype = dtype or (int64 if (not isinstance(initial_value, Tensor) and isinstance(initial_value, int))
+                        else float32)
+    g.variables[full] = v
+    return v
+
+
+def _np_full(shape, v):
+    import numpy as _np
+    return _np.broadcast_to(_np.asarray(v, dtype=_np.float32), shape).copy()
+
+
+def zeros_like(t, name=None):
+    op = Op("ZerosLike", [t], {}, name)
+    op.outputs[0].shape = t.shape
+    return op.outputs[0]
+
+
+def constant(value, dtype=None, shape=None, name=None):
+    import numpy as _np
+    arr = _np.asarray(value, dtype=_np.float32)
+    op = Op("Const", [], {"value": arr}, name or "Const")
+    op.outputs[0].shape = arr.shape
+    return op.outputs[0]
+
+
+def scalar_mul(scalar, x, name=None):
+    """tf.scalar_mul(scalar, x) with scalar a tf.constant or a number."""
+    ins = [x] + ([scalar] if isinstance(scalar, Tensor) else [])
+    op = Op("ScalarMul", ins, {"scalar": scalar, "x": x}, name)
+    op.outputs[0].shape = x.shape
+    return op.outputs[0]
+
+
+def const_value(t):
+    """Python float of a number or a scalar tf.constant."""
+    if isinstance(t, Tensor):
+        if t.op.type != "Const":
+            raise NotImplementedError(f"expected a tf.constant, got {t.op.type}")
+        return float(t.op.attrs["value"])
+    return float(t)
 
 
 def trainable_variables():
@@ -373,6 +457,11 @@ def batch_normalization(inputs, epsilon=1e-3, name=None):
     with _root_scope():
         gamma = get_variable(f"{base}/gamma", [C], constant_initializer(1.0))
         beta = get_variable(f"{base}/beta", [C], constant_initializer(0.0))
+        # TF's non-trainable moving statistics (saved by tf.train.Saver; frozen
+        # at their initial values since training=False never updates them)
+        mean = get_variable(f"{base}/moving_mean", [C], constant_initializer(0.0), trainable=False)
+        var = get_variable(f"{base}/moving_variance", [C], constant_initializer(1.0), trainable=False)
+        mean.bn_stat, var.bn_stat = "mean", "variance"
     op = Op("FusedBatchNorm", [inputs, gamma, beta], {"epsilon": epsilon}, base)
     op.outputs[0].shape = inputs.shape
     return op.outputs[0]
@@ -440,14 +529,37 @@ class AdamOptimizer:
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
         self.lr, self.beta1, self.beta2, self.epsilon = learning_rate, beta1, beta2, epsilon
 
-    def minimize(self, loss, var_list=None, grad_scale=1.0, name=None):
+    def minimize(self, loss, global_step=None, var_list=None, grad_scale=1.0, name=None):
         """grad_scale=1 gives FCN.py's `minimize` semantics; grad_scale=9 the
         effective gradient of the accumulate-then-apply template
-        (Network/main.py:71, :168-175: 3B accumulations of (3/B)*g)."""
+        (Network/main.py:71, :168-175: 3B accumulations of (3/B)*g) computed
+        once.  Only `var_list` (default: all trainables) is updated;
+        `global_step`, if given, is incremented per step as in TF."""
         var_list = var_list or trainable_variables()
         op = Op("TrainStep", [loss], {"optimizer": self, "var_list": list(var_list),
-                                      "grad_scale": float(grad_scale)}, name or "train_step")
+                                      "grad_scale": float(grad_scale), "global_step": global_step},
+                name or "train_step")
         return op
+
+    def compute_gradients(self, loss, var_list=None):
+        """[(gradient, variable)] (Network/main.py:88-89): each gradient is a
+        symbolic d loss / d var the Session computes in one backward pass."""
+        var_list = var_list or trainable_variables()
+        out = []
+        for v in var_list:
+            op = Op("Gradient", [loss, v], {"loss": loss, "var": v}, "gradients")
+            op.outputs[0].shape = tuple(v.shape)
+            out.append((op.outputs[0], v))
+        return out
+
+    def apply_gradients(self, grads_and_vars, global_step=None, name=None):
+        """One TF1 Adam step on each variable with the paired gradient source:
+        a compute_gradients gradient (optionally scalar_mul-scaled) or an
+        accumulator variable (Network/main.py:98-101)."""
+        pairs = list(grads_and_vars)
+        ins = [g for g, _ in pairs if isinstance(g, Tensor)]
+        return Op("ApplyGradients", ins, {"optimizer": self, "pairs": pairs, "global_step": global_step},
+                  name or "Adam")
 
 
 def global_variables_initializer():

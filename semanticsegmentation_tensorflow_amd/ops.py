@@ -560,6 +560,13 @@ def cast(x, y, stream=None):
     return y
 
 
+def axpy(y, x, alpha, stream=None):
+    """y += alpha * x (fp32, same number of elements)."""
+    assert y.dtype == torch.float32 and x.dtype == torch.float32 and y.numel() == x.numel()
+    check(_lib.lib().seg_axpy(ptr(y), ptr(x), float(alpha), y.numel(), stream_ptr(stream)), "axpy")
+    return y
+
+
 def fill(y, value, stream=None):
     check(_lib.lib().seg_fill(ptr(y), y.numel(), float(value), seg_dtype(y), stream_ptr(stream)),
           "fill")

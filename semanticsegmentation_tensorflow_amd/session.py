@@ -46,6 +46,40 @@ class Plan:
     pass
 
 
+def _is_op(f, type_):
+    return isinstance(f, G.Op) and f.type == type_
+
+
+def _accumulator_pairs(op):
+    """apply_gradients whose gradient sources are all variables (accumulators)."""
+    return all(isinstance(g, G.Variable) for g, _ in op.attrs["pairs"])
+
+
+def _gradient_source(t):
+    """(loss, var, scale) of a compute_gradients output, optionally wrapped in
+    tf.scalar_mul."""
+    scale = 1.0
+    if isinstance(t, G.Tensor) and t.op.type == "ScalarMul":
+        scale = G.const_value(t.op.attrs["scalar"])
+        t = t.op.attrs["x"]
+    if not (isinstance(t, G.Tensor) and t.op.type == "Gradient"):
+        raise NotImplementedError("expected an optimizer.compute_gradients output")
+    return t.op.attrs["loss"], t.op.attrs["var"], scale
+
+
+class _TrainSpec:
+    """What a run call's gradient-consuming fetches ask for: the loss, the
+    variables whose gradients are needed, and what consumes them (Adam with
+    `optimizer`, or `accum` = [(accumulator, variable, scale)])."""
+
+    def __init__(self, loss, optimizer, var_list, grad_scale, global_step, accum, ops_):
+        self.inputs = [loss]
+        self.attrs = {"optimizer": optimizer, "var_list": list(var_list), "grad_scale": float(grad_scale),
+                      "global_step": global_step}
+        self.accum = accum
+        self.ops = ops_
+
+
 def _np(x):
     if isinstance(x, torch.Tensor):
         return x
@@ -61,10 +95,11 @@ class _AdamOverlap:
     (its input gradient is enqueued before its filter gradient).  finish()
     updates the remaining variables and makes the compute stream wait."""
 
-    def __init__(self, sess, opt, gs):
+    def __init__(self, sess, opt, gs, var_set):
         self.s = sess
         self.opt = opt
         self.gs = gs
+        self.var_set = var_set
         if sess._side is None:
             sess._side = torch.cuda.Stream(device=sess.device)
         self.side = sess._side
@@ -74,6 +109,9 @@ class _AdamOverlap:
     def _adam(self, names):
         st = self.s.store
         o = self.opt
+        names = [nm for nm in names if nm in self.var_set]
+        if not names:
+            return
         ops.adam_tf1_pack(st.params, st.grads, st.m, st.v, self.s._adam_plan(names), o.lr, st.step, o.beta1,
                           o.beta2, o.epsilon, grad_scale=self.gs, dtype=self.s._pack_dtype(), stream=self.side)
         self.done.update(names)
@@ -84,10 +122,11 @@ class _AdamOverlap:
         self.side.wait_event(ev)
         self._adam(names)
 
-    def after_work(self, work, names):
-        if work is not None:
+    def after_work(self, works, names):
+        if works:
             with torch.cuda.stream(self.side):
-                work.wait()
+                for w in works:
+                    w.wait()
         else:
             ev = torch.cuda.Event()
             ev.record(self.main)
@@ -95,7 +134,7 @@ class _AdamOverlap:
         self._adam(names)
 
     def finish(self):
-        rest = [v.var_name for v in self.s.store.order if v.var_name not in self.done]
+        rest = [v.var_name for v in self.s.store.order if v.var_name in self.var_set and v.var_name not in self.done]
         if rest:
             self.launch(rest)
         self.main.wait_stream(self.side)
@@ -138,16 +177,18 @@ class Session:
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
+        self._ready_filter = None
+        self.capture = None    # tests: list -> per-conv buffer records of the last backward
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
 
     # ------------------------------------------------------------------ vars
     def _ensure_store(self):
-        if self.store is None or len(self.store.vars) != len(self.graph.variables):
+        if self.store is None or len(self.store.all_vars) != len(self.graph.variables):
             old = self.store
             self.store = VariableStore(list(self.graph.variables.values()), self.device, self.seed)
             self.store.initialize()
             if old is not None:
-                for v in old.vars:
+                for v in old.all_vars:
                     self.store.assign(v.var_name, old.read(v.var_name))
             self.plans = {}
         return self.store
@@ -163,19 +204,32 @@ class Session:
         feed_dict = feed_dict or {}
         single = not isinstance(fetches, (list, tuple))
         flist = [fetches] if single else list(fetches)
-        if any(isinstance(f, G.Op) and f.type == "InitAll" for f in flist):
+        if any(_is_op(f, "InitAll") for f in flist):
             self._ensure_store().initialize()
-            flist = [f for f in flist if not (isinstance(f, G.Op) and f.type == "InitAll")]
-            if not flist:
-                return None
         self._ensure_store()
-        key = (tuple(id(f) for f in flist),
-               tuple(sorted((id(k), tuple(np.shape(v))) for k, v in feed_dict.items())))
-        plan = self.plans.get(key)
-        if plan is None:
-            plan = self._compile(flist, feed_dict)
-            self.plans[key] = plan
-        out = self._execute(plan, feed_dict)
+        out = {}
+        rest, post = [], []
+        for f in flist:
+            if _is_op(f, "InitAll"):
+                out[id(f)] = None
+            elif _is_op(f, "Assign"):              # zero_ops (Network/main.py:84-85)
+                self._run_assign(f)
+                out[id(f)] = None
+            elif _is_op(f, "ApplyGradients") and _accumulator_pairs(f):
+                post.append(f)                      # Adam on accumulated gradients, after the fetches
+            else:
+                rest.append(f)
+        if rest:
+            key = (tuple(id(f) for f in rest),
+                   tuple(sorted((id(k), tuple(np.shape(v))) for k, v in feed_dict.items())))
+            plan = self.plans.get(key)
+            if plan is None:
+                plan = self._compile(rest, feed_dict)
+                self.plans[key] = plan
+            out.update(self._execute(plan, feed_dict))
+        for f in post:
+            self._apply_accumulated(f)
+            out[id(f)] = None
         res = []
         for f in flist:
             r = out.get(id(f))
@@ -184,15 +238,109 @@ class Session:
             res.append(r)
         return res[0] if single else res
 
+    # ------------------------------------------- accumulate-then-apply template
+    def _run_assign(self, op):
+        """`var.assign(tf.zeros_like(var))` / `var.assign(constant)` on device."""
+        store = self.store
+        var, val = op.attrs["var"], op.attrs["value"]
+        if isinstance(val, G.Tensor) and val.op.type == "ZerosLike":
+            value = 0.0
+        else:
+            value = G.const_value(val)
+        if var.var_name in store.aux:
+            ops.fill(store.aux[var.var_name], value)
+            store.aux_version += 1
+        else:
+            ops.fill(store.param(var.var_name), value)
+            store.version += 1
+
+    def _apply_accumulated(self, op):
+        """optimizer.apply_gradients([(accum_i, var_i)]) (Network/main.py:98-101):
+        TF1 Adam on each var_i with the accumulated gradient accum_i; nothing
+        else in the graph runs."""
+        store = self.store
+        opt = op.attrs["optimizer"]
+        names = []
+        for acc, var in op.attrs["pairs"]:
+            g = store.grad(var.var_name)
+            ops.fill(g, 0.0)
+            ops.axpy(g.view(-1), store.aux[acc.var_name].view(-1), 1.0)
+            names.append(var.var_name)
+        self._repack(None)
+        store.step += 1
+        ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(names), opt.lr,
+                          store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=1.0,
+                          dtype=self._pack_dtype())
+        store.version += 1
+        self._packed_version = store.version     # adam_tf1_pack rewrote the packed copies it owns
+        self._bump_global_step(op.attrs.get("global_step"))
+
+    def _bump_global_step(self, gs):
+        if gs is not None:
+            t = self.store.aux.get(gs.var_name)
+            if t is None:
+                raise ValueError(f"global_step {gs.var_name} must be a non-trainable tf.Variable")
+            t.add_(1.0)
+
+    def _train_spec(self, fetches):
+        """The gradient-consuming fetches of one run call as one spec:
+        TrainStep (minimize), ApplyGradients over compute_gradients outputs, or
+        AssignAdd(accum, [scalar_mul(c,] gradient[)]) accumulation ops."""
+        trains = [f for f in fetches if _is_op(f, "TrainStep")]
+        applies = [f for f in fetches if _is_op(f, "ApplyGradients")]
+        accs = [f for f in fetches if _is_op(f, "AssignAdd")]
+        if len(trains) + len(applies) + (1 if accs else 0) > 1:
+            raise NotImplementedError("one train / apply_gradients / accumulate group per run call")
+        if trains:
+            a = trains[0].attrs
+            return _TrainSpec(trains[0].inputs[0], a["optimizer"], a["var_list"], a["grad_scale"],
+                              a.get("global_step"), [], [trains[0]])
+        if applies:
+            op = applies[0]
+            loss, scales, vars_ = None, set(), []
+            for g, v in op.attrs["pairs"]:
+                lss, var, sc = _gradient_source(g)
+                if var is not v:
+                    raise NotImplementedError("apply_gradients: gradient paired with a different variable")
+                if loss is not None and lss is not loss:
+                    raise NotImplementedError("apply_gradients: gradients of different losses")
+                loss = lss
+                scales.add(sc)
+                vars_.append(v)
+            if len(scales) != 1:
+                raise NotImplementedError("apply_gradients: one gradient scale for all variables")
+            return _TrainSpec(loss, op.attrs["optimizer"], vars_, scales.pop(), op.attrs.get("global_step"),
+                              [], [op])
+        if accs:
+            loss, vars_, acc = None, [], []
+            for op in accs:
+                lss, var, sc = _gradient_source(op.attrs["value"])
+                if loss is not None and lss is not loss:
+                    raise NotImplementedError("assign_add: gradients of different losses")
+                loss = lss
+                if op.attrs["var"].trainable:
+                    raise NotImplementedError("assign_add target must be a non-trainable accumulator")
+                if tuple(op.attrs["var"].shape) != tuple(var.shape):
+                    raise ValueError(f"{op.attrs['var'].var_name}: accumulator shape != {var.var_name}")
+                vars_.append(var)
+                acc.append((op.attrs["var"].var_name, var.var_name, sc))
+            return _TrainSpec(loss, None, vars_, 1.0, None, acc, accs)
+        return None
+
     # --------------------------------------------------------------- compile
     def _compile(self, fetches, feed_dict):
         g = self.graph
         store = self.store
         p = Plan()
         p.fetches = fetches
-        train = [f for f in fetches if isinstance(f, G.Op) and f.type == "TrainStep"]
-        p.train = train[0] if train else None
-        roots = [f.inputs[0] if isinstance(f, G.Op) else f for f in fetches]
+        p.train = self._train_spec(fetches)
+        train_ops = {id(o) for o in p.train.ops} if p.train else set()
+        stray = [f for f in fetches if isinstance(f, G.Op) and id(f) not in train_ops]
+        if stray:
+            raise NotImplementedError(f"cannot fetch {stray[0]!r} here")
+        roots = [f for f in fetches if not isinstance(f, G.Op)]
+        if p.train:
+            roots.append(p.train.inputs[0])
 
         # ---- needed ops (ancestors of the fetches), topological = creation order
         needed = set()
@@ -592,13 +740,22 @@ class Session:
         for n in p.nodes:
             if n.kind == "conv" and ops.wgrad_adam_fusable(n.desc):
                 p.adam_fusable.add(id(n))
-            elif n.kind == "conv":
+            if n.kind == "conv":
                 p.wg_ws[id(n)] = torch.empty(max(256, ops.conv_workspace(n.desc, ops.OP_BWD_FILTER)),
                                              dtype=torch.uint8, device=self.device)
         p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
+        p.var_set = set(p.var_names)
+        # Adam / accumulation touch var_list only (TF: minimize(var_list=...)),
+        # in store (= backward) order
+        p.adam_names = [v.var_name for v in self.store.order if v.var_name in p.var_set]
         p.uncovered = [v for v in p.var_names if v not in covered]
         for v in p.uncovered:            # no gradient path: keep the grad slice at 0
             self.store.grad(v).zero_()
+        # variables whose gradient is never reported ready during backward
+        # (outside var_list, or no gradient path): released to the
+        # data-parallel buckets up front so they do not hold later buckets back
+        p.never_ready = [v.var_name for v in self.store.order
+                         if v.var_name not in p.var_set or v.var_name not in covered]
         # data parallel bucket schedule (var readiness in backward order)
         if self.dp is not None:
             self.dp.prepare(self.store)
@@ -689,7 +846,11 @@ class Session:
 
     def _execute(self, p, feed_dict):
         self.run_count += 1
+        # packed filter copies are current from here on; every update below
+        # (fused filter-gradient + Adam, adam_tf1_pack) rewrites the copies of
+        # the variables it changes, so they stay current after the step
         self._repack(p)
+        self._check_bn_stats(p)
         scal = self._feed(p, feed_dict)
         buf = p.buf
         store = self.store
@@ -764,11 +925,13 @@ class Session:
         if p.train:
             ts = p.train.attrs
             opt = ts["optimizer"]
-            gs = ts["grad_scale"] / (self.dp.world if self.dp is not None else 1)
-            fresh = self._packed_version == store.version
-            store.step += 1
+            world = self.dp.world if self.dp is not None else 1
+            gs = ts["grad_scale"] / world
+            if opt is not None:
+                store.step += 1
             self._fused = None
-            if self.fuse_adam and self.dp is None and not self.overlap_optimizer and fresh and p.adam_fusable:
+            if opt is not None and self.fuse_adam and self.dp is None and not self.overlap_optimizer \
+                    and p.adam_fusable:
                 self._fused = (opt, gs, set())
             self._red = None
             if self.defer_wgrad_reduce and self.dp is None and not self.overlap_optimizer and \
@@ -776,36 +939,44 @@ class Session:
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self.device)
                 self._red = (self._side, torch.cuda.current_stream(self.device))
-            if self.overlap_optimizer and self.device.type == "cuda":
+            if opt is not None and self.overlap_optimizer and self.device.type == "cuda":
                 # per-layer Adam on a side stream as soon as the layer's gradient is final
-                self._adam_ctx = _AdamOverlap(self, opt, gs)
+                self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set)
                 if self.dp is not None:
                     self.dp.on_launch = self._adam_ctx.after_work
-            self._backward(p, scal)
+            if self.dp is not None and p.never_ready:
+                self.dp.ready(p.never_ready)
+            self._ready_filter = p.var_set
+            try:
+                self._backward(p, scal)
+            finally:
+                self._ready_filter = None
             if self._red is not None:            # pending filter-gradient reductions done before Adam
                 self._red[1].wait_stream(self._red[0])
                 self._red = None
             if self.dp is not None:
                 self.dp.finish()
                 self.dp.on_launch = None
-            if self._adam_ctx is not None:
+            if opt is None:
+                # accumulate template: accum += const * grad (Network/main.py:92-95)
+                for acc, var, sc in p.train.accum:
+                    ops.axpy(store.aux[acc].view(-1), store.grad(var).view(-1), sc / world)
+                store.aux_version += 1
+            elif self._adam_ctx is not None:
                 self._adam_ctx.finish()
                 self._adam_ctx = None
-            elif self._fused is not None and self._fused[2]:
-                done = self._fused[2]
-                rest = [v.var_name for v in store.order if v.var_name not in done]
+            else:
+                done = self._fused[2] if self._fused is not None else set()
+                rest = [nm for nm in p.adam_names if nm not in done]
                 if rest:
                     ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(rest), opt.lr,
                                       store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
                                       dtype=self._pack_dtype())
-            else:
-                ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(), opt.lr,
-                                  store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
-                                  dtype=self._pack_dtype())
             self._fused = None
-            store.version += 1
-            if fresh:           # the fused update rewrote every packed copy
+            if opt is not None:
+                store.version += 1
                 self._packed_version = store.version
+                self._bump_global_step(ts.get("global_step"))
         # ---------------- fetch values
         for f in p.fetches:
             if isinstance(f, G.Op):
@@ -846,6 +1017,8 @@ class Session:
         """The gradients of `names` are final once the kernels enqueued so far
         run: hand them to the all-reduce (DP) or straight to the overlapped
         optimizer."""
+        if self._ready_filter is not None:
+            names = [nm for nm in names if nm in self._ready_filter]
         if self.dp is not None:
             self.dp.ready(names)
         elif self._adam_ctx is not None:
@@ -966,13 +1139,27 @@ class Session:
                     db = store.grad(n.bias.var_name) if n.bias is not None else None
                     K = n.desc.k_valid
                     self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
+                dx = None
                 if id(x) in ng:
                     dx, acc = dest(x)
                     self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
                                 self._mask_epi(p, x))
                     done(dx, acc)
-                if self._fused is not None and id(n) in p.adam_fusable:
+                if self.capture is not None:
+                    # tests: the buffers of this layer's three kernels (they persist
+                    # after the step; dx before any accumulation of other consumers)
+                    mask = self._mask_epi(p, x) if dx is not None else None
+                    self.capture.append({"kind": "conv", "name": n.w.var_name, "bias": getattr(n.bias, "var_name", None),
+                                         "x": buf[id(x)], "y": buf[id(n.output)], "dz": dz, "dx": dx,
+                                         "dx_masked": mask is not None, "relu": n.relu, "desc": n.desc,
+                                         "stride": n.stride, "dilation": n.dilation, "padding": n.padding})
+                want_w = n.w.var_name in p.var_set
+                want_b = n.bias is not None and n.bias.var_name in p.var_set
+                gw = store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w)
+                if not (want_w or want_b):
+                    pass          # frozen layer (outside var_list): no filter gradient
+                elif self._fused is not None and id(n) in p.adam_fusable and want_w:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
@@ -985,7 +1172,7 @@ class Session:
                 elif self._red is not None:
                     # kernel now, its split-K reduction on the side stream
                     side, main = self._red
-                    gw, wsb = store.grad(n.w.var_name), p.wg_ws[id(n)]
+                    wsb = p.wg_ws[id(n)]
                     tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc, buf[id(x)],
                                       dz, gw, wsb, fused_db)
                     if tok[1][0] > 1:
@@ -995,7 +1182,7 @@ class Session:
                         ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db, stream=side)
                 else:
                     self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter, n.desc, buf[id(x)], dz,
-                                store.grad(n.w.var_name), ws, None, fused_db)
+                                gw, ws, None, fused_db)
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "tconv":
                 x = n.inputs[0]
@@ -1007,9 +1194,12 @@ class Session:
                                 store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws, None,
                                 self._mask_epi(p, x))
                     done(dx, acc)
-                self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
-                            store.grad(n.w.var_name), ws, None,
-                            store.grad(n.bias.var_name) if n.bias is not None else None)
+                want_w = n.w.var_name in p.var_set
+                want_b = n.bias is not None and n.bias.var_name in p.var_set
+                if want_w or want_b:
+                    self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
+                                store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w), ws, None,
+                                store.grad(n.bias.var_name) if n.bias is not None else None)
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
@@ -1098,6 +1288,34 @@ class Session:
                 continue
             else:
                 raise NotImplementedError(f"backward of {k}")
+
+    def _scratch_grad(self, p, var):
+        """fp32 gradient sink for a filter outside var_list whose layer still
+        needs its bias gradient (the filter-gradient launch sums it)."""
+        t = p.tmp.get(("wscratch", var.var_name))
+        if t is None:
+            t = torch.zeros(tuple(var.shape), dtype=torch.float32, device=self.device)
+            p.tmp[("wscratch", var.var_name)] = t
+        return t
+
+    def _check_bn_stats(self, p):
+        """The kernels fold BatchNorm's frozen statistics as mean 0 / variance
+        1 (tf.layers.batch_normalization with training=False and never-updated
+        moving averages, Network/utils/utils.py:300-301).  Refuse to run if a
+        restore or assign changed them."""
+        store = self.store
+        if not store.aux_vars or getattr(self, "_bn_checked", None) == store.aux_version:
+            return
+        for v in store.aux_vars:
+            kind = getattr(v, "bn_stat", None)
+            if kind is None:
+                continue
+            t = store.aux[v.var_name]
+            want = 0.0 if kind == "mean" else 1.0
+            if not bool((t == want).all()):
+                raise NotImplementedError(f"{v.var_name}: BatchNormalization moving statistics other than "
+                                          f"the frozen (0, 1) of the reference are not on the hot path")
+        self._bn_checked = store.aux_version
 
     def _bias_relu_bwd(self, dy, y, dz, dbias, k_valid, relu, scale):
         # with TF1 dropout fused after the relu: dz = dy * (y > 0) / keep_prob

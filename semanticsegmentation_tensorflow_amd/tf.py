@@ -31,6 +31,10 @@ concat = _g.concat
 argmax = _g.argmax
 expand_dims = _g.expand_dims
 reduce_mean = _g.reduce_mean
+Variable = _g.Variable_
+zeros_like = _g.zeros_like
+constant = _g.constant
+scalar_mul = _g.scalar_mul
 
 nn = SimpleNamespace(
     conv2d=_g.conv2d,
@@ -49,4 +53,7 @@ image = SimpleNamespace(resize_bilinear=_g.resize_bilinear)
 train = SimpleNamespace(AdamOptimizer=_g.AdamOptimizer, Saver=_ckpt.Saver,
                         get_checkpoint_state=_ckpt.get_checkpoint_state,
                         latest_checkpoint=_ckpt.latest_checkpoint)
-compat = SimpleNamespace(v1=SimpleNamespace(train=train, placeholder=placeholder))
+compat = SimpleNamespace(v1=SimpleNamespace(
+    train=train, placeholder=placeholder, Variable=Variable, zeros_like=zeros_like, constant=constant,
+    trainable_variables=trainable_variables, global_variables=global_variables,
+    global_variables_initializer=global_variables_initializer, Session=Session))

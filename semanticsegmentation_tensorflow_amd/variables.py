@@ -40,8 +40,15 @@ def init_value(var: G.Variable, seed: int = 0) -> np.ndarray:
 
 
 class VariableStore:
+    """Trainable variables in the flat buffers (`vars`, backward order);
+    non-trainable ones (the accumulate template's gradient accumulators,
+    `global_step`, BatchNorm moving statistics) as separate fp32 tensors in
+    `aux` -- they never enter Adam or the gradient all-reduce."""
+
     def __init__(self, variables, device, seed=0):
-        self.vars = list(variables)
+        variables = list(variables)
+        self.vars = [v for v in variables if getattr(v, "trainable", True)]
+        self.aux_vars = [v for v in variables if not getattr(v, "trainable", True)]
         self.device = device
         self.seed = seed
         order = list(reversed(self.vars))
@@ -57,6 +64,10 @@ class VariableStore:
         self.m = torch.zeros(off, dtype=torch.float32, device=device)
         self.v = torch.zeros(off, dtype=torch.float32, device=device)
         self.by_name = {v.var_name: v for v in self.vars}
+        self.aux_by_name = {v.var_name: v for v in self.aux_vars}
+        self.aux = {v.var_name: torch.zeros(tuple(v.shape), dtype=torch.float32, device=device)
+                    for v in self.aux_vars}
+        self.aux_version = 0    # bumped when a non-trainable value is written from the host
         self.order = order
         self.step = 0           # Adam t (TF beta powers)
         self.packed = {}        # (var_name, mode) -> (tensor, a_pad, b_pad)
@@ -68,7 +79,13 @@ class VariableStore:
         o = self.offset[name]
         return buf[o:o + n].view(*v.shape)
 
+    @property
+    def all_vars(self):
+        return self.vars + self.aux_vars
+
     def param(self, name):
+        if name in self.aux:
+            return self.aux[name]
         return self._view(self.params, name)
 
     def grad(self, name):
@@ -87,6 +104,9 @@ class VariableStore:
             o = self.offset[v.var_name]
             host[o:o + n] = init_value(v, self.seed).reshape(-1)
         self.params.copy_(torch.from_numpy(host).to(self.device))
+        for v in self.aux_vars:
+            self.aux[v.var_name].copy_(torch.from_numpy(init_value(v, self.seed)).to(self.device))
+        self.aux_version += 1
         self.m.zero_()
         self.v.zero_()
         self.step = 0
@@ -94,6 +114,10 @@ class VariableStore:
 
     def assign(self, name, value):
         t = torch.as_tensor(np.asarray(value, dtype=np.float32)).to(self.device)
+        if name in self.aux:
+            self.aux[name].copy_(t.view(self.aux[name].shape))
+            self.aux_version += 1
+            return
         self.param(name).copy_(t.view(self.by_name[name].shape))
         self.version += 1
 
@@ -107,6 +131,8 @@ class VariableStore:
             out[v.var_name] = self.read(v.var_name)
             out[v.var_name + "/Adam"] = self._view(self.m, v.var_name).cpu().numpy().copy()
             out[v.var_name + "/Adam_1"] = self._view(self.v, v.var_name).cpu().numpy().copy()
+        for v in self.aux_vars:
+            out[v.var_name] = self.aux[v.var_name].cpu().numpy().copy()
         out["beta_step"] = np.array(self.step)
         return out
 
@@ -117,6 +143,9 @@ class VariableStore:
             if v.var_name + "/Adam" in d:
                 self._view(self.m, v.var_name).copy_(torch.from_numpy(np.asarray(d[v.var_name + "/Adam"], np.float32)).to(self.device))
                 self._view(self.v, v.var_name).copy_(torch.from_numpy(np.asarray(d[v.var_name + "/Adam_1"], np.float32)).to(self.device))
+        for v in self.aux_vars:
+            if v.var_name in d:
+                self.assign(v.var_name, d[v.var_name])
         if "beta_step" in d:
             self.step = int(d["beta_step"])
         self.version += 1

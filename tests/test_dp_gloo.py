@@ -70,9 +70,10 @@ def _worker(rank, world, port, q):
         shard = slice(rank * 2, rank * 2 + 2)
         g = grads_of(weights, x[shard], lab[shard])
         store = FakeStore(SHAPES)
-        dp = DataParallel(bucket_mb=0.002)          # tiny buckets: several of them
+        dp = DataParallel(bucket_mb=0.002)          # tiny buckets: several, c2/weights chunked
         dp.prepare(store)
         assert len(dp.buckets) >= 3
+        assert len(dp.var_buckets["c2/weights"]) >= 2             # chunked across buckets
         # contiguous, disjoint, cover the whole buffer
         spans = sorted((s, e) for s, e, _ in dp.buckets)
         assert spans[0][0] == 0 and spans[-1][1] == store.numel

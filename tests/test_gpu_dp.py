@@ -1,0 +1,87 @@
+"""The Session's data-parallel path executed for real (it had
+never run): two ranks on the shared cuda:0 over gloo, each training on half of
+a 4-image batch, vs one process on the whole batch.
+
+Checked (fp32 compute path): the all-reduced gradient sum / world equals the
+single-process gradient within 1e-5 of each variable's max |g| (the mean of
+per-shard means is the global mean for equal shards; only fp32 summation order
+differs), Adam-updated parameters within 1e-6 + 1e-5 * max |p|, both ranks
+bit-identical after the step, with and without the overlapped per-bucket
+optimizer (dp.on_launch -> side-stream Adam).  bf16: ranks bit-identical,
+gradients within relative L2 2e-2 of the single-process bf16 run (different
+split-K / tile choices at batch 2 vs 4 reorder bf16-rounded partial sums)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import models as M
+from semanticsegmentation_tensorflow_amd import tf
+from tests.model_inputs import he_weights, synthetic_batch
+from tests.test_gpu_fcn import build_fcn
+from tests.workers.dp_session_worker import CASES, H, N_GLOBAL, W
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _single(dtype):
+    weights = he_weights(M.fcn_param_shapes(3, 2), 51)
+    img, lab = synthetic_batch(N_GLOBAL, H, W, 52)
+    image, labels, keep, pred, logits, loss, train_step = build_fcn(H, W)
+    sess = tf.Session(compute_dtype=dtype, seed=5)
+    sess.store_fused_grads = True
+    sess.run(tf.global_variables_initializer())
+    for k, v in weights.items():
+        sess.assign(k, v)
+    sess.run(train_step, feed_dict={image: img, labels: lab, keep: 1.0})
+    return ({k: sess.store.grad(k).cpu().numpy() for k in weights},
+            {k: sess.variable_value(k) for k in weights})
+
+
+def test_session_dp_world2_matches_single_process(dev, tmp_path):
+    port = str(_free_port())
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+    procs = [subprocess.Popen([sys.executable, "-u", "-m", "tests.workers.dp_session_worker", str(r), "2", port,
+                               str(tmp_path)], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o)
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    ref = {}
+    for dtype, overlap in CASES:
+        if dtype not in ref:
+            ref[dtype] = _single(dtype)
+        g_ref, p_ref = ref[dtype]
+        r = [dict(np.load(os.path.join(tmp_path, f"rank{i}_{dtype}_{int(overlap)}.npz"))) for i in range(2)]
+        assert int(r[0]["buckets"]) >= 3
+        for k in g_ref:
+            assert np.array_equal(r[0]["g:" + k], r[1]["g:" + k]), (dtype, overlap, k)
+            assert np.array_equal(r[0]["p:" + k], r[1]["p:" + k]), (dtype, overlap, k)
+            g = r[0]["g:" + k] / 2.0
+            if dtype == "f32":
+                assert np.abs(g - g_ref[k]).max() <= 1e-5 * max(np.abs(g_ref[k]).max(), 1e-30), (overlap, k)
+                pr = p_ref[k]
+                assert np.abs(r[0]["p:" + k] - pr).max() <= 1e-6 + 1e-5 * np.abs(pr).max(), (overlap, k)
+            else:
+                rel = np.linalg.norm(g - g_ref[k]) / max(np.linalg.norm(g_ref[k]), 1e-30)
+                assert rel <= 2e-2, (k, rel)

@@ -39,7 +39,7 @@ def test_fcdensenet_logits_grads_adam_f32(dev, alias):
     N, H, W = 1, 64, 96
     image, labels, keep, pred, logits, loss, train_step = build(H, W)
     shapes = M.fcdensenet_param_shapes(3, 2)
-    assert {v.var_name for v in tf.global_variables()} == set(shapes)
+    assert {v.var_name for v in tf.trainable_variables()} == set(shapes)
     weights = densenet_weights(shapes, 7)
     img, lab = synthetic_batch(N, H, W, 8)
 

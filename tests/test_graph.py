@@ -66,7 +66,7 @@ def test_fcdensenet_variables_match_reference():
     x = tf.placeholder(tf.float32, [None, 64, 96, 3])
     kp = tf.placeholder(tf.float32)
     pred, logits = FCDenseNet(x, kp, 2)
-    vs = {v.var_name: tuple(v.shape) for v in tf.global_variables()}
+    vs = {v.var_name: tuple(v.shape) for v in tf.trainable_variables()}
     ref = {k: tuple(s) for k, s in M.fcdensenet_param_shapes(3, 2).items()}
     assert vs == ref
     assert logits.shape[1:] == (64, 96, 2)
@@ -85,6 +85,6 @@ def test_deeplab_variables_match_oracle():
     G.reset_default_graph()
     image = tf.placeholder(tf.float32, [None, 64, 96, 3])
     pred, logits = DeepLabASPP(image, 1.0, 2)
-    got = {v.var_name: tuple(v.shape) for v in tf.global_variables()}
+    got = {v.var_name: tuple(v.shape) for v in tf.trainable_variables()}
     assert got == {k: tuple(s) for k, s in M.deeplab_param_shapes(3, 2).items()}
     assert tuple(logits.shape) == (None, 64, 96, 2) or list(logits.shape)[1:] == [64, 96, 2]
