@@ -12,7 +12,14 @@
 
 Tolerances: logits 1e-4 relative, gradients 2e-3 of each variable's max
 |value| (fp32 accumulation order vs the float64 oracle, as
-tests/test_gpu_fcn.py), parameters after Adam 1e-6 + 1e-5 * max|p|."""
+tests/test_gpu_fcn.py).  Parameters after Adam on the SAME gradient: 1e-6 +
+1e-5 * max|p|.  Parameters after Adam on gradients from a different summation
+order (another plan, or the float64 oracle): all but 1 % of the elements
+within 2 % of lr per step, and none off by more than a full Adam step -- TF1
+Adam moves an element whose gradient g is a near-cancelling sum by
+lr_t * (1 - b1) * g / (sqrt(v) + eps), so a rounding difference in g that is
+tiny against max|g| but comparable to eps = 1e-8 (or flips g's sign) changes
+that element's update by up to a whole step while the rest agree to ~1e-6."""
 import numpy as np
 import pytest
 import torch
@@ -59,6 +66,13 @@ def _close_params(got, ref, what):
     assert err <= 1e-6 + 1e-5 * np.abs(ref).max(), f"{what}: {err:.3e}"
 
 
+def _close_updates(got, ref, what, steps):
+    d = np.abs(got - ref)
+    frac = float((d > 2e-2 * LR * steps).mean())
+    assert frac <= 1e-2, f"{what}: {frac:.2e} of the elements off by > 2% of lr per step"
+    assert d.max() <= 3.5 * LR * steps, f"{what}: {d.max():.3e}"
+
+
 def test_accumulate_template_is_adam_on_9g(dev):
     N, H, W, B = 2, 64, 96, 2
     image, labels, keep, pred, logits, loss = _fcn(H, W)
@@ -75,21 +89,29 @@ def test_accumulate_template_is_adam_on_9g(dev):
     feed = {image: img, labels: lab, keep: 1.0}
 
     sess = _session(weights)
-    for _ in range(2):                                              # two batches, zeroed in between
+    for step in range(2):                                           # two batches, zeroed in between
         sess.run(zero_ops)
         for _ in range(3 * B):                                      # Network/main.py:168-170
             sess.run(accum_ops, feed_dict=feed)
+        if step == 0:
+            acc0 = [sess.store.aux[a.var_name].cpu().numpy() for a in accum]
         sess.run(train_step, feed_dict=feed)
     assert sess.store.step == 2
 
-    # the same two steps computed once per batch with grad_scale = 9
-    image2, labels2, keep2, _, _, loss2 = image, labels, keep, pred, logits, loss
-    step9 = tf.train.AdamOptimizer(LR).minimize(loss2, grad_scale=9.0)
+    # the same two steps computed once per batch with grad_scale = 9: the
+    # batch-2 accumulators hold 9x that plan's gradient (fp32 sums of six
+    # 1.5 g terms vs one 9 g scale), and its parameters track
+    step9 = tf.train.AdamOptimizer(LR).minimize(loss, grad_scale=9.0)
     ref = _session(weights)
-    for _ in range(2):
-        ref.run(step9, feed_dict={image2: img, labels2: lab, keep2: 1.0})
-    for v in t_vars:
-        _close_params(sess.variable_value(v.var_name), ref.variable_value(v.var_name), v.var_name)
+    ref.store_fused_grads = True
+    for step in range(2):
+        ref.run(step9, feed_dict={image: img, labels: lab, keep: 1.0})
+        if step == 0:    # same parameters as the first accumulation: 9 g vs sum of 6 x 1.5 g, tight
+            for i, v in enumerate(t_vars):
+                g9 = 9.0 * ref.store.grad(v.var_name).cpu().numpy()
+                assert np.abs(acc0[i] - g9).max() <= 1e-5 * max(np.abs(g9).max(), 1e-30), v.var_name
+    for i, v in enumerate(t_vars):
+        _close_updates(sess.variable_value(v.var_name), ref.variable_value(v.var_name), v.var_name, 2)
 
     # the oracle: TF1 Adam on 9 * g, two steps; the accumulators hold 9 * g of step 2
     adam = T.AdamTF1(lr=LR)
@@ -103,7 +125,7 @@ def test_accumulate_template_is_adam_on_9g(dev):
                 assert np.abs(a - gr).max() <= 2e-3 * max(np.abs(gr).max(), 1e-30), v.var_name
         w = adam.apply(w, {k: 9.0 * g[k] for k in w})
     for k in ["conv1_1/weights", "conv4_2/weights", "conv6/weights", "conv8/biases", "conv_t3/bias"]:
-        _close_params(sess.variable_value(k), w[k].numpy(), k)
+        _close_updates(sess.variable_value(k), w[k].numpy(), k, 2)
 
 
 def test_three_adam_steps_track_the_oracle(dev):
@@ -133,9 +155,7 @@ def test_three_adam_steps_track_the_oracle(dev):
     for k in ["conv1_1/weights", "conv3_3/weights", "conv5_3/biases", "conv6/weights", "conv7/weights",
               "conv_t1/weights", "conv_t3/weights"]:
         got, ref = sess.variable_value(k), w[k].numpy()
-        # Adam's first steps move each parameter by ~lr: compare the update
-        upd_got, upd_ref = got - weights[k], ref - weights[k]
-        assert np.abs(upd_got - upd_ref).max() <= 2e-2 * np.abs(upd_ref).max() + 1e-7, k
+        _close_updates(got, ref, k, 3)
 
 
 def test_var_list_freezes_a_mid_network_layer(dev):
@@ -157,15 +177,19 @@ def test_var_list_freezes_a_mid_network_layer(dev):
             assert np.array_equal(sess.variable_value(k), weights[k]), (dtype, k)
         for k in ("conv3_1/weights", "conv3_3/weights", "conv6/biases", "conv7/weights"):
             assert not np.array_equal(sess.variable_value(k), weights[k]), (dtype, k)
-    # fp32: the updated variables follow the oracle's Adam on the same gradients
+    # fp32: the updated variables take TF1 Adam on their gradient (tight: the
+    # same gradient), and that gradient is the oracle's
     _, _, g = _oracle_grads(weights, img, lab)
-    adam = T.AdamTF1(lr=LR)
-    w = adam.apply({k: torch.from_numpy(v).double() for k, v in weights.items() if k not in frozen},
-                   {k: g[k] for k in weights if k not in frozen})
     sess = _session(weights)
+    sess.store_fused_grads = True
     sess.run(train, feed_dict={image: img, labels: lab, keep: 1.0})
+    dg = {k: sess.store.grad(k).cpu().numpy() for k in weights if k not in frozen}
+    w = T.AdamTF1(lr=LR).apply({k: torch.from_numpy(weights[k]).double() for k in dg},
+                               {k: torch.from_numpy(v).double() for k, v in dg.items()})
     for k in ("conv3_1/weights", "conv3_3/weights", "conv6/biases", "conv7/weights", "conv_t2/weights"):
         _close_params(sess.variable_value(k), w[k].numpy(), k)
+        gr = g[k].numpy()
+        assert np.abs(dg[k] - gr).max() <= 2e-3 * np.abs(gr).max(), k
 
 
 def test_fcn_merge_rgba_input_at_160x576(dev):
