@@ -130,7 +130,7 @@ def cpu_baseline(H, W, HP, WP, steps, model="fcn"):
     return {"value": round(1.0 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle {dict(fcn='FCN', fcdensenet='FC-DenseNet', deeplab='DeepLab-ASPP')[model]} "
                       f"fwd+bwd, torch-CPU fp32, "
-                      f"1 image {HP}x{WP} ({H}x{W} padded), "
+                      f"1 image {HP}x{WP}" + (f" ({H}x{W} padded)" if (H, W) != (HP, WP) else "") + ", "
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step"}
 
 
