@@ -223,6 +223,19 @@ int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, 
 /* dx is zeroed then scatter-added (fp32 dx only). */
 int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, int W, int C, int OH,
                             int OW, int dtype, void* stream);
+/* Global average pooling (tflearn global_avg_pool = tf.reduce_mean(x, [1, 2]),
+ * Network/utils/utils.py:312; DeepLab's image-pooling branch,
+ * Network/model/DeepLabv3Plus.py:215-225): y[n, c] = scale * sum_hw x[n, h, w, c]
+ * (scale = 1/(H*W); scale = 1 is the gradient of a 1x1 -> HxW align_corners
+ * resize).  y is [N, C] in the compute dtype; ws: N*C fp32 scratch.
+ * C <= 256 chunks of 16 bytes. */
+int seg_spatial_reduce(const void* x, int ldx, void* y, int N, int H, int W, int C, float scale,
+                       float* ws, int dtype, void* stream);
+/* y[n, h, w, c] = scale * x[n, c]: the gradient of global average pooling
+ * (scale = 1/(H*W)) and the forward of a 1x1 -> HxW align_corners resize
+ * (scale = 1, Network/model/DeepLabv3Plus.py:222-223). */
+int seg_spatial_broadcast(const void* x, void* y, int ldy, int N, int H, int W, int C, float scale,
+                          int dtype, void* stream);
 /* tf.concat(axis=-1) (Network/utils/utils.py:332-333; DenseBlock
  * FCDenseNet.py:48-61): parts at arbitrary (unaligned) channel offsets.
  * fwd: y[p, off_i + c] = part_i[p, c]; channels >= sum are written 0.

@@ -207,8 +207,9 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
 
 # ---------------------------------------------------------------------------
 # DeepLab-style atrous model (config C5), semanticsegmentation_tensorflow_amd/
-# deeplab.py: VGG16 backbone at output stride 8 (conv5 rate 2), ASPP (1x1 +
-# rates 6/12/18, frozen BN + ReLU), 1x1 projection, classifier, bilinear x8.
+# deeplab.py: VGG16 backbone at output stride 8 (conv5 rate 2), ASPP (image
+# pooling + 1x1 + rates 6/12/18, frozen BN + ReLU), 1x1 projection,
+# classifier, bilinear x8.
 # ---------------------------------------------------------------------------
 DEEPLAB_ASPP_RATES = (6, 12, 18)
 
@@ -229,12 +230,14 @@ def deeplab_param_shapes(in_channels=3, num_classes=2, depth=256):
         shapes[f"{n}/gamma"] = (c,)
         shapes[f"{n}/beta"] = (c,)
 
+    shapes["image_pooling/weights"] = (1, 1, 512, depth)      # DeepLabv3Plus.py:215-223
+    bnv(depth)
     shapes["aspp0/weights"] = (1, 1, 512, depth)
     bnv(depth)
     for i in range(3):
         shapes[f"aspp{i + 1}/weights"] = (3, 3, 512, depth)
         bnv(depth)
-    shapes["concat_projection/weights"] = (1, 1, 4 * depth, depth)
+    shapes["concat_projection/weights"] = (1, 1, 5 * depth, depth)
     bnv(depth)
     shapes["Last_layer/weights"] = (1, 1, depth, num_classes)
     return shapes
@@ -259,7 +262,11 @@ def deeplab_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
     h = tf.max_pool2x2(h)
     h = cl(cl(cl(h, "conv4_1"), "conv4_2"), "conv4_3")
     feat = cl(cl(cl(h, "conv5_1", 2), "conv5_2", 2), "conv5_3", 2)
-    br = [q(tf.relu(BN(q(tf.conv2d(feat, p["aspp0/weights"])))))]
+    # image pooling: reduce_mean over H, W -> 1x1 conv -> BN -> ReLU -> align_corners resize
+    gap = q(feat.mean(dim=(1, 2), keepdim=True))
+    b4 = q(tf.relu(BN(q(tf.conv2d(gap, p["image_pooling/weights"])))))
+    br = [q(tf.resize_bilinear(b4, (feat.shape[1], feat.shape[2])))]
+    br.append(q(tf.relu(BN(q(tf.conv2d(feat, p["aspp0/weights"]))))))
     for i, r in enumerate(DEEPLAB_ASPP_RATES):
         br.append(q(tf.relu(BN(q(tf.conv2d(feat, p[f"aspp{i + 1}/weights"], dilation=r))))))
     h = tf.concat(br)

@@ -149,6 +149,8 @@ SIGNATURES = {
     "seg_resize_bilinear_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_resize_bilinear_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_copy_channels": (_I, [_P, _I, _P, _I, _L, _I, _I, _P]),
+    "seg_spatial_reduce": (_I, [_P, _I, _P, _I, _I, _I, _I, _F, _P, _I, _P]),
+    "seg_spatial_broadcast": (_I, [_P, _P, _I, _I, _I, _I, _I, _F, _I, _P]),
     "seg_prepare_input": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_prepare_input_u8": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_png_info": (_I, [_P, _Z, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),

@@ -464,6 +464,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
 
 int g_adam_tr_fused = 0;   // 1: the fused epilogue also writes the KRSC copy (transposed 16-byte stores)
 
+extern int g_adam_blocks;   // optim.hip
+
 extern "C" int seg_set_option(const char* name, int value) {
     if (!name) return SEG_EINVAL;
     if (!strcmp(name, "igemm_nt_variant")) {
@@ -498,6 +500,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt2_short")) {   // max k tiles (64 deep) of the 2-stage igemm_nt2; 0 = off
         if (value < 0 || value > 64) return SEG_EINVAL;
         seg::g_nt2_short = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "adam_blocks")) {   // grid cap of seg_adam_tf1_pack (0 = one block per tile)
+        if (value < 0) return SEG_EINVAL;
+        g_adam_blocks = value;
         return SEG_OK;
     }
     if (!strcmp(name, "nt3_fill")) {

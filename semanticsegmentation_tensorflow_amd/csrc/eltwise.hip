@@ -1106,6 +1106,97 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
     return SEG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Global average pooling (tflearn global_avg_pool = tf.reduce_mean(x, [1, 2]),
+// Network/utils/utils.py:312; DeepLab's image-pooling ASPP branch,
+// Network/model/DeepLabv3Plus.py:215-225) and its broadcast counterpart.
+// reduce: grid (N, slices); a thread owns one 8-channel chunk and a strided
+// pixel subset, the block combines equal chunks through LDS and adds its
+// partial sum into an fp32 workspace (one atomic per channel per block); a
+// second pass writes scale * sum in the compute dtype.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void spatial_sum_k(const T* __restrict__ x, int ldx, float* __restrict__ acc,
+                                                     int HW, int C) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    __shared__ float red[256][EPC + 1];
+    const int CK = C / EPC;                       // <= 256 (checked by the entry point)
+    const int n = blockIdx.y;
+    const int prow = 256 / CK;                    // pixel rows per block step
+    const int t = threadIdx.x, ck = t % CK, pr = t / CK;
+    float a[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) a[e] = 0.f;
+    if (pr < prow) {
+        for (long pix = (long)blockIdx.x * prow + pr; pix < HW; pix += (long)gridDim.x * prow) {
+            float v[EPC];
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(x + ((long)n * HW + pix) * ldx + ck * EPC), v);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) a[e] += v[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) red[t][e] = a[e];
+    __syncthreads();
+    if (t < CK) {
+        for (int r = 1; r < prow; ++r)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) a[e] += red[t + r * CK][e];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) atomicAdd(acc + (long)n * C + t * EPC + e, a[e]);
+    }
+}
+
+template <typename T>
+__global__ void scale_cast_k(const float* __restrict__ acc, T* __restrict__ y, long n, float scale) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f32<T>(acc[i] * scale);
+}
+
+template <typename T>
+__global__ void spatial_bcast_k(const T* __restrict__ x, T* __restrict__ y, int ldy, long NHW, int HW, int C,
+                                float scale) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int CK = C / EPC;
+    const long total = NHW * CK;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long p = i / CK;
+        const int cc = (int)(i - p * CK);
+        const long n = p / HW;
+        float v[EPC];
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(x + n * C + cc * EPC), v);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] *= scale;
+        *reinterpret_cast<uint4*>(y + p * ldy + cc * EPC) = Chunk<T>::pack(v);
+    }
+}
+
+extern "C" int seg_spatial_reduce(const void* x, int ldx, void* y, int N, int H, int W, int C, float scale,
+                                  float* ws, int dtype, void* stream) {
+    if (!x || !y || !ws || N <= 0 || H <= 0 || W <= 0 || (C & 7) || ldx < C || (ldx & 7)) return SEG_EINVAL;
+    if (C / epc_of(dtype) > 256) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(ws, 0, (size_t)N * C * sizeof(float), s) != hipSuccess) return SEG_ELAUNCH;
+    const int HW = H * W;
+    const int slices = std::max(1, std::min(256, (HW + 255) / 256));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(spatial_sum_k<T>, dim3(slices, N), dim3(256), 0, s, (const T*)x, ldx, ws,
+                                         HW, C));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(scale_cast_k<T>, dim3(seg_grid_1d((long)N * C, 256)), dim3(256), 0, s, ws,
+                                         (T*)y, (long)N * C, scale));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_spatial_broadcast(const void* x, void* y, int ldy, int N, int H, int W, int C, float scale,
+                                     int dtype, void* stream) {
+    if (!x || !y || N <= 0 || H <= 0 || W <= 0 || (C & 7) || ldy < C || (ldy & 7)) return SEG_EINVAL;
+    const long NHW = (long)N * H * W;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(spatial_bcast_k<T>, dim3(seg_grid_1d(NHW * (C / 8), 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (T*)y, ldy, NHW, H * W, C, scale));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
 extern "C" int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
                                        void* stream) {
     if (!x || !y) return SEG_EINVAL;

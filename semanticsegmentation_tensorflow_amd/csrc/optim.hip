@@ -36,15 +36,15 @@ __device__ __forceinline__ int find_segment(const seg_adam_segment* segs, int ns
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const float* __restrict__ G,
-                                                    float* __restrict__ Mm, float* __restrict__ Vv,
-                                                    const seg_adam_segment* __restrict__ segs, int nsegs,
-                                                    float lr_t, float b1, float b2, float eps, float gs) {
-    __shared__ float lds[TB][TA + 1];
-    const int si = find_segment(segs, nsegs, blockIdx.x);
+__device__ __forceinline__ void adam_pack_tile(float* __restrict__ P, const float* __restrict__ G,
+                                               float* __restrict__ Mm, float* __restrict__ Vv,
+                                               const seg_adam_segment* __restrict__ segs, int nsegs, int tile,
+                                               float lr_t, float b1, float b2, float eps, float gs,
+                                               float (*lds)[TA + 1]) {
+    const int si = find_segment(segs, nsegs, tile);
     const seg_adam_segment sg = segs[si];
     const int ta = (sg.a + TA - 1) / TA, tb = (sg.b + TB - 1) / TB;
-    int t = blockIdx.x - sg.tile_begin;
+    int t = tile - sg.tile_begin;
     const int rs = t / (ta * tb);
     t -= rs * ta * tb;
     const int a0 = (t / tb) * TA, b0 = (t - (t / tb) * tb) * TB;
@@ -138,7 +138,25 @@ __global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const 
     }
 }
 
+// one tile per block (full grid), or -- capped grid -- each block walks tiles
+// blockIdx.x, +gridDim.x, ...: a low-occupancy update that streams HBM beside
+// MFMA-bound kernels on another stream instead of taking their CUs
+template <typename T>
+__global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const float* __restrict__ G,
+                                                    float* __restrict__ Mm, float* __restrict__ Vv,
+                                                    const seg_adam_segment* __restrict__ segs, int nsegs,
+                                                    int total_tiles, float lr_t, float b1, float b2, float eps,
+                                                    float gs) {
+    __shared__ float lds[TB][TA + 1];
+    for (int tile = blockIdx.x; tile < total_tiles; tile += gridDim.x) {
+        adam_pack_tile<T>(P, G, Mm, Vv, segs, nsegs, tile, lr_t, b1, b2, eps, gs, lds);
+        __syncthreads();          // the LDS transpose tile is reused by the next tile
+    }
+}
+
 }  // namespace
+
+int g_adam_blocks = 0;    // seg_set_option("adam_blocks"): grid cap of seg_adam_tf1_pack (0 = one block per tile)
 
 extern "C" int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs) {
     if (!segs || nsegs <= 0) return -SEG_EINVAL;
@@ -162,11 +180,12 @@ extern "C" int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, c
     if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return SEG_EALIGN;
     const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
     hipStream_t st = (hipStream_t)stream;
+    const int grid = g_adam_blocks > 0 ? std::min(total_tiles, g_adam_blocks) : total_tiles;
     if (dtype == SEG_BF16)
-        hipLaunchKernelGGL(adam_pack_k<bf16>, dim3(total_tiles), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs,
+        hipLaunchKernelGGL(adam_pack_k<bf16>, dim3(grid), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs, total_tiles,
                            (float)lr_t, b1, b2, eps, gs);
     else if (dtype == SEG_F32)
-        hipLaunchKernelGGL(adam_pack_k<float>, dim3(total_tiles), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs,
+        hipLaunchKernelGGL(adam_pack_k<float>, dim3(grid), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs, total_tiles,
                            (float)lr_t, b1, b2, eps, gs);
     else
         return SEG_EINVAL;

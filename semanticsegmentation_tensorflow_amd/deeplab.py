@@ -15,16 +15,18 @@ them onto the hot-path builders:
   3x3 branches `aspp1..3` (rates 6 / 12 / 18, the out_stride=16 rates of
   :150), each Conv2D_Block / Atrous_Conv2D_Block with frozen-stat BN + ReLU
   (utils.py:186-229), concatenated (Concat, utils.py:332) and projected by a
-  1x1 `concat_projection` block + Dropout (:246-247);
-  the global-average-pool branch (b4, :213-225) is omitted (no such op on the
-  hot path; the reference's MobileNetV2 head also uses two branches only);
+  1x1 `concat_projection` block + Dropout (:246-247); first in the concat,
+  the image-pooling branch b4 (:213-225): Global_Avg_Pool (utils.py:312),
+  two expand_dims, a 1x1 `image_pooling` Conv2D_Block with BN + ReLU and
+  Resize_Bilinear back to the feature map size (tf.shape(feat)[1:3]);
 * classifier `Last_layer` (1x1, :262) and Resize_Bilinear (align_corners,
   utils.py:329) back to the input size (:264-266).
 
 Returns (expand_dims(argmax(logits)), logits) like FCN.create().
 """
 from . import tf
-from .layers import STDDEV, Atrous_Conv2D_Block, Concat, Conv2D_Block, Dropout, Resize_Bilinear, conv_layer, max_pool
+from .layers import (STDDEV, Atrous_Conv2D_Block, Concat, Conv2D_Block, Dropout, Global_Avg_Pool, Resize_Bilinear,
+                     conv_layer, max_pool)
 
 ASPP_RATES = (6, 12, 18)
 ASPP_DEPTH = 256
@@ -60,9 +62,17 @@ def DeepLabASPP(x, keep_prob, num_classes):
     h = atrous_conv_layer(h, 512, "conv5_2", 2)
     feat = atrous_conv_layer(h, 512, "conv5_3", 2)
 
+    # image feature branch (DeepLabv3Plus.py:215-223)
+    b4 = Global_Avg_Pool(feat)
+    b4 = tf.expand_dims(b4, dim=1)
+    b4 = tf.expand_dims(b4, dim=1)
+    b4 = Conv2D_Block(b4, ASPP_DEPTH, filter_height=1, filter_width=1, stride=1, padding="SAME",
+                      batch_normalization=True, relu=True, name="image_pooling")
+    size_before = tf.shape(feat)
+    b4 = Resize_Bilinear(b4, size_before[1:3], name="Upsampling")
     b0 = Conv2D_Block(feat, ASPP_DEPTH, filter_height=1, filter_width=1, batch_normalization=True, relu=True,
                       name="aspp0")
-    branches = [b0]
+    branches = [b4, b0]
     for i, r in enumerate(ASPP_RATES):
         branches.append(Atrous_Conv2D_Block(feat, ASPP_DEPTH, dilation=r, batch_normalization=True, relu=True,
                                             name=f"aspp{i + 1}"))

@@ -308,6 +308,8 @@ class ShapeOf:
         self.t = t
 
     def __getitem__(self, i):
+        if isinstance(i, slice):                    # size_before[1:3] (DeepLabv3Plus.py:222)
+            return [ShapeElem(self.t, j) for j in range(*i.indices(4))]
         return ShapeElem(self.t, i)
 
 
@@ -478,10 +480,22 @@ def _root_scope():
 
 
 def resize_bilinear(images, size, align_corners=True, name=None):
+    """size: two ints, Dimensions or tf.shape(t) elements (resolved at compile time)."""
     if not align_corners:
         raise NotImplementedError("only align_corners=True (utils.py:330)")
-    op = Op("ResizeBilinear", [images], {"size": tuple(size)}, name)
-    op.outputs[0].shape = (images.shape[0], size[0], size[1], images.shape[3])
+    size = tuple(size)
+    op = Op("ResizeBilinear", [images], {"size": size}, name)
+    st = [v if not isinstance(v, ShapeElem) else _static(v.t, v.i) for v in size]
+    op.outputs[0].shape = (images.shape[0], getattr(st[0], "value", st[0]), getattr(st[1], "value", st[1]),
+                           images.shape[3])
+    return op.outputs[0]
+
+
+def global_avg_pool(x, name=None):
+    """tflearn global_avg_pool (Network/utils/utils.py:312): tf.reduce_mean(x,
+    [1, 2]) -> [N, C]."""
+    op = Op("GlobalAvgPool", [x], {}, name or "global_avg_pooling")
+    op.outputs[0].shape = (x.shape[0], x.shape[3])
     return op.outputs[0]
 
 
@@ -508,8 +522,11 @@ def argmax(x, dimension=3, axis=None, name=None):
 
 
 def expand_dims(x, dim=-1, axis=None, name=None):
-    op = Op("ExpandDims", [x], {}, name)
-    op.outputs[0].shape = tuple(x.shape) + (1,)
+    d = axis if axis is not None else dim
+    shp = list(x.shape)
+    d = d if d >= 0 else len(shp) + 1 + d
+    op = Op("ExpandDims", [x], {"dim": d}, name)
+    op.outputs[0].shape = tuple(shp[:d] + [1] + shp[d:])
     op.outputs[0].dtype = x.dtype
     return op.outputs[0]
 

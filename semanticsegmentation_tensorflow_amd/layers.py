@@ -146,6 +146,11 @@ def Avg_Pooling(x, name, filter_height=2, filter_width=2, stride_height=2, strid
                           strides=[1, stride_height, stride_width, 1], padding=padding, name=name)
 
 
+def Global_Avg_Pool(x, stride=1):
+    """utils.py:312-313: tflearn global_avg_pool -> [N, C]."""
+    return tf.nn.global_avg_pool(x, name="global_avg_pooling")
+
+
 def Dropout(x, keep_prob):
     return tf.nn.dropout(x, keep_prob=keep_prob)
 

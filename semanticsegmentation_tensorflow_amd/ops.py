@@ -393,6 +393,25 @@ def resize_bilinear_bwd(dy, dx_f32, stream=None):
     return dx_f32
 
 
+def spatial_reduce(x, y, scale, ws, stream=None):
+    """y[n, 0, 0, c] = scale * sum_hw x[n, h, w, c] (x [N,H,W,C], y [N,1,1,C], padded C)."""
+    N, H, W, C = x.shape
+    assert y.shape[0] == N and y.shape[-1] == C
+    wsp, _ = ws.ptr_size(4 * N * C)
+    check(_lib.lib().seg_spatial_reduce(ptr(x), pixel_stride(x), ptr(y), N, H, W, C, float(scale),
+                                        wsp, seg_dtype(x), stream_ptr(stream)), "spatial_reduce")
+    return y
+
+
+def spatial_broadcast(x, y, scale, stream=None):
+    """y[n, h, w, c] = scale * x[n, 0, 0, c] (padded C)."""
+    N, H, W, C = y.shape
+    assert x.shape[0] == N and x.shape[-1] == C
+    check(_lib.lib().seg_spatial_broadcast(ptr(x), ptr(y), pixel_stride(y), N, H, W, C, float(scale),
+                                           seg_dtype(y), stream_ptr(stream)), "spatial_broadcast")
+    return y
+
+
 class ConcatPart(ctypes.Structure):
     """seg_concat_part (include/segkern.h)."""
     _fields_ = [("ptr", ctypes.c_void_p), ("ld", ctypes.c_int), ("channels", ctypes.c_int),

@@ -474,7 +474,7 @@ class Session:
             elif t == "Placeholder":
                 nodes.append(_Node("input", [op], [], y))
             elif t in ("MaxPool", "AvgPool", "Add", "Relu", "Dropout", "BiasAdd", "ConcatV2",
-                       "ResizeBilinear", "ArgMax", "ExpandDims", "Softmax"):
+                       "ResizeBilinear", "ArgMax", "ExpandDims", "Softmax", "GlobalAvgPool"):
                 nodes.append(_Node(t, [op], list(op.inputs), y))
             elif t == "Mean":
                 raise NotImplementedError("reduce_mean is only supported on the xent loss")
@@ -517,7 +517,11 @@ class Session:
             return tuple(ins[0][:3]) + (sum(s[3] for s in ins),)
         if t == "ResizeBilinear":
             N, H, W, C = ins[0]
-            return (N, op.attrs["size"][0], op.attrs["size"][1], C)
+            OH, OW = G.resolve_shape(op.attrs["size"], lambda tt: shp[id(tt)])
+            return (N, int(OH), int(OW), C)
+        if t == "GlobalAvgPool":          # kept 4-D on the device: [N, 1, 1, C]
+            N, H, W, C = ins[0]
+            return (N, 1, 1, C)
         if t == "SoftmaxXent":
             return tuple(ins[0][:3])
         if t == "Mean":
@@ -525,6 +529,8 @@ class Session:
         if t == "ArgMax":
             return tuple(ins[0][:3])
         if t == "ExpandDims":
+            if len(ins[0]) == 4:          # global-average-pool chain: already [N, 1, 1, C]
+                return tuple(ins[0])
             return tuple(ins[0]) + (1,)
         raise NotImplementedError(t)
 
@@ -638,7 +644,7 @@ class Session:
                 continue
             if n.kind == "ExpandDims":
                 src = buf[id(n.inputs[0])]
-                buf[id(y)] = src.unsqueeze(-1)
+                buf[id(y)] = src if len(shp[id(y)]) == 4 and src.dim() == 4 else src.unsqueeze(-1)
                 continue
             s = shp[id(y)]
             if id(y) in p.alias:
@@ -916,7 +922,14 @@ class Session:
             elif k == "Softmax":
                 ops.softmax(buf[id(n.inputs[0])], y, p.shapes[id(n.inputs[0])][3])
             elif k == "ResizeBilinear":
-                ops.resize_bilinear_fwd(buf[id(n.inputs[0])], y)
+                x = buf[id(n.inputs[0])]
+                if x.shape[1] == 1 and x.shape[2] == 1:      # align_corners from 1x1: a broadcast
+                    ops.spatial_broadcast(x, y, 1.0)
+                else:
+                    ops.resize_bilinear_fwd(x, y)
+            elif k == "GlobalAvgPool":
+                x = buf[id(n.inputs[0])]
+                ops.spatial_reduce(x, y, 1.0 / (x.shape[1] * x.shape[2]), self.ws)
             elif k == "ExpandDims":
                 pass
             else:
@@ -934,8 +947,9 @@ class Session:
                     and p.adam_fusable:
                 self._fused = (opt, gs, set())
             self._red = None
-            if self.defer_wgrad_reduce and self.dp is None and not self.overlap_optimizer and \
-                    self.device.type == "cuda":
+            if self.defer_wgrad_reduce and self.dp is None and self.device.type == "cuda":
+                # (with the overlapped optimizer the reductions and each layer's
+                # Adam share the side stream: a layer's reduction precedes its update)
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self.device)
                 self._red = (self._side, torch.cuda.current_stream(self.device))
@@ -1269,6 +1283,21 @@ class Session:
                 else:
                     ops.copy_channels(dy, dx)
                 done(dx, acc)
+            elif k == "GlobalAvgPool":
+                x = n.inputs[0]
+                if id(x) in ng:
+                    dx, acc = dest(x)
+                    xs = buf[id(x)]
+                    ops.spatial_broadcast(dy, dx, 1.0 / (xs.shape[1] * xs.shape[2]))
+                    done(dx, acc)
+            elif k == "ExpandDims" and len(p.shapes[id(n.output)]) == 4 and len(p.shapes[id(n.inputs[0])]) == 4:
+                contribute_alias(n.inputs[0], dy)          # global-average-pool chain: same buffer
+            elif k == "ResizeBilinear" and buf[id(n.inputs[0])].shape[1] == 1 and buf[id(n.inputs[0])].shape[2] == 1:
+                x = n.inputs[0]
+                if id(x) in ng:                            # 1x1 -> HxW broadcast: gradient = spatial sum
+                    dx, acc = dest(x)
+                    ops.spatial_reduce(dy, dx, 1.0, self.ws)
+                    done(dx, acc)
             elif k == "ResizeBilinear":
                 # align_corners bilinear: fp32 scatter-add, then cast to the compute dtype
                 x = n.inputs[0]

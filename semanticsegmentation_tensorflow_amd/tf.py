@@ -46,6 +46,7 @@ nn = SimpleNamespace(
     avg_pool=_g.avg_pool,
     dropout=_g.dropout,
     softmax=_g.softmax,
+    global_avg_pool=_g.global_avg_pool,
     softmax_cross_entropy_with_logits=_g.softmax_cross_entropy_with_logits,
 )
 layers = SimpleNamespace(batch_normalization=_g.batch_normalization)
