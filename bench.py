@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "train images/sec on KITTI 375×1242 2-class at 1/2/4/8 MI355X; mIoU parity"
-PEAK = {"bf16": 2.5e15, "f32": 157.3e12}          # dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK = {"bf16": 2.5e15, "f16": 2.5e15, "f32": 157.3e12}   # dense MFMA peaks (MI355X_MICROARCH.md)
+DEFAULT_DTYPE = {"fcn": "bf16", "fcdensenet": "bf16", "deeplab": "f16"}   # C5: "fp16 with fp32 accum"
 HBM_PEAK = 8.0e12                                  # HBM3E bytes/s (MI355X_MICROARCH.md)
 FCN_TRAIN_FLOP_PER_IMG = 1348.97e9                 # SURVEY.md 8d at 384x1248, C_in=3
 
@@ -43,7 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (fcn 4, fcdensenet 8, deeplab 2)")
     ap.add_argument("--height", type=int, default=None, help="375 (KITTI); deeplab 1024")
     ap.add_argument("--width", type=int, default=None, help="1242 (KITTI); deeplab 2048")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "f16", "f32"],
+                    help="compute dtype (default: bf16; f16 + dynamic loss scaling for --model deeplab, config C5)")
     ap.add_argument("--keep-prob", type=float, default=None,
                     help="fcn 0.8 (FCN.py:395), fcdensenet 0.2 (FCDenseNet.py:13)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -378,7 +380,7 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
     per = {}
     step_conv_flops = 0.0
     rows = []
-    esz = 2 if dtype == "bf16" else 4
+    esz = 4 if dtype == "f32" else 2
     for desc, op, s_ev, e_ev in sess.timer:
         name, splits, flops = ops.conv_kernel_info(desc, op)
         ms = s_ev.elapsed_time(e_ev)
@@ -415,6 +417,9 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
     out.update({"value": B * world * steps / elapsed, "ms_per_step": ms_per_step, "roofline": roof,
                 "step_mfma_frac": step_flops / (ms_per_step * 1e-3) / peak,
                 "conv_gflop_per_step": step_conv_flops / 1e9, "rows": rows, "groups": per})
+    if dtype == "f16":
+        out["loss_scaling"] = {"kind": "dynamic" if sess.dynamic_scale else "fixed", "scale": sess.loss_scale,
+                               "skipped_steps": sess.skipped_steps}
     del sess
     torch.cuda.empty_cache()
     return out
@@ -424,12 +429,14 @@ def extra_config(model, dtype, device, steps, warmup):
     """C3 / C5 measured in the same run as the headline (a reported side line;
     the headline metric stays C2)."""
     H, W, B, kp = DEFAULTS[model]
+    dtype = DEFAULT_DTYPE[model] if dtype is None else dtype
     m = measure(model, B, H, W, kp, steps, warmup, dtype, device)
     return {"config": {"workload": WORKLOAD[model], "batch": B, "image": f"{H}x{W} -> {m['HP']}x{m['WP']}",
                        "keep_prob": kp},
             "value": round(m["value"], 3), "unit": "images/s", "steps": steps, "warmup": warmup,
             "ms_per_step": round(m["ms_per_step"], 3), "dtype": dtype,
-            "step_mfma_frac": round(m["step_mfma_frac"], 4), "roofline": m["roofline"]}
+            "step_mfma_frac": round(m["step_mfma_frac"], 4), "roofline": m["roofline"],
+            **({"loss_scaling": m["loss_scaling"]} if "loss_scaling" in m else {})}
 
 
 def main():
@@ -453,6 +460,8 @@ def main():
         name, val = kv.split("=")
         ops.set_option(name, int(val))
     dH, dW, dB, dkp = DEFAULTS[args.model]
+    if args.dtype is None:
+        args.dtype = DEFAULT_DTYPE[args.model]
     H, W = args.height or dH, args.width or dW
     B = args.batch or dB
     kp = args.keep_prob if args.keep_prob is not None else dkp
@@ -498,6 +507,8 @@ def main():
         "loss_after": round(m["loss"], 5),
         "miou_parity": m.get("miou"),
     }
+    if "loss_scaling" in m:
+        result["loss_scaling"] = m["loss_scaling"]
     if rank == 0 and world == 1 and not args.no_pipeline and args.model == "fcn":
         try:
             result["data_pipeline"] = pipeline_rate(H, W, device)
@@ -520,7 +531,7 @@ def main():
         # C3 and C5 in the same run (side lines; the headline stays C2)
         for key, model in (("c3_fcdensenet", "fcdensenet"), ("c5_deeplab", "deeplab")):
             try:
-                result[key] = extra_config(model, args.dtype, device, args.extra_steps, 3)
+                result[key] = extra_config(model, None, device, args.extra_steps, 3)
             except Exception as exc:  # report, never crash the headline line
                 result[key] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

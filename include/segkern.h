@@ -30,7 +30,11 @@
 extern "C" {
 #endif
 
-enum seg_dtype { SEG_F32 = 0, SEG_BF16 = 1 };
+/* SEG_F16: IEEE half storage with fp32 accumulation (v_mfma_f32_16x16x32_f16),
+ * config C5's "fp16 with fp32 accum" (BASELINE.json configs[4]); runs on the
+ * generic implicit-GEMM kernels (the bf16-specialised halo / 256x256 paths are
+ * bf16 only). */
+enum seg_dtype { SEG_F32 = 0, SEG_BF16 = 1, SEG_F16 = 2 };
 
 enum seg_status {
     SEG_OK = 0,
@@ -390,6 +394,10 @@ int seg_fill(void* y, long n, float value, int dtype, void* stream);
  * `accum.assign_add(tf.scalar_mul(const, grad))` (Network/main.py:92-95,
  * Network/model/FCDenseNet.py:213). */
 int seg_axpy(float* y, const float* x, float alpha, long n, void* stream);
+/* *flag = 1 if any of the n fp32 values is Inf / NaN, else 0 (dynamic loss
+ * scaling for the fp16 path: a step with overflowed scaled gradients is
+ * skipped and the scale halved, as TF's DynamicLossScale). g 16-byte aligned. */
+int seg_check_finite(const float* g, long n, int* flag, void* stream);
 int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);
 const char* seg_status_string(int status);
 int seg_version(void);

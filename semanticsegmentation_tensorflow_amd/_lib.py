@@ -171,6 +171,7 @@ SIGNATURES = {
     "seg_fill": (_I, [_P, _L, _F, _I, _P]),
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
     "seg_axpy": (_I, [_P, _P, _F, _L, _P]),
+    "seg_check_finite": (_I, [_P, _L, _P, _P]),
     "seg_status_string": (ctypes.c_char_p, [_I]),
     "seg_version": (_I, []),
 }

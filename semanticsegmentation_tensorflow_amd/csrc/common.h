@@ -7,8 +7,10 @@
 #include "../../include/segkern.h"
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -23,12 +25,34 @@ template <> struct dt_traits<bf16> {
     static constexpr int EPC = 8;
     static constexpr int id = SEG_BF16;
 };
+template <> struct dt_traits<f16> {
+    static constexpr int EPC = 8;
+    static constexpr int id = SEG_F16;
+};
+template <typename T> inline constexpr bool is_bf16_v = false;
+template <> inline constexpr bool is_bf16_v<bf16> = true;
+template <typename T> inline constexpr bool is_f16_v = false;
+template <> inline constexpr bool is_f16_v<f16> = true;
 
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(bf16 v) { return (float)v; }
+__device__ __forceinline__ float to_f32(f16 v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f32(float v);
 template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+template <> __device__ __forceinline__ f16 from_f32<f16>(float v) { return (f16)v; }
+
+// 16x16x32 MFMA on eight packed 16-bit elements per lane (A, B as loaded from
+// LDS), fp32 accumulation: bf16 or IEEE half operands
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16x16x32(const uint4& a, const uint4& b, const f32x4& c) {
+    if constexpr (is_f16_v<T>)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                       c, 0, 0, 0);
+}
 
 // 16-byte chunk <-> floats
 template <typename T> struct Chunk;
@@ -60,6 +84,27 @@ template <> struct Chunk<bf16> {
             bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
             w[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) |
                    ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+        }
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    }
+};
+
+template <> struct Chunk<f16> {
+    static constexpr int N = 8;
+    __device__ __forceinline__ static void unpack(const uint4& u, float* f) {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f[2 * i] = (float)__builtin_bit_cast(f16, (uint16_t)(w[i] & 0xffffu));
+            f[2 * i + 1] = (float)__builtin_bit_cast(f16, (uint16_t)(w[i] >> 16));
+        }
+    }
+    __device__ __forceinline__ static uint4 pack(const float* f) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f16 lo = (f16)f[2 * i], hi = (f16)f[2 * i + 1];
+            w[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
         }
         return make_uint4(w[0], w[1], w[2], w[3]);
     }

@@ -29,7 +29,7 @@ static int valid_out(int in, int k, int s, int d) {
 
 static int check_desc(const seg_conv_desc* d) {
     if (!d) return SEG_EINVAL;
-    if (d->dtype != SEG_F32 && d->dtype != SEG_BF16) return SEG_EINVAL;
+    if (d->dtype != SEG_F32 && d->dtype != SEG_BF16 && d->dtype != SEG_F16) return SEG_EINVAL;
     if (d->N <= 0 || d->H <= 0 || d->W <= 0 || d->OH <= 0 || d->OW <= 0 || d->R <= 0 || d->S <= 0) return SEG_ESHAPE;
     if ((d->C & 7) || (d->K & 7) || (d->ldx & 7) || (d->ldy & 7)) return SEG_EALIGN;
     if (d->ldx < d->C || d->ldy < d->K) return SEG_EALIGN;
@@ -219,7 +219,7 @@ __global__ void tconv_col2im_k(const T* __restrict__ Z, T* __restrict__ y, int N
                 const int iw = (ow + pl - s2) / st;
                 if (iw < 0 || iw >= W) continue;
                 const T* zp = Z + (((long)n * H + ih) * W + iw) * zrow + (r * S + s2) * KQ;
-                if constexpr (sizeof(T) == 2 && KQ == 2) {
+                if constexpr (is_bf16_v<T> && KQ == 2) {
                     const unsigned u = *reinterpret_cast<const unsigned*>(zp);
                     acc[0] += __uint_as_float(u << 16);
                     acc[1] += __uint_as_float(u & 0xffff0000u);
@@ -270,7 +270,7 @@ __global__ void tconv_gather_dy_k(const T* __restrict__ dy, T* __restrict__ D, i
         for (int j = 0; j < TPC; ++j) {
             const int ow = iw * st - pl + s0 + j;
             const bool ok = rok && (unsigned)ow < (unsigned)OW;
-            if constexpr (sizeof(T) == 2 && KQ == 2) {
+            if constexpr (is_bf16_v<T> && KQ == 2) {
                 const unsigned u = ok ? *reinterpret_cast<const unsigned*>(src + (long)ow * ldy) : 0u;
                 v[2 * j] = __uint_as_float(u << 16);
                 v[2 * j + 1] = __uint_as_float(u & 0xffff0000u);
@@ -295,7 +295,7 @@ static int tconv_dense_kq(const seg_conv_desc* d) {
 }
 
 static size_t tconv_dense_zbytes(const seg_conv_desc* d) {
-    const size_t esz = d->dtype == SEG_BF16 ? 2 : 4;
+    const size_t esz = d->dtype == SEG_F32 ? 4 : 2;
     return ((size_t)d->N * d->H * d->W * d->R * d->S * tconv_dense_kq(d) * esz + 255) & ~(size_t)255;
 }
 
@@ -319,6 +319,8 @@ static int launch_gather_dy(const seg_conv_desc* d, const void* dy, void* D, hip
                                          d->N, d->H, d->W, d->OH, d->OW, d->ldy, d->R, d->S, d->stride_h, d->pad_top, d->pad_left)
     if (d->dtype == SEG_BF16) {
         if (kq == 2) GATHER(bf16, 2); else if (kq == 4) GATHER(bf16, 4); else GATHER(bf16, 8);
+    } else if (d->dtype == SEG_F16) {
+        if (kq == 2) GATHER(f16, 2); else if (kq == 4) GATHER(f16, 4); else GATHER(f16, 8);
     } else {
         if (kq == 2) GATHER(float, 2); else if (kq == 4) GATHER(float, 4); else GATHER(float, 8);
     }
@@ -383,7 +385,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
     if (st) return st;
     int bm = 0, bn = 0, sp = 1;
     const char* fam = "igemm_nt";
-    const char* ty = d->dtype == SEG_BF16 ? "bf16" : "f32";
+    const char* ty = d->dtype == SEG_BF16 ? "bf16" : d->dtype == SEG_F16 ? "f16" : "f32";
     const double macs_conv = (double)d->N * d->OH * d->OW * d->R * d->S * d->c_valid * d->k_valid;
     // conv2d_transpose MACs: every input pixel meets every tap
     const double macs_t = (double)d->N * d->H * d->W * d->R * d->S * d->c_valid * d->k_valid;
@@ -812,6 +814,8 @@ extern "C" int seg_tconv2d_fwd(const seg_conv_desc* d, const void* x, const void
                                          d->stride_h, d->pad_top, d->pad_left, d->ldy, bias, (const T*)res, ldr)
         if (d->dtype == SEG_BF16) {
             if (kq == 2) COL2IM(bf16, 2); else if (kq == 4) COL2IM(bf16, 4); else COL2IM(bf16, 8);
+        } else if (d->dtype == SEG_F16) {
+            if (kq == 2) COL2IM(f16, 2); else if (kq == 4) COL2IM(f16, 4); else COL2IM(f16, 8);
         } else {
             if (kq == 2) COL2IM(float, 2); else if (kq == 4) COL2IM(float, 4); else COL2IM(float, 8);
         }
@@ -914,7 +918,7 @@ __global__ void pack_rows_k(const float* __restrict__ src, T* __restrict__ dst, 
         }
         T* d = dst + ra * bp + b0;
         if constexpr (sizeof(T) == 2) {
-            *reinterpret_cast<uint4*>(d) = Chunk<bf16>::pack(v);
+            *reinterpret_cast<uint4*>(d) = Chunk<T>::pack(v);
         } else {
             *reinterpret_cast<uint4*>(d) = Chunk<float>::pack(v);
             *reinterpret_cast<uint4*>(d + 4) = Chunk<float>::pack(v + 4);
@@ -958,6 +962,8 @@ extern "C" int seg_pack_filter(const float* src, void* dst, int R, int S, int a_
             hipLaunchKernelGGL(pack_transpose_k<bf16>, grid, dim3(256), 0, st, src, (bf16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
         else if (dtype == SEG_F32)
             hipLaunchKernelGGL(pack_transpose_k<float>, grid, dim3(256), 0, st, src, (float*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else if (dtype == SEG_F16)
+            hipLaunchKernelGGL(pack_transpose_k<f16>, grid, dim3(256), 0, st, src, (f16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
         else
             return SEG_EINVAL;
     } else {
@@ -967,6 +973,8 @@ extern "C" int seg_pack_filter(const float* src, void* dst, int R, int S, int a_
             hipLaunchKernelGGL(pack_rows_k<bf16>, dim3(grid), dim3(256), 0, st, src, (bf16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
         else if (dtype == SEG_F32)
             hipLaunchKernelGGL(pack_rows_k<float>, dim3(grid), dim3(256), 0, st, src, (float*)dst, RS, a_valid, b_valid, a_pad, b_pad);
+        else if (dtype == SEG_F16)
+            hipLaunchKernelGGL(pack_rows_k<f16>, dim3(grid), dim3(256), 0, st, src, (f16*)dst, RS, a_valid, b_valid, a_pad, b_pad);
         else
             return SEG_EINVAL;
     }

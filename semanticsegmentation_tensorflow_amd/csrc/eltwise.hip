@@ -833,11 +833,14 @@ __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float
         } else if ((dtype) == SEG_F32) {                \
             typedef float T;                            \
             KERNEL_CALL;                                \
+        } else if ((dtype) == SEG_F16) {                \
+            typedef f16 T;                              \
+            KERNEL_CALL;                                \
         } else                                          \
             return SEG_EINVAL;                          \
     } while (0)
 
-static inline int epc_of(int dtype) { return dtype == SEG_BF16 ? 8 : 4; }
+static inline int epc_of(int dtype) { return dtype == SEG_F32 ? 4 : 8; }
 
 extern "C" size_t seg_bias_grad_workspace(long P, int K) {
     (void)P;
@@ -959,6 +962,30 @@ extern "C" int seg_fill(void* y, long n, float v, int dtype, void* stream) {
     return SEG_OK;
 }
 
+// any non-finite element of n fp32 values -> *flag = 1 (dynamic loss scaling:
+// a step whose scaled gradients overflowed is skipped)
+__global__ void check_finite_k(const float* __restrict__ g, long n, int* __restrict__ flag) {
+    bool bad = false;
+    const long n4 = n / 4;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+        const float4 v = reinterpret_cast<const float4*>(g)[i];
+        bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    }
+    for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        bad |= !isfinite(g[i]);
+    if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+extern "C" int seg_check_finite(const float* g, long n, int* flag, void* stream) {
+    if (!g || !flag || n < 0 || ((uintptr_t)g & 15)) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(flag, 0, sizeof(int), s) != hipSuccess) return SEG_ELAUNCH;
+    if (n == 0) return SEG_OK;
+    hipLaunchKernelGGL(check_finite_k, dim3(seg_grid_1d(n / 4 + 1, 256, 4096)), dim3(256), 0, s, g, n, flag);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
 extern "C" int seg_axpy(float* y, const float* x, float alpha, long n, void* stream) {
     if (!y || !x || n < 0) return SEG_EINVAL;
     if (n == 0) return SEG_OK;
@@ -975,6 +1002,9 @@ extern "C" int seg_cast(const void* x, int xd, void* y, int yd, long n, void* st
     else if (xd == SEG_BF16 && yd == SEG_F32) hipLaunchKernelGGL((cast_k<bf16, float>), dim3(g), dim3(256), 0, s, (const bf16*)x, (float*)y, n);
     else if (xd == SEG_F32 && yd == SEG_F32) hipLaunchKernelGGL((cast_k<float, float>), dim3(g), dim3(256), 0, s, (const float*)x, (float*)y, n);
     else if (xd == SEG_BF16 && yd == SEG_BF16) hipLaunchKernelGGL((cast_k<bf16, bf16>), dim3(g), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n);
+    else if (xd == SEG_F32 && yd == SEG_F16) hipLaunchKernelGGL((cast_k<float, f16>), dim3(g), dim3(256), 0, s, (const float*)x, (f16*)y, n);
+    else if (xd == SEG_F16 && yd == SEG_F32) hipLaunchKernelGGL((cast_k<f16, float>), dim3(g), dim3(256), 0, s, (const f16*)x, (float*)y, n);
+    else if (xd == SEG_F16 && yd == SEG_F16) hipLaunchKernelGGL((cast_k<f16, f16>), dim3(g), dim3(256), 0, s, (const f16*)x, (f16*)y, n);
     else return SEG_EINVAL;
     SEG_CHECK_LAUNCH();
     return SEG_OK;
@@ -1053,7 +1083,7 @@ extern "C" int seg_concat_bwd(const void* dy, int ldy, const seg_concat_part* pa
 
 extern "C" int seg_prepare_input(const float* img, void* x, int N, int H, int W, int cin, int HP, int WP, int CP,
                                  int dtype, void* stream) {
-    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_BF16 ? 8 : 4)) return SEG_EINVAL;
+    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_F32 ? 4 : 8)) return SEG_EINVAL;
     const long total = (long)N * HP * WP * CP;
     DISPATCH_T(dtype, hipLaunchKernelGGL(prepare_input_k<T>, dim3(seg_grid_1d(total / CP + 1, 256)), dim3(256), 0,
                                          (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));
@@ -1063,7 +1093,7 @@ extern "C" int seg_prepare_input(const float* img, void* x, int N, int H, int W,
 
 extern "C" int seg_prepare_input_u8(const uint8_t* img, void* x, int N, int H, int W, int cin, int HP, int WP, int CP,
                                     int dtype, void* stream) {
-    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_BF16 ? 8 : 4)) return SEG_EINVAL;
+    if (!img || !x || HP < H || WP < W || CP < cin || CP % (dtype == SEG_F32 ? 4 : 8)) return SEG_EINVAL;
     const long total = (long)N * HP * WP * CP;
     DISPATCH_T(dtype, hipLaunchKernelGGL((prepare_input_k<T, uint8_t>), dim3(seg_grid_1d(total / CP + 1, 256)),
                                          dim3(256), 0, (hipStream_t)stream, img, (T*)x, N, H, W, cin, HP, WP, CP));

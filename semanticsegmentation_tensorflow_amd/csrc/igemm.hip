@@ -243,9 +243,7 @@ __global__ __launch_bounds__(256) void igemm_nt(NTParams p) {
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
                     if constexpr (sizeof(T) == 2) {
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]),
-                            acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
                     } else {
                         const f32x4 a4 = __builtin_bit_cast(f32x4, af[mi]);
                         const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[ni]);
@@ -477,7 +475,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
         if constexpr (BF) {
 #pragma unroll
             for (int ks = 0; ks < BKP / 32; ++ks) {
-                bf16x8 af[TM], bfr[TN];
+                uint4 af[TM], bfr[TN];
                 const int r1 = ks * 32 + 8 * fg + tq;
 #pragma unroll
                 for (int mi = 0; mi < TM; ++mi) {
@@ -488,7 +486,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)p2);
                     typedef short s16x8 __attribute__((ext_vector_type(8)));
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    af[mi] = __builtin_bit_cast(bf16x8, v);
+                    af[mi] = __builtin_bit_cast(uint4, v);
                 }
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
@@ -499,13 +497,13 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)p2);
                     typedef short s16x8 __attribute__((ext_vector_type(8)));
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    bfr[ni] = __builtin_bit_cast(bf16x8, v);
+                    bfr[ni] = __builtin_bit_cast(uint4, v);
                 }
 #pragma unroll
                 for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
             }
         } else {
 #pragma unroll
@@ -641,7 +639,7 @@ static void choose_nt(int M, int N, int K, int bk, int& bm, int& bn, int& splits
 }
 
 void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* splits) {
-    choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, *bm, *bn, *splits);
+    choose_nt(M, N, K, dtype == SEG_F32 ? 32 : 64, *bm, *bn, *splits);
     if (phase) *splits = 1;
 }
 
@@ -652,7 +650,7 @@ void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     if (phase) return 0;
     int bm, bn, splits;
-    choose_nt(M, N, K, dtype == SEG_BF16 ? 64 : 32, bm, bn, splits);
+    choose_nt(M, N, K, dtype == SEG_F32 ? 32 : 64, bm, bn, splits);
     if (g_nt_variant == 2 && nt3_applies(N, dtype)) {
         int s3, s4;
         nt3_info(M, N, K, num_cus(), &s3);
@@ -692,13 +690,13 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
     if (nphases > 1) splits = 1;
     p.partial = nullptr;
-    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
+    if (is_bf16_v<T> && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
         launch_res64(p, num_cus(), s);
         SEG_CHECK_LAUNCH();
         return SEG_OK;
     }
     HaloPlan hp;
-    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, splits, num_cus(), &hp)) {
+    if (is_bf16_v<T> && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, splits, num_cus(), &hp)) {
         if (hp.splits > 1) {
             const size_t need = (size_t)hp.splits * p.M * p.N * sizeof(float);
             if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
@@ -714,7 +712,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         }
         return SEG_OK;
     }
-    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m);
+    const bool nt3 = is_bf16_v<T> && g_nt_variant == 2 && nt3_pick(p, nphases, max_m);
     const bool nt4 = nt3 && nt4_ok(p, SEG_BF16);
     if (nt4) {
         nt4_info(max_m, p.N, p.K, num_cus(), &splits);
@@ -751,7 +749,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
 
 // The kernel launch_nt would pick for p (host-only mirror of launch_nt_typed).
 const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits) {
-    const int bk = dtype == SEG_BF16 ? 64 : 32;
+    const int bk = dtype == SEG_F32 ? 32 : 64;
     choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
     if (nphases > 1) *splits = 1;
     if (dtype == SEG_BF16 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
@@ -777,13 +775,14 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {
     if (dtype == SEG_BF16) return launch_nt_typed<bf16>(p, nphases, max_m, ws, ws_bytes, s);
     if (dtype == SEG_F32) return launch_nt_typed<float>(p, nphases, max_m, ws, ws_bytes, s);
+    if (dtype == SEG_F16) return launch_nt_typed<f16>(p, nphases, max_m, ws, ws_bytes, s);
     return SEG_EINVAL;
 }
 
 int g_tn_variant = 2;
 
-static void choose_tn(int M, int N, int P, int bkp, int& bm, int& bn, int& splits) {
-    if (g_tn_variant == 2 && bkp == 64 && M >= 128) {
+static void choose_tn(int M, int N, int P, int bkp, bool v2, int& bm, int& bn, int& splits) {
+    if (g_tn_variant == 2 && v2 && M >= 128) {
         // v2 tiles: minimise padded work / relative tile efficiency
         static const int cand[5][2] = {{128, 256}, {256, 128}, {128, 128}, {256, 64}, {128, 64}};
         static const double eff[5] = {1.0, 1.0, 0.85, 0.85, 0.8};
@@ -809,12 +808,12 @@ static void choose_tn(int M, int N, int P, int bkp, int& bm, int& bn, int& split
 }
 
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits) {
-    choose_tn(M, N, P, dtype == SEG_BF16 ? 64 : 32, *bm, *bn, *splits);
+    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype == SEG_BF16, *bm, *bn, *splits);
 }
 
 size_t tn_workspace(int M, int N, int P, int dtype) {
     int bm, bn, splits;
-    choose_tn(M, N, P, dtype == SEG_BF16 ? 64 : 32, bm, bn, splits);
+    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype == SEG_BF16, bm, bn, splits);
     if (g_tn_variant == 2 && tn3_applies(M, N, dtype)) {
         int s3;
         tn3_info(M, N, P, num_cus(), &s3);
@@ -853,7 +852,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
     p.partial = nullptr;
     p.Mp = p.M;
-    if (smallc_wgrad_ok(p, sizeof(T) == 2 ? SEG_BF16 : SEG_F32)) {
+    if (smallc_wgrad_ok(p, dt_traits<T>::id)) {
         const int splits = smallc_wgrad_splits(p, num_cus());
         if (p.dbias) p.Mp = p.M + 1;
         if (splits > 1) {
@@ -868,7 +867,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         return SEG_OK;
     }
     WgradPlan wp;
-    if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
+    if (is_bf16_v<T> && g_tn_variant == 2 && wgrad_plan(p, SEG_BF16, num_cus(), &wp)) {
         if (p.dbias) p.Mp = p.M + wp.nbias;   // wgrad_halo sums dy columns too (nbias partial rows)
         if (wp.splits > 1) {
             if (!ws || ws_bytes < wgrad_workspace(wp, p)) return SEG_EWORKSPACE;
@@ -882,8 +881,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         return SEG_OK;
     }
     int bm, bn, splits;
-    choose_tn(p.M, p.N, p.P, BKP, bm, bn, splits);
-    const bool tn3 = sizeof(T) == 2 && g_tn_variant == 2 && tn3_ok(p, SEG_BF16);
+    choose_tn(p.M, p.N, p.P, BKP, is_bf16_v<T>, bm, bn, splits);
+    const bool tn3 = is_bf16_v<T> && g_tn_variant == 2 && tn3_ok(p, SEG_BF16);
     if (tn3) tn3_info(p.M, p.N, p.P, num_cus(), &splits);
     int gridz = 1;
     if (splits > 1) {
@@ -897,7 +896,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     if (tn3) {
         launch_tn3(p, gridz, s);
-    } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
+    } else if (g_tn_variant == 2 && is_bf16_v<T> && (bm == 256 || bn == 256 || p.M >= 128)) {
         launch_tn2(p, bm, bn, gridz, s);
     } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
     else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);
@@ -912,6 +911,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
     if (dtype == SEG_BF16) return launch_tn_typed<bf16>(p, ws, ws_bytes, s);
     if (dtype == SEG_F32) return launch_tn_typed<float>(p, ws, ws_bytes, s);
+    if (dtype == SEG_F16) return launch_tn_typed<f16>(p, ws, ws_bytes, s);
     return SEG_EINVAL;
 }
 

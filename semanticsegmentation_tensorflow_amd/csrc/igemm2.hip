@@ -221,9 +221,7 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
                     if constexpr (ABL == 2) {
                         asm volatile("" ::"v"(af[mi].x), "v"(af[mi].w), "v"(bfr[ni].x), "v"(bfr[ni].w));
                     } else if constexpr (sizeof(T) == 2) {
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]), acc[mi][ni], 0,
-                            0, 0);
+                        acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
                     } else {
                         const f32x4 a4 = __builtin_bit_cast(f32x4, af[mi]);
                         const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[ni]);
@@ -528,7 +526,7 @@ template <typename T, int BM, int BN, int WM, int WN>
 void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const dim3 g(tiles, 1, gridz), b(WM * WN * 64);
-    if constexpr (sizeof(T) == 2 && BN == 128) {
+    if constexpr (is_bf16_v<T> && BN == 128) {
         switch (g_nt2_ablate) {
             case 1: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 1>), g, b, 0, s, p); return;
             case 2: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 2>), g, b, 0, s, p); return;
@@ -553,6 +551,9 @@ void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_
             hipLaunchKernelGGL((igemm_nt2<bf16, 256, 64, 4, 2, 0, 2>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
         } else if (bn == 64) launch_nt2_t<bf16, 256, 64, 4, 2>(p, gridz, max_m, s);
         else launch_nt2_t<bf16, 256, 128, 4, 2>(p, gridz, max_m, s);
+    } else if (dtype == SEG_F16) {
+        if (bn == 64) launch_nt2_t<f16, 256, 64, 4, 2>(p, gridz, max_m, s);
+        else launch_nt2_t<f16, 256, 128, 4, 2>(p, gridz, max_m, s);
     } else {
         if (bn == 64) launch_nt2_t<float, 256, 64, 4, 2>(p, gridz, max_m, s);
         else launch_nt2_t<float, 256, 128, 4, 2>(p, gridz, max_m, s);

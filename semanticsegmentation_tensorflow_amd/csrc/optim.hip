@@ -20,8 +20,9 @@ namespace {
 
 constexpr int TA = 32, TB = 128;   // tile [a][b]; 256 threads = 32 lanes x float4 per b-row
 
-__device__ __forceinline__ uint2 pack4_bf16(const float* v) {
-    bf16 h[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+template <typename T>
+__device__ __forceinline__ uint2 pack4_16(const float* v) {   // four 16-bit (bf16 / half) values
+    T h[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
     return *reinterpret_cast<const uint2*>(h);
 }
 
@@ -96,7 +97,7 @@ __device__ __forceinline__ void adam_pack_tile(float* __restrict__ P, const floa
                 T* d = rows + ((long)rs * sg.rows_ap + a) * sg.rows_bp + b;
                 if (b + 4 <= sg.b) {
                     if constexpr (sizeof(T) == 2) {
-                        *reinterpret_cast<uint2*>(d) = pack4_bf16(pv);
+                        *reinterpret_cast<uint2*>(d) = pack4_16<T>(pv);
                     } else {
                         *reinterpret_cast<float4*>(d) = float4{pv[0], pv[1], pv[2], pv[3]};
                     }
@@ -126,8 +127,8 @@ __device__ __forceinline__ void adam_pack_tile(float* __restrict__ P, const floa
 #pragma unroll
         for (int j = 0; j < 16; ++j) v[j] = lds[blr][ab + j];
         if constexpr (sizeof(T) == 2) {
-            *reinterpret_cast<uint4*>(d) = Chunk<bf16>::pack(v);
-            *reinterpret_cast<uint4*>(d + 8) = Chunk<bf16>::pack(v + 8);
+            *reinterpret_cast<uint4*>(d) = Chunk<T>::pack(v);
+            *reinterpret_cast<uint4*>(d + 8) = Chunk<T>::pack(v + 8);
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -186,6 +187,9 @@ extern "C" int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, c
                            (float)lr_t, b1, b2, eps, gs);
     else if (dtype == SEG_F32)
         hipLaunchKernelGGL(adam_pack_k<float>, dim3(grid), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs, total_tiles,
+                           (float)lr_t, b1, b2, eps, gs);
+    else if (dtype == SEG_F16)
+        hipLaunchKernelGGL(adam_pack_k<f16>, dim3(grid), dim3(256), 0, st, p, g, m, v, dev_segs, nsegs, total_tiles,
                            (float)lr_t, b1, b2, eps, gs);
     else
         return SEG_EINVAL;

@@ -15,8 +15,8 @@ import torch
 from . import _lib
 from ._lib import SegConvDesc, SegEpilogue, check
 
-F32, BF16 = 0, 1
-_TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16}
+F32, BF16, F16 = 0, 1, 2
+_TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
 SAME, VALID = 0, 1
 
 
@@ -29,6 +29,8 @@ def seg_dtype(t: torch.Tensor) -> int:
         return BF16
     if t.dtype == torch.float32:
         return F32
+    if t.dtype == torch.float16:
+        return F16
     raise TypeError(f"unsupported activation dtype {t.dtype}")
 
 
@@ -577,6 +579,12 @@ def cast(x, y, stream=None):
     assert x.numel() == y.numel()
     check(_lib.lib().seg_cast(ptr(x), seg_dtype(x), ptr(y), seg_dtype(y), x.numel(), stream_ptr(stream)), "cast")
     return y
+
+
+def check_finite(g, flag, stream=None):
+    """flag (int32 device scalar) = 1 if g holds an Inf / NaN."""
+    check(_lib.lib().seg_check_finite(ptr(g), g.numel(), ptr(flag), stream_ptr(stream)), "check_finite")
+    return flag
 
 
 def axpy(y, x, alpha, stream=None):

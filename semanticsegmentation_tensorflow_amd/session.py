@@ -142,13 +142,27 @@ class _AdamOverlap:
 
 class Session:
     def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None,
-                 overlap_optimizer=False, fuse_adam=True):
+                 overlap_optimizer=False, fuse_adam=True, loss_scale=None):
+        """compute_dtype: "bf16" (default), "f16" (IEEE half activations and
+        filter copies, fp32 accumulation -- config C5) or "f32" (parity path).
+        loss_scale (f16): "dynamic" (default for f16: TF's DynamicLossScale,
+        2^15 initial, x2 after 2000 finite steps, /2 and skip the update on
+        overflow), a fixed number, or None/1 (no scaling)."""
         self.graph = graph or G.get_default_graph()
         if not torch.cuda.is_available():
             raise RuntimeError("Session needs an MI355X (HIP device); there is no CPU fallback")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.cdt = ops.BF16 if compute_dtype in ("bf16", "bfloat16") else ops.F32
+        self.cdt = {"bf16": ops.BF16, "bfloat16": ops.BF16, "f16": ops.F16, "fp16": ops.F16,
+                    "float16": ops.F16, "f32": ops.F32, "fp32": ops.F32, "float32": ops.F32}[compute_dtype]
         self.tdt = ops.torch_dtype(self.cdt)
+        if loss_scale is None and self.cdt == ops.F16:
+            loss_scale = "dynamic"
+        self.dynamic_scale = loss_scale == "dynamic"
+        self.loss_scale = 2.0 ** 15 if self.dynamic_scale else float(loss_scale or 1.0)
+        self.scale_increment_period = 2000
+        self.good_steps = 0
+        self.skipped_steps = 0
+        self._finite_flag = None
         self.seed = seed
         self.store = None
         self.plans = {}
@@ -910,7 +924,7 @@ class Session:
                 lg = buf[id(n.inputs[0])]
                 labels = buf[id(n.labels)]
                 ops.softmax_xent(lg, labels, n.dlogits, n.loss_sum, n.num_classes, n.valid_hw,
-                                 grad_scale=1.0 / n.count, ws=self.ws)
+                                 grad_scale=(self.loss_scale if p.train else 1.0) / n.count, ws=self.ws)
             elif k == "ConcatV2":
                 if id(n) not in p.alias_nodes:      # aliased: the parts already sit in place
                     ops.concat_fwd([(buf[id(t)], p.shapes[id(t)][3]) for t in n.inputs], y,
@@ -939,12 +953,16 @@ class Session:
             ts = p.train.attrs
             opt = ts["optimizer"]
             world = self.dp.world if self.dp is not None else 1
-            gs = ts["grad_scale"] / world
+            S = self.loss_scale                     # the scale this step's loss gradient carries
+            scaled = S != 1.0
+            gs = ts["grad_scale"] / world / S
+            if scaled and self.overlap_optimizer:
+                raise NotImplementedError("loss scaling needs the whole gradient checked before any update")
             if opt is not None:
                 store.step += 1
             self._fused = None
             if opt is not None and self.fuse_adam and self.dp is None and not self.overlap_optimizer \
-                    and p.adam_fusable:
+                    and not scaled and p.adam_fusable:
                 self._fused = (opt, gs, set())
             self._red = None
             if self.defer_wgrad_reduce and self.dp is None and self.device.type == "cuda":
@@ -971,10 +989,27 @@ class Session:
             if self.dp is not None:
                 self.dp.finish()
                 self.dp.on_launch = None
+            if scaled and not self._grads_finite():
+                # overflow in the scaled fp16 gradients: no update this step
+                # (TF LossScaleOptimizer), halve the scale
+                self.skipped_steps += 1
+                if opt is not None:
+                    store.step -= 1
+                self.loss_scale = max(self.loss_scale / 2.0, 1.0)
+                self.good_steps = 0
+                opt = None
+                p_accum = []
+            else:
+                p_accum = p.train.accum
+                if scaled and self.dynamic_scale:
+                    self.good_steps += 1
+                    if self.good_steps >= self.scale_increment_period:
+                        self.loss_scale *= 2.0
+                        self.good_steps = 0
             if opt is None:
                 # accumulate template: accum += const * grad (Network/main.py:92-95)
-                for acc, var, sc in p.train.accum:
-                    ops.axpy(store.aux[acc].view(-1), store.grad(var).view(-1), sc / world)
+                for acc, var, sc in p_accum:
+                    ops.axpy(store.aux[acc].view(-1), store.grad(var).view(-1), sc / world / S)
                 store.aux_version += 1
             elif self._adam_ctx is not None:
                 self._adam_ctx.finish()
@@ -1025,7 +1060,7 @@ class Session:
         ops.bn_relu_fwd(x, y, one, zero, C, True, eps=0.0)
 
     def _pack_dtype(self):
-        return ops.BF16 if self.tdt == torch.bfloat16 else ops.F32
+        return self.cdt
 
     def _grad_ready(self, names):
         """The gradients of `names` are final once the kernels enqueued so far
@@ -1317,6 +1352,17 @@ class Session:
                 continue
             else:
                 raise NotImplementedError(f"backward of {k}")
+
+    def _grads_finite(self):
+        """All gradients finite (every rank's, under data parallelism)?  One
+        device-to-host read per step on the loss-scaled path."""
+        if self._finite_flag is None:
+            self._finite_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        ops.check_finite(self.store.grads, self._finite_flag)
+        if self.dp is not None:
+            import torch.distributed as dist
+            dist.all_reduce(self._finite_flag, op=dist.ReduceOp.MAX, group=self.dp.group)
+        return int(self._finite_flag.item()) == 0
 
     def _scratch_grad(self, p, var):
         """fp32 gradient sink for a filter outside var_list whose layer still
