@@ -414,7 +414,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
             } else if (seg::g_tn_variant == 2 && seg::tn3_ok(p, d->dtype)) {
                 fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(p.M, p.N, p.P, seg::device_cus(), &sp);
-            } else if (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && p.M >= 128) {
+            } else if (seg::g_tn_variant == 2 && d->dtype != SEG_F32 && p.M >= 128) {
                 fam = "igemm_tn2";
             }
             macs = macs_conv;
@@ -449,7 +449,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 5: {
             const int Mt = tconv_dense_kq(d) ? d->R * d->S * tconv_dense_kq(d) : d->R * d->S * d->K;
             seg::tn_info(Mt, d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
-            fam = (seg::g_tn_variant == 2 && d->dtype == SEG_BF16 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
+            fam = (seg::g_tn_variant == 2 && d->dtype != SEG_F32 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
             if (seg::g_tn_variant == 2 && seg::tn3_applies(Mt, d->C, d->dtype)) {
                 fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(Mt, d->C, d->N * d->H * d->W, seg::device_cus(), &sp);
             }

@@ -47,9 +47,8 @@ struct HaloGeom {
     int nchunks, kc_per_split;
 };
 
-template <int BW, int HI, int BN>
+template <int BW, int HI, int BN, typename T = bf16>
 __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
-    using T = bf16;
     constexpr int NW = 8, WM = 4, WN = 2, BM = 256, BH = BM / BW;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int B_INS = BN / 8 / NW;
@@ -192,8 +191,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8, af[mi]), __builtin_bit_cast(bf16x8, bfr[ni]), acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
         }
         stage = stage == 2 ? 0 : stage + 1;
         ++tap;
@@ -312,9 +310,8 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
 // MFMA, 3 = no LDS fragment reads.
 // PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
 // both B halves read in the first).
-template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256>
+template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16>
 __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
-    using T = bf16;
     constexpr int NW = 8, BM = 256, BN = BNT, BH = BM / BW, HI = 6;
     constexpr int WTN = BN / 4, NFH = WTN / 32;   // per-wave columns, n-fragments per B half
     constexpr int HBUF = HI * NW * 1024;
@@ -448,9 +445,8 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                         if constexpr (ABL == 2) {
                             asm volatile("" ::"v"(af[ks][mi].x), "v"(af[ks][mi].w), "v"(bq[nh][ks][ni].x), "v"(bq[nh][ks][ni].w));
                         } else {
-                            acc[mh * 4 + mi][nh * NFH + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[nh][ks][ni]),
-                                acc[mh * 4 + mi][nh * NFH + ni], 0, 0, 0);
+                            acc[mh * 4 + mi][nh * NFH + ni] = mfma16x16x32<T>(
+                                af[ks][mi], bq[nh][ks][ni], acc[mh * 4 + mi][nh * NFH + ni]);
                         }
                     }
             __builtin_amdgcn_s_setprio(0);
@@ -613,9 +609,8 @@ constexpr int R64_PER = (R64_HROWS * 8 + 511) / 512;                            
 
 // ABL (diagnostics only, garbage results): 1 no halo fetch, 2 no MFMA,
 // 3 no epilogue stores, 4 no LDS fragment reads
-template <int ABL = 0>
+template <int ABL = 0, typename T = bf16>
 __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int tiles_y, int ntiles) {
-    using T = bf16;
     constexpr int NW = 8, WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2;
     constexpr int BS = 9 * 64 * 128;                 // resident filter
     constexpr int HS = R64_HROWS * 128;              // halo
@@ -747,9 +742,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
                     if constexpr (ABL == 2) {
                         asm volatile("" ::"v"(fb[cur][ni].x), "v"(fa[cur][mi].x), "v"(fb[cur][ni].w), "v"(fa[cur][mi].w));
                     } else {
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, fb[cur][ni]), __builtin_bit_cast(bf16x8, fa[cur][mi]),
-                            acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = mfma16x16x32<T>(fb[cur][ni], fa[cur][mi], acc[mi][ni]);
                     }
                 }
         }
@@ -772,18 +765,16 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
                     if (col0 >= p.N) continue;
                     float mk[4] = {1.f, 1.f, 1.f, 1.f}, res[4] = {0.f, 0.f, 0.f, 0.f};
                     if (e.mask) {
-                        const uint2 mv = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.mask) +
-                                                                         img * e.mask_img + pix * e.ld_mask + col0);
-                        mk[0] = __uint_as_float(mv.x << 16); mk[1] = __uint_as_float(mv.x & 0xffff0000u);
-                        mk[2] = __uint_as_float(mv.y << 16); mk[3] = __uint_as_float(mv.y & 0xffff0000u);
+                        const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) mk[j] = to_f32(mp[j]);
                     }
                     if (e.residual) {
-                        const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.residual) +
-                                                                         img * e.res_img + pix * e.ld_res + col0);
-                        res[0] = __uint_as_float(rv.x << 16); res[1] = __uint_as_float(rv.x & 0xffff0000u);
-                        res[2] = __uint_as_float(rv.y << 16); res[3] = __uint_as_float(rv.y & 0xffff0000u);
+                        const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) res[j] = to_f32(rp[j]);
                     }
-                    bf16 o[4];
+                    T o[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int col = col0 + j;
@@ -792,7 +783,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
                         if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                         x += res[j];
                         if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
-                        o[j] = (bf16)(col < e.n_valid ? x : 0.f);
+                        o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
                     }
                     if constexpr (ABL == 3) {
                         asm volatile("" ::"v"(o[0]), "v"(o[3]));
@@ -815,7 +806,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
 static constexpr int kHaloBW[3] = {16, 32, 64};
 
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp) {
-    if (!g_nt_halo || dtype != SEG_BF16) return false;
+    if (!g_nt_halo || (dtype != SEG_BF16 && dtype != SEG_F16)) return false;
     if (p.phase || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1 || p.ooh != 0 || p.oow != 0) return false;
     if (p.Ha != p.OH || p.Wa != p.OW || p.rb != 0 || p.sb != 0) return false;
     if (p.C % 64 != 0 || p.K % p.C != 0 || p.taps_w <= 0) return false;
@@ -889,27 +880,34 @@ bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* 
 }
 
 template <int BW, int HI, int BN>
-static void launch_halo_t(NTParams& p, const HaloGeom& g, long tiles, int gridz, hipStream_t s) {
-    hipLaunchKernelGGL((conv_halo<BW, HI, BN>), dim3((unsigned)tiles, 1, gridz), dim3(512), 0, s, p, g);
+static void launch_halo_t(NTParams& p, const HaloGeom& g, long tiles, int gridz, hipStream_t s, int dtype) {
+    if (dtype == SEG_F16)
+        hipLaunchKernelGGL((conv_halo<BW, HI, BN, f16>), dim3((unsigned)tiles, 1, gridz), dim3(512), 0, s, p, g);
+    else
+        hipLaunchKernelGGL((conv_halo<BW, HI, BN>), dim3((unsigned)tiles, 1, gridz), dim3(512), 0, s, p, g);
 }
 
 template <int BW, int HI>
-static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s) {
-    if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s);
-    else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s);
+static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s, int dtype) {
+    if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s, dtype);
+    else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s, dtype);
 }
 
 bool res64_ok(const NTParams& p, int dtype) {
-    return g_res64 && g_nt_halo && dtype == SEG_BF16 && !p.phase && p.ish == 1 && p.isw == 1 && p.osh == 1 &&
+    return g_res64 && g_nt_halo && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.ish == 1 && p.isw == 1 && p.osh == 1 &&
            p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.Ha == p.OH && p.Wa == p.OW && p.C == 64 && p.K == 9 * 64 &&
            p.taps_w == 3 && (p.tsh == 1 || p.tsh == -1) && (p.tsw == 1 || p.tsw == -1) && p.N <= 64 &&
            p.N % 8 == 0 && p.OH > 0 && p.OW > 0 && p.M % (p.OH * p.OW) == 0;
 }
 
-void launch_res64(NTParams& p, int cus, hipStream_t s) {
+void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     const int grid = std::min(ntiles, cus);
+    if (dtype == SEG_F16) {
+        hipLaunchKernelGGL((conv_res64<0, f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        return;
+    }
     switch (g_nt2_ablate) {
         case 1: hipLaunchKernelGGL(conv_res64<1>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
         case 2: hipLaunchKernelGGL(conv_res64<2>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
@@ -919,11 +917,28 @@ void launch_res64(NTParams& p, int cus, hipStream_t s) {
     hipLaunchKernelGGL(conv_res64<0>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
 }
 
-void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {
+void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype) {
     HaloGeom g;
     g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
     g.hwd = hp.geom[4]; g.hrows = hp.geom[5]; g.hy0 = hp.geom[6]; g.hx0 = hp.geom[7];
     g.nchunks = hp.geom[8]; g.kc_per_split = hp.geom[9];
+    if (dtype == SEG_F16) {   // half: the production schedules only
+        const dim3 grid((unsigned)hp.tiles, 1, gridz);
+        if (hp.bn == 256) {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+            return;
+        }
+        switch (hp.bw * 10 + hp.hi) {
+            case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+            case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+            case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+            case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+            case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+            default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        }
+        return;
+    }
     if (hp.bn == 128 && hp.hi == 6 && g_halo_wide && g_halo2_n128) {
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
         if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 128>), grid, dim3(512), 0, s, p, g);
@@ -954,12 +969,12 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s) {
     }
     const int key = hp.bw * 10 + hp.hi;
     switch (key) {
-        case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
-        case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
-        case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
-        case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
-        case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s); break;
-        default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s); break;
+        case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
     }
 }
 

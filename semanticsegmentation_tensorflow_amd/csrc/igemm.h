@@ -103,7 +103,7 @@ bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
 extern int g_tn_variant;
 extern int g_nt2_ablate;
-void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s);
+void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype = SEG_BF16);
 
 // 256 x 256 NT tiles (igemm3.hip) for bf16 with N > 128
 extern int g_nt3;
@@ -141,11 +141,11 @@ extern int g_halo_stagger;
 extern int g_halo_phases;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
-void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s);
+void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype = SEG_BF16);
 extern int g_res64;
 extern int g_halo2_n128;
 bool res64_ok(const NTParams& p, int dtype);
-void launch_res64(NTParams& p, int cus, hipStream_t s);
+void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 
 // 8-input-channel first layer (smallc.hip)
 extern int g_smallc;

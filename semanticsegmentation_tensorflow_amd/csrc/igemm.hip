@@ -690,19 +690,19 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
     if (nphases > 1) splits = 1;
     p.partial = nullptr;
-    if (is_bf16_v<T> && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
-        launch_res64(p, num_cus(), s);
+    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dt_traits<T>::id)) {
+        launch_res64(p, num_cus(), s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
         return SEG_OK;
     }
     HaloPlan hp;
-    if (is_bf16_v<T> && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, splits, num_cus(), &hp)) {
+    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, dt_traits<T>::id, splits, num_cus(), &hp)) {
         if (hp.splits > 1) {
             const size_t need = (size_t)hp.splits * p.M * p.N * sizeof(float);
             if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
         }
-        launch_halo(p, hp, hp.splits, s);
+        launch_halo(p, hp, hp.splits, s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
         if (p.partial) {
             const long total = (long)p.M * (p.N / 8);
@@ -752,12 +752,12 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
     const int bk = dtype == SEG_F32 ? 32 : 64;
     choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
     if (nphases > 1) *splits = 1;
-    if (dtype == SEG_BF16 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, SEG_BF16)) {
+    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dtype)) {
         *bn = 64; *splits = 1;
         return "conv_res64";
     }
     HaloPlan hp;
-    if (dtype == SEG_BF16 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, SEG_BF16, *splits, num_cus(), &hp)) {
+    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, dtype, *splits, num_cus(), &hp)) {
         *bm = 256; *bn = hp.bn; *splits = hp.splits;
         return "conv_halo";
     }
@@ -808,12 +808,12 @@ static void choose_tn(int M, int N, int P, int bkp, bool v2, int& bm, int& bn, i
 }
 
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits) {
-    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype == SEG_BF16, *bm, *bn, *splits);
+    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype != SEG_F32, *bm, *bn, *splits);
 }
 
 size_t tn_workspace(int M, int N, int P, int dtype) {
     int bm, bn, splits;
-    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype == SEG_BF16, bm, bn, splits);
+    choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype != SEG_F32, bm, bn, splits);
     if (g_tn_variant == 2 && tn3_applies(M, N, dtype)) {
         int s3;
         tn3_info(M, N, P, num_cus(), &s3);
@@ -881,7 +881,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         return SEG_OK;
     }
     int bm, bn, splits;
-    choose_tn(p.M, p.N, p.P, BKP, is_bf16_v<T>, bm, bn, splits);
+    choose_tn(p.M, p.N, p.P, BKP, sizeof(T) == 2, bm, bn, splits);
     const bool tn3 = is_bf16_v<T> && g_tn_variant == 2 && tn3_ok(p, SEG_BF16);
     if (tn3) tn3_info(p.M, p.N, p.P, num_cus(), &splits);
     int gridz = 1;
@@ -896,8 +896,8 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     if (tn3) {
         launch_tn3(p, gridz, s);
-    } else if (g_tn_variant == 2 && is_bf16_v<T> && (bm == 256 || bn == 256 || p.M >= 128)) {
-        launch_tn2(p, bm, bn, gridz, s);
+    } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
+        launch_tn2(p, bm, bn, gridz, s, dt_traits<T>::id);
     } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
     else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);
     else if (bn == 64) launch_tn_t<T, 128, 64>(p, gridz, s);

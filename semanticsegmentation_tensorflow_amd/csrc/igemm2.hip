@@ -334,9 +334,8 @@ __device__ __forceinline__ int tn2_swz(int row) {
     else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m, int tiles_n, int splits) {
-    using T = bf16;
     constexpr int NW = WM * WN;
     constexpr int BKP = 64;
     constexpr int AROWB = BM * 2, BROWB = BN * 2;
@@ -447,7 +446,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
         const char* Bs = As + ASZ;
 #pragma unroll
         for (int ks = 0; ks < BKP / 32; ++ks) {
-            bf16x8 af[TM], bfr[TN];
+            uint4 af[TM], bfr[TN];
             const int r1 = ks * 32 + 8 * fg + tq;
             const int s1 = tn2_swz<AROWB>(r1), s2 = tn2_swz<AROWB>(r1 + 4);
 #pragma unroll
@@ -457,7 +456,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(As + r1 * AROWB + 16 * c1 + 8 * (tpp & 1)));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(As + (r1 + 4) * AROWB + 16 * c2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                af[mi] = __builtin_bit_cast(bf16x8, v);
+                af[mi] = __builtin_bit_cast(uint4, v);
             }
             const int t1 = tn2_swz<BROWB>(r1), t2 = tn2_swz<BROWB>(r1 + 4);
 #pragma unroll
@@ -467,13 +466,13 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Bs + r1 * BROWB + 16 * c1 + 8 * (tpp & 1)));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Bs + (r1 + 4) * BROWB + 16 * c2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bfr[ni] = __builtin_bit_cast(bf16x8, v);
+                bfr[ni] = __builtin_bit_cast(uint4, v);
             }
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
         }
         stage = stage == 2 ? 0 : stage + 1;
     }
@@ -505,19 +504,25 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
         }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN>
 void launch_tn2_t(TNParams& p, int splits, hipStream_t s) {
     const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
-    hipLaunchKernelGGL((igemm_tn2<BM, BN, WM, WN>), dim3(tm * tn * splits), dim3(WM * WN * 64), 0, s, p, tm, tn,
+    hipLaunchKernelGGL((igemm_tn2<T, BM, BN, WM, WN>), dim3(tm * tn * splits), dim3(WM * WN * 64), 0, s, p, tm, tn,
                        splits);
 }
 
-void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s) {
-    if (bm == 256 && bn == 128) launch_tn2_t<256, 128, 4, 2>(p, splits, s);
-    else if (bm == 128 && bn == 256) launch_tn2_t<128, 256, 2, 4>(p, splits, s);
-    else if (bm == 256 && bn == 64) launch_tn2_t<256, 64, 4, 2>(p, splits, s);
-    else if (bm == 128 && bn == 64) launch_tn2_t<128, 64, 4, 2>(p, splits, s);
-    else launch_tn2_t<128, 128, 2, 4>(p, splits, s);
+template <typename T>
+static void launch_tn2_typed(TNParams& p, int bm, int bn, int splits, hipStream_t s) {
+    if (bm == 256 && bn == 128) launch_tn2_t<T, 256, 128, 4, 2>(p, splits, s);
+    else if (bm == 128 && bn == 256) launch_tn2_t<T, 128, 256, 2, 4>(p, splits, s);
+    else if (bm == 256 && bn == 64) launch_tn2_t<T, 256, 64, 4, 2>(p, splits, s);
+    else if (bm == 128 && bn == 64) launch_tn2_t<T, 128, 64, 4, 2>(p, splits, s);
+    else launch_tn2_t<T, 128, 128, 2, 4>(p, splits, s);
+}
+
+void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype) {
+    if (dtype == SEG_F16) launch_tn2_typed<f16>(p, bm, bn, splits, s);
+    else launch_tn2_typed<bf16>(p, bm, bn, splits, s);
 }
 
 int g_nt2_ablate = 0;

@@ -3,7 +3,7 @@ import torch
 
 from semanticsegmentation_tensorflow_amd import ops
 
-TOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2}
+TOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2, torch.float16: 2e-3}
 
 
 def to_dev(x, dtype, dev, cpad=None):

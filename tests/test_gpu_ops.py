@@ -1,8 +1,8 @@
 """Op-level parity: every HIP kernel vs the CPU oracle (oracle/tf1_ops.py).
 
 fp32 path: exact-f32 MFMA, compared at ~1e-5 relative (of max |ref|).
-bf16 path: the oracle sees the same bf16-rounded inputs; tolerance covers
-fp32-accumulation order + one bf16 output rounding (~2^-8 relative).
+bf16 / fp16 paths: the oracle sees the same rounded inputs; tolerance covers
+fp32-accumulation order + one output rounding (~2^-8 bf16, ~2^-11 fp16).
 """
 import math
 
@@ -56,8 +56,8 @@ def ntv(request, dev):
     ops.set_option("halo2_n128", 0)
 
 
-DTYPES = [torch.float32, torch.bfloat16]
-DT = {torch.float32: ops.F32, torch.bfloat16: ops.BF16}
+DTYPES = [torch.float32, torch.bfloat16, torch.float16]
+DT = {torch.float32: ops.F32, torch.bfloat16: ops.BF16, torch.float16: ops.F16}
 
 # (N, H, W, C, K, R, S(=R), stride, dilation, padding)
 CONV_CASES = [
