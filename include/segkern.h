@@ -399,6 +399,10 @@ int seg_axpy(float* y, const float* x, float alpha, long n, void* stream);
  * skipped and the scale halved, as TF's DynamicLossScale). g 16-byte aligned. */
 int seg_check_finite(const float* g, long n, int* flag, void* stream);
 int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* stream);
+/* CRC-32C (Castagnoli) of n bytes continuing from crc (0 to start): host
+ * code for tf.train.Saver's tensor-bundle checkpoints (per-tensor checksums
+ * in the .index file, SSTable block trailers). */
+uint32_t seg_crc32c(const void* data, size_t n, uint32_t crc);
 const char* seg_status_string(int status);
 int seg_version(void);
 

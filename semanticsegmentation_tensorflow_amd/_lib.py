@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
 SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "igemm4.hip"]
-HOST_SOURCES = ["pngdec.cpp"]          # host-only C++ (g++), linked into the same library
+HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]   # host-only C++ (g++), linked into the same library
 HOST_LIBS = ["-lz"]
 # per-source extra flags: the 4-wave 128x128 GEMM keeps its accumulators in
 # VGPRs and the MFMA operands in AGPRs (the default form copies acc through
@@ -172,6 +172,7 @@ SIGNATURES = {
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
     "seg_axpy": (_I, [_P, _P, _F, _L, _P]),
     "seg_check_finite": (_I, [_P, _L, _P, _P]),
+    "seg_crc32c": (ctypes.c_uint32, [_P, _Z, ctypes.c_uint32]),
     "seg_status_string": (ctypes.c_char_p, [_I]),
     "seg_version": (_I, []),
 }

@@ -1,23 +1,33 @@
 """tf.train.Saver / get_checkpoint_state / latest_checkpoint for the
 reference's save-and-resume flow (Network/model/FCN.py:370-378,
-Network/main.py:143-153 and :190).
+Network/main.py:143-153 and :190, Network/model/FCDenseNet.py:247-263, :285).
 
-Checkpoints carry TF1 Saver names: every variable under its graph name
-(`conv1_1/weights`, `batch_normalization_3/gamma`, ...), the Adam slots as
-`<name>/Adam` and `<name>/Adam_1`, and the optimizer's `beta1_power` /
-`beta2_power` (beta^t, as TF keeps them).  Filters keep TF's layouts (HWIO;
-conv2d_transpose [kh, kw, out, in]); the packed compute copies are rebuilt on
-the next step.  Storage is a NumPy .npz (no pickle) per checkpoint plus TF's
-`checkpoint` index file, so `get_checkpoint_state(dir).model_checkpoint_path`
-works as in the reference.  Reading TF's own tensor-bundle files needs
-TensorFlow, which is not part of this path.
+`Saver.save` writes TensorFlow's own V2 checkpoint format (tensor bundle:
+`<prefix>.index` + `<prefix>.data-00000-of-00001`, tf_bundle.py) under TF1
+Saver names:
+
+* every graph variable under its name (`conv1_1/weights` HWIO,
+  `conv_t1/weights` [kh, kw, out, in], `batch_normalization_3/gamma`,
+  the BN `moving_mean` / `moving_variance`, non-trainable `tf.Variable`s such
+  as the accumulate template's accumulators and `global_step`, int64);
+* the Adam slots as `<name>/Adam` and `<name>/Adam_1`;
+* the optimizer's `beta1_power` / `beta2_power` (beta^t, float32, as TF keeps
+  them) -- the Adam step t is restored from these, as TF does.
+
+plus TF's `checkpoint` state file, so `get_checkpoint_state(dir)
+.model_checkpoint_path` works as in the reference.  `restore` reads bundles
+(ours or TensorFlow's: sliced / multi-shard / compressed ones are refused)
+and the `.npz` checkpoints of earlier versions of this package.
 """
 from __future__ import annotations
 
+import math
 import os
 import re
 
 import numpy as np
+
+from . import tf_bundle
 
 BETA1, BETA2 = 0.9, 0.999
 
@@ -26,42 +36,61 @@ def _npz(path):
     return path if path.endswith(".npz") else path + ".npz"
 
 
+def _adam_step(d):
+    """Adam t from TF's beta powers (float32 beta^t; 0.9^t underflows past t ~ 980)."""
+    b1 = float(d.get("beta1_power", 0.0))
+    b2 = float(d.get("beta2_power", 0.0))
+    if 0.0 < b1 < 1.0:
+        return int(round(math.log(b1) / math.log(BETA1)))
+    if 0.0 < b2 < 1.0:
+        return int(round(math.log(b2) / math.log(BETA2)))
+    return 0 if b1 >= 1.0 else 10 ** 6
+
+
 class Saver:
     def __init__(self, var_list=None, max_to_keep=5):
         self.var_list = var_list
         self.max_to_keep = max_to_keep
         self._kept = []
 
-    def _names(self, sess):
+    def _vars(self, sess):
         store = sess._ensure_store()
         if self.var_list is None:
-            return [v.var_name for v in store.vars]
-        return [v.var_name for v in self.var_list]
+            return list(store.all_vars)
+        return list(self.var_list)
+
+    def _global_step_value(self, sess, global_step):
+        if global_step is None:
+            return None
+        if hasattr(global_step, "var_name"):          # tf.Variable(0, trainable=False, name='global_step')
+            return int(round(float(sess.variable_value(global_step.var_name).reshape(-1)[0])))
+        return int(global_step)
 
     def save(self, sess, save_path, global_step=None):
         store = sess._ensure_store()
-        path = save_path if global_step is None else f"{save_path}-{int(global_step)}"
-        sd = store.state_dict()
-        names = set(self._names(sess))
+        gs = self._global_step_value(sess, global_step)
+        path = save_path if gs is None else f"{save_path}-{gs}"
         out = {}
-        for k, v in sd.items():
-            base = re.sub(r"/Adam(_1)?$", "", k)
-            if k == "beta_step":
-                continue
-            if base in names:
-                out[k] = np.ascontiguousarray(v)
-        t = int(sd["beta_step"])
+        for v in self._vars(sess):
+            name = v.var_name
+            val = store.read(name)
+            if getattr(v, "dtype", None) == "int64":
+                val = np.rint(val).astype(np.int64)
+            out[name] = val
+            if name in store.by_name:                 # trainable: Adam slots
+                out[name + "/Adam"] = store.adam_m(name).cpu().numpy()
+                out[name + "/Adam_1"] = store.adam_v(name).cpu().numpy()
+        t = store.step
         out["beta1_power"] = np.float32(BETA1 ** t)
         out["beta2_power"] = np.float32(BETA2 ** t)
-        out["global_step"] = np.int64(t)
+        tf_bundle.write_bundle(path, out)
         d = os.path.dirname(os.path.abspath(path))
-        os.makedirs(d, exist_ok=True)
-        np.savez(_npz(path), **out)
         self._kept.append(path)
         while self.max_to_keep and len(self._kept) > self.max_to_keep:
             old = self._kept.pop(0)
-            if os.path.exists(_npz(old)):
-                os.remove(_npz(old))
+            for f in (f"{old}.index", tf_bundle.data_path(old), _npz(old)):
+                if os.path.exists(f):
+                    os.remove(f)
         with open(os.path.join(d, "checkpoint"), "w") as f:
             f.write(f'model_checkpoint_path: "{os.path.basename(path)}"\n')
             for p in self._kept:
@@ -70,15 +99,27 @@ class Saver:
 
     def restore(self, sess, save_path):
         store = sess._ensure_store()
-        with np.load(_npz(save_path), allow_pickle=False) as z:
-            d = {k: z[k] for k in z.files}
-        missing = [n for n in self._names(sess) if n not in d]
+        names = [v.var_name for v in self._vars(sess)]
+        if tf_bundle.is_bundle(save_path):
+            index = tf_bundle.read_index(save_path)
+            want = [n for n in names if n in index]
+            want += [n + s for n in names if n in store.by_name for s in ("/Adam", "/Adam_1") if n + s in index]
+            want += [k for k in ("beta1_power", "beta2_power") if k in index]
+            d = tf_bundle.read_bundle(save_path, want)
+        elif os.path.exists(_npz(save_path)):
+            with np.load(_npz(save_path), allow_pickle=False) as z:
+                d = {k: z[k] for k in z.files}
+        else:
+            raise FileNotFoundError(f"no checkpoint at {save_path}")
+        missing = [n for n in names if n not in d]
         if missing:
             raise ValueError(f"checkpoint {save_path} lacks variables {missing[:5]}")
-        if "global_step" in d:
-            d["beta_step"] = int(d["global_step"])
-        elif "beta1_power" in d:
-            d["beta_step"] = int(round(np.log(float(d["beta1_power"])) / np.log(BETA1)))
+        for n in names:
+            want = tuple(store.by_name[n].shape) if n in store.by_name else tuple(store.aux[n].shape)
+            if tuple(np.shape(d[n])) != want:
+                raise ValueError(f"{n}: checkpoint shape {np.shape(d[n])} != variable shape {want}")
+        d = {k: (np.asarray(v, np.float32) if k != "beta_step" else v) for k, v in d.items()}
+        d["beta_step"] = _adam_step(d) if ("beta1_power" in d or "beta2_power" in d) else store.step
         store.load_state_dict(d)
 
 

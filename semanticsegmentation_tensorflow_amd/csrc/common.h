@@ -42,6 +42,21 @@ template <> __device__ __forceinline__ float from_f32<float>(float v) { return v
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
 template <> __device__ __forceinline__ f16 from_f32<f16>(float v) { return (f16)v; }
 
+// 8-lane 16-bit vector of T (MFMA operand) and one element's bits -> fp32
+template <typename T> struct vec8 { typedef bf16x8 type; };
+template <> struct vec8<f16> { typedef f16x8 type; };
+template <typename T> using vec8_t = typename vec8<T>::type;
+template <typename T>
+__device__ __forceinline__ float bits16_to_f32(unsigned short u) {
+    if constexpr (is_f16_v<T>) return (float)__builtin_bit_cast(f16, u);
+    else return __uint_as_float((unsigned)u << 16);
+}
+template <typename T>
+__device__ __forceinline__ f32x4 mfma_v8(const vec8_t<T>& a, const vec8_t<T>& b, const f32x4& c) {
+    if constexpr (is_f16_v<T>) return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // 16x16x32 MFMA on eight packed 16-bit elements per lane (A, B as loaded from
 // LDS), fp32 accumulation: bf16 or IEEE half operands
 template <typename T>

@@ -168,6 +168,6 @@ extern int g_wgrad_abl;
 extern int g_wgrad_nbias;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
-void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s);
+void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);
 
 }  // namespace seg

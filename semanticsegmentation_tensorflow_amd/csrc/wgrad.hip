@@ -53,9 +53,9 @@ __device__ __forceinline__ int wg_swz(int row) {
 // LA: A-fragment read-ahead distance in (substep, tap) steps (1 or 2).
 // ABL (diagnostic builds, garbage results): 1 no DMA in the loop, 2 no MFMA,
 // 3 no LDS fragment reads.
-template <int BW, int NT, int NST, int HI, int LA = 1, int ABL = 0>
+template <int BW, int NT, int NST, int HI, int LA = 1, int ABL = 0, typename T = bf16>
 __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
-    using T = bf16;
+    using V8 = vec8_t<T>;
     constexpr int NW = 8, BH = 128 / BW;
     constexpr int NF = NT / 32;               // n fragments per wave
     constexpr int DROWB = NT * 2;             // dy tile row bytes
@@ -229,12 +229,12 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
         // flat software pipeline over the 36 (substep, tap) steps of the tile:
         // the A fragment of step s+1 (and the B fragments of the next substep)
         // are read while the MFMAs of step s issue
-        auto read_b = [&](int ss, bf16x8* bo) {
+        auto read_b = [&](int ss, V8* bo) {
             if constexpr (ABL == 3) {
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     s16x8 v = {(short)ss, (short)ni, 1, 2, 3, 4, 5, (short)lane};
-                    bo[ni] = __builtin_bit_cast(bf16x8, v);
+                    bo[ni] = __builtin_bit_cast(V8, v);
                 }
                 return;
             }
@@ -254,11 +254,11 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                     hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
                 }
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bo[ni] = __builtin_bit_cast(bf16x8, v);
+                bo[ni] = __builtin_bit_cast(V8, v);
                 if (do_bias && ni == cf && ss % g.nbias == ct) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
-                        dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                        dsum[ni] += bits16_to_f32<T>((unsigned short)v[e]);
                 }
             }
         };
@@ -268,11 +268,11 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] & 0xffffu)));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] >> 16)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                return __builtin_bit_cast(bf16x8, v);
+                return __builtin_bit_cast(V8, v);
             }
             if constexpr (ABL == 3) {
                 s16x8 v = {(short)ss, (short)tap, 1, 2, 3, 4, 5, (short)lane};
-                return __builtin_bit_cast(bf16x8, v);
+                return __builtin_bit_cast(V8, v);
             }
             const int kk = ss * 32 + 8 * fg + tq;
             const int py = kk / BW, px = kk - (kk / BW) * BW;
@@ -282,9 +282,9 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + r1 * 128 + 16 * a1 + 8 * (tpp & 1)));
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (r1 + 4) * 128 + 16 * a2 + 8 * (tpp & 1)));
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            return __builtin_bit_cast(bf16x8, v);
+            return __builtin_bit_cast(V8, v);
         };
-        bf16x8 b0[NF], b1[NF];
+        V8 b0[NF], b1[NF];
         if constexpr (LA == 2) {
             // flat 36-step pipeline (requires BW = 16 and hwd % 8 == 0, so a
             // substep = +2 halo rows x hwd keeps every XOR swizzle): all LDS
@@ -301,23 +301,23 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const unsigned so = (unsigned)ss * (32 / BW) * g.hwd * 128;
                 const s16x4 lo = rd(a_lo[tap] + so), hi = rd(a_hi[tap] + so);
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                return __builtin_bit_cast(bf16x8, v);
+                return __builtin_bit_cast(V8, v);
             };
-            auto fb = [&](int ss, bf16x8* bo) {
+            auto fb = [&](int ss, V8* bo) {
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     const s16x4 lo = rdd(b_lo[ni] + ss * 32 * DROWB), hi = rdd(b_hi[ni] + ss * 32 * DROWB);
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    bo[ni] = __builtin_bit_cast(bf16x8, v);
+                    bo[ni] = __builtin_bit_cast(V8, v);
                     if (do_bias && ni == cf && ss % g.nbias == ct) {
 #pragma unroll
                         for (int e = 0; e < 8; ++e)
-                            dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                            dsum[ni] += bits16_to_f32<T>((unsigned short)v[e]);
                     }
                 }
             };
             fb(0, b0);
-            bf16x8 ar[3];
+            V8 ar[3];
             ar[0] = fa(0);
             ar[1] = fa(1);
 #pragma unroll
@@ -325,28 +325,28 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 const int ss = k / 9, tap = k - (k / 9) * 9;
                 if (k + 2 < 36) ar[(k + 2) % 3] = fa(k + 2);
                 if (tap == 4 && ss + 1 < 4) fb(ss + 1, (ss & 1) ? b0 : b1);
-                bf16x8* bc = (ss & 1) ? b1 : b0;
+                V8* bc = (ss & 1) ? b1 : b0;
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni)
-                    acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[k % 3], bc[ni], acc[tap][ni], 0, 0, 0);
+                    acc[tap][ni] = mfma_v8<T>(ar[k % 3], bc[ni], acc[tap][ni]);
             }
             buf = buf == NST - 1 ? 0 : buf + 1;
             continue;
         }
         read_b(0, b0);
-        bf16x8 a_cur = read_a(0, 0);
+        V8 a_cur = read_a(0, 0);
         // one substep: 9 taps, A(tap+1) read ahead, next substep's B at tap 4
-        auto substep = [&](int ss, bf16x8* bc, bf16x8* bn) {
+        auto substep = [&](int ss, V8* bc, V8* bn) {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                bf16x8 a_nxt = a_cur;
+                V8 a_nxt = a_cur;
                 if (tap < 8) a_nxt = read_a(ss, tap + 1);
                 else if (ss + 1 < 4) a_nxt = read_a(ss + 1, 0);
                 if (tap == 4 && ss + 1 < 4) read_b(ss + 1, bn);
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     if constexpr (ABL == 2) asm volatile("" ::"v"(a_cur), "v"(bc[ni]));
-                    else acc[tap][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, bc[ni], acc[tap][ni], 0, 0, 0);
+                    else acc[tap][ni] = mfma_v8<T>(a_cur, bc[ni], acc[tap][ni]);
                 }
                 a_cur = a_nxt;
             }
@@ -407,7 +407,8 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
 // host side
 // ---------------------------------------------------------------------------
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
-    if (!g_wgrad_halo || dtype != SEG_BF16) return false;
+    if (!g_wgrad_halo || (dtype != SEG_BF16 && dtype != SEG_F16)) return false;
+    if (dtype == SEG_F16 && g_wgrad_la != 3) return false;   // half: the production schedule only
     if (p.ish != 1 || p.isw != 1 || p.taps_w != 3 || p.Cg % 64 != 0 || p.M != 9 * p.Cg) return false;
     if (p.tsh <= 0 || p.tsw <= 0 || p.N % 8 != 0 || p.ldb % 8 != 0 || p.ldx % 8 != 0) return false;
     if (p.Ha <= 0 || p.Wa <= 0 || p.P % (p.Ha * p.Wa) != 0) return false;
@@ -450,7 +451,7 @@ size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p) {
     return wp.splits > 1 ? (size_t)wp.splits * (p.M + wp.nbias) * p.N * sizeof(float) : 0;
 }
 
-void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s) {
+void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
     WGGeom g;
     g.tiles_x = wp.g[0]; g.tiles_y = wp.g[1]; g.nimg = wp.g[2]; g.hwd = wp.g[3]; g.hrows = wp.g[4];
     g.nct = wp.g[5]; g.nnt = wp.g[6]; g.splits = wp.g[7]; g.tps = wp.g[8]; g.ptiles = wp.g[9];
@@ -471,6 +472,12 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s) {
     }
     if (g_wgrad_la == 2 && wp.nt == 128 && wp.bw == 16) {
         hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 2>), grid, block, 0, s, p, g);
+        return;
+    }
+    if (dtype == SEG_F16) {                   // wgrad_plan: la == 3, bw == 16
+        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 3, 0, f16>), grid, block, 0, s, p, g);
+        else if (small) hipLaunchKernelGGL((wgrad_halo<16, 64, 3, 4, 3, 0, f16>), grid, block, 0, s, p, g);
+        else hipLaunchKernelGGL((wgrad_halo<16, 64, 2, 5, 3, 0, f16>), grid, block, 0, s, p, g);
         return;
     }
     if (g_wgrad_la == 3 && wp.bw == 16) {
