@@ -125,18 +125,29 @@ template <> struct Chunk<f16> {
     }
 };
 
-// Counter-based uniform in [0,1) for TF1 dropout, top 24 bits of a 32-bit
-// lowbias32 finalizer (xorshift-multiply, two 32-bit multiplies) of the
-// counter's low word plus a per-seed key; counters >= 2^32 fold their high
-// word in first.  32-bit integer multiplies are quarter rate on CDNA: this is
-// ~2.5x cheaper than a 64-bit splitmix, which made the dropout draws a large
-// part of the fused conv epilogues.  Restated in numpy by the tests.
-__host__ __device__ __forceinline__ float seg_uniform(uint64_t seed, uint64_t idx) {
-    const uint32_t key = (uint32_t)(seed ^ (seed >> 32)) * 0x9E3779B9u + 0x632BE59Bu;
-    uint32_t x = (uint32_t)idx + key;
-    x ^= (uint32_t)(idx >> 32) * 0x85EBCA6Bu;
+// Counter-based uniform in [0,1) for TF1 dropout: the top 24 bits of a
+// lowbias32-style finalizer (xorshift-multiply, 32-bit multiplies: quarter
+// rate on CDNA, ~2.5x cheaper than a 64-bit splitmix in the fused conv
+// epilogues) of the counter (high word folded in first), with the seed key --
+// itself fully avalanched, a loop invariant -- XORed in after the first
+// multiply.  Mixing the key non-additively keeps the streams of different
+// seeds (layers, steps, data-parallel ranks) from being shifted copies of one
+// another, which F(idx + key) would make them.  Restated in numpy by the tests.
+__host__ __device__ __forceinline__ uint32_t seg_avalanche32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__host__ __device__ __forceinline__ float seg_uniform(uint64_t seed, uint64_t idx) {
+    const uint32_t key = seg_avalanche32((uint32_t)(seed ^ (seed >> 32)) ^ 0x632BE59Bu);
+    uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x85EBCA6Bu);
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= key;
     x ^= x >> 15;
     x *= 0x846CA68Bu;
     x ^= x >> 16;

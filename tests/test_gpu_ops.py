@@ -405,18 +405,41 @@ def test_adam_tf1(dev):
     assert_close(pd.double().cpu(), params["p"], torch.float32, "adam", 1e-6)
 
 
-def _np_uniform(seed, idx):
-    """seg_uniform (csrc/common.h): lowbias32 of the counter plus a seed key."""
+def _np_avalanche32(x):
     M = 0xFFFFFFFF
-    key = (((seed ^ (seed >> 32)) & M) * 0x9E3779B9 + 0x632BE59B) & M
-    x = ((idx & M) + key) & M
-    x ^= ((idx >> 32) * 0x85EBCA6B) & M
     x ^= x >> 16
     x = (x * 0x7FEB352D) & M
     x ^= x >> 15
     x = (x * 0x846CA68B) & M
     x ^= x >> 16
+    return x
+
+
+def _np_uniform(seed, idx):
+    """seg_uniform (csrc/common.h): counter finalizer with the avalanched seed
+    key XORed in after the first multiply."""
+    M = 0xFFFFFFFF
+    key = _np_avalanche32(((seed ^ (seed >> 32)) & M) ^ 0x632BE59B)
+    x = ((idx & M) ^ (((idx >> 32) * 0x85EBCA6B) & M)) & M
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M
+    x ^= key
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M
+    x ^= x >> 16
     return (x >> 8) / 16777216.0
+
+
+def test_uniform_streams_of_different_seeds_are_not_shifts():
+    """with F(idx + key) two seeds' masks were shifted copies of one
+    stream; with the key mixed non-additively no small shift aligns them."""
+    a = np.array([_np_uniform(1000, i) for i in range(4096)])
+    for seed in (1001, 1131, 1000 + 7919):
+        b = np.array([_np_uniform(seed, i) for i in range(4096)])
+        for shift in range(0, 2048, 7):
+            assert np.mean(a[shift:] == b[:4096 - shift]) < 0.01
+            assert np.mean(b[shift:] == a[:4096 - shift]) < 0.01
+    assert abs(a.mean() - 0.5) < 0.02
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
