@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 side lines")
     ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--kernel-table", action="store_true", help="print per-launch timings to stderr")
+    ap.add_argument("--no-fold-bn", action="store_true",
+                    help="A/B: keep FC-DenseNet's BatchNorm+ReLU as separate passes (no conv prologue)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes (FETCH_SIZE / WRITE_SIZE) behind roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -231,17 +233,18 @@ def kernel_symbol(name):
     fam, rest = name.split("<", 1)
     a = rest.rstrip(">").split(",")
     bm, bn = a[1], a[2]
+    # dtype-templated kernels appear mangled (`_ZN3seg10conv_halo2ILi16E...`)
     if fam == "conv_halo":
-        return r"conv_halo2<" if bn == "256" else r"conv_halo<"
+        return r"conv_halo2[<I]" if bn == "256" else r"conv_halo[<I]"
     if fam in ("igemm_nt3", "igemm_tn3"):
         return fam + "<"
     if fam == "igemm_nt2":
         return rf"igemm_nt2I\w*Li{bm}ELi{bn}E"
     if fam == "igemm_tn2":
-        return rf"igemm_tn2<{bm}, {bn},"
+        return rf"igemm_tn2(<{bm}, {bn},|I\w*Li{bm}ELi{bn}E)"
     if fam == "wgrad_halo":
-        return rf"wgrad_halo<\d+, {bn},"
-    return {"conv_res64": r"conv_res64<", "conv_c8": r"conv_c8_fwd", "wgrad_c8": r"wgrad_c8",
+        return rf"wgrad_halo(<\d+, {bn},|ILi\d+ELi{bn}E)"
+    return {"conv_res64": r"conv_res64[<I]", "conv_c8": r"conv_c8_fwd", "wgrad_c8": r"wgrad_c8",
             "igemm_nt": r"igemm_ntI", "igemm_tn": r"igemm_tnI"}.get(fam, re.escape(fam))
 
 
@@ -314,7 +317,7 @@ WORKLOAD = {"fcn": "FCN (reference Network/model/FCN.py topology)",
 
 
 def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, fuse_adam=True,
-            overlap_optimizer=False, want_miou=False):
+            overlap_optimizer=False, want_miou=False, fold_bn=True):
     """Build `model`'s training graph, run `warmup` + `steps` timed train steps
     on a synthetic batch resident in HBM, then one more step with HIP events
     around every conv launch (on its launch stream) for the per-kernel
@@ -344,6 +347,7 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
     train_step = tf.train.AdamOptimizer(1e-4).minimize(loss)
     sess = tf.Session(compute_dtype=dtype, seed=0, data_parallel=dp, overlap_optimizer=overlap_optimizer,
                       fuse_adam=fuse_adam)
+    sess.fold_bn = fold_bn
     sess.run(tf.global_variables_initializer())
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
     feed = {image: img, labels: lab, keep: kp}
@@ -467,7 +471,7 @@ def main():
     kp = args.keep_prob if args.keep_prob is not None else dkp
     m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, rank,
                 fuse_adam=not args.no_fuse_adam, overlap_optimizer=args.overlap_optimizer,
-                want_miou=rank == 0 and not args.no_miou and not args.pmc_child)
+                want_miou=rank == 0 and not args.no_miou and not args.pmc_child, fold_bn=not args.no_fold_bn)
     if args.pmc_child:
         return
     HP, WP = m["HP"], m["WP"]

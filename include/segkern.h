@@ -102,6 +102,26 @@ int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_krsc,
                    const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropInput.  w_hwio: packed filter [R][S][C][K] in `dtype`
  * (seg_pack_filter mode 1).  dx may be a channel-slice view (ldx). */
+/* A-operand prologue: the conv reads relu(x * gamma / sqrt(1 + eps) + beta)
+ * in place of x (frozen-statistics tf.layers.batch_normalization + ReLU
+ * feeding the conv, Network/model/FCDenseNet.py:25-28 and :39-41,
+ * Network/utils/utils.py:300-303) without the BN output ever being written:
+ * zero-padded taps stay zero, as TF pads the BN output.  gamma / beta: fp32
+ * [c_valid]; relu 0/1. */
+typedef struct seg_prologue {
+    const float* gamma;
+    const float* beta;
+    float eps;
+    int relu;
+} seg_prologue;
+/* Conv2D of relu(BN(x)) (tf.nn.conv2d on the Batch_Normalization + ReLU
+ * output, utils.py:182 / :300-303) with the epilogue of seg_conv2d_fwd. */
+int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro, const void* w,
+                       const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
+/* Conv2DBackpropFilter with input relu(BN(x)) recomputed from x. */
+int seg_conv2d_bwd_filter_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro,
+                              const void* dy, float* dw, float* dbias, void* ws, size_t ws_bytes,
+                              void* stream);
 int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,
                         const seg_epilogue* epi, void* dx, void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropFilter: dw_f32 is the fp32 master-gradient layout

@@ -96,6 +96,11 @@ class SegAugView(ctypes.Structure):
                 ("bc", ctypes.c_int), ("bright", ctypes.c_int), ("contrast", ctypes.c_double)]
 
 
+class SegPrologue(ctypes.Structure):
+    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("relu", ctypes.c_int)]
+
+
 class SegAdamFused(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
                 ("rows_dst", ctypes.c_void_p), ("rows_ap", ctypes.c_int), ("rows_bp", ctypes.c_int),
@@ -118,6 +123,8 @@ SIGNATURES = {
     "seg_tconv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "seg_conv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_fwd_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_bwd_filter_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _P, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_tconv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),

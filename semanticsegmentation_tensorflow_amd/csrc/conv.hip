@@ -504,6 +504,27 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_nt2_short = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "tn_fill")) {        // filter-gradient split-K target, blocks per CU
+        if (value < 1 || value > 64) return SEG_EINVAL;
+        seg::g_tn_fill = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn_split_cap")) {   // max filter-gradient split-K slabs
+        if (value < 1 || value > 4096) return SEG_EINVAL;
+        seg::g_tn_split_cap = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn_reduce_sl")) {   // split-lanes of the filter-gradient split-K reducer
+        if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32 && value != 64)
+            return SEG_EINVAL;
+        seg::g_tn_reduce_sl = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn2_smallm")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_tn2_smallm = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "adam_blocks")) {   // grid cap of seg_adam_tf1_pack (0 = one block per tile)
         if (value < 0) return SEG_EINVAL;
         g_adam_blocks = value;
@@ -628,6 +649,51 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// BiasAddGrad of dy [N*OH*OW][K] when the filter-gradient kernel did not fuse it.
+static int bias_grad_fallback(const seg_conv_desc* d, const void* dy, float* dbias, void* ws, size_t ws_bytes,
+                              void* stream) {
+    return seg_bias_relu_bwd(dy, d->ldy, nullptr, 0, const_cast<void*>(dy), d->ldy, dbias,
+                             (long)d->N * d->OH * d->OW, d->K, d->k_valid, 0, 1.f, d->dtype, ws, ws_bytes, stream);
+}
+
+static seg::ProParams make_pro(const seg_prologue* pro, int cv) {
+    seg::ProParams r = {};
+    if (pro) {
+        r.gamma = pro->gamma;
+        r.beta = pro->beta;
+        r.inv = 1.0f / sqrtf(1.0f + pro->eps);   // seg_bn_relu_fwd's arithmetic
+        r.relu = pro->relu;
+        r.cv = cv;
+    }
+    return r;
+}
+
+extern "C" int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro, const void* w,
+                                  const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !w || !y || !pro || !pro->gamma || !pro->beta) return SEG_EINVAL;
+    NTParams p = conv_fwd_params(d);
+    p.x = x; p.w = w; p.y = y;
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    p.pro = make_pro(pro, d->c_valid);
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int seg_conv2d_bwd_filter_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro,
+                                         const void* dy, float* dw, float* dbias, void* ws, size_t ws_bytes,
+                                         void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !dy || !dw || !pro || !pro->gamma || !pro->beta) return SEG_EINVAL;
+    TNParams p = conv_bwd_filter_params(d);
+    p.x = x; p.b = dy; p.out = dw; p.dbias = nullptr;
+    p.pro = make_pro(pro, d->c_valid);
+    st = seg::launch_tn(p, d->dtype, ws, ws_bytes, (hipStream_t)stream);
+    if (st || !dbias) return st;
+    return bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
+}
+
 extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w, const seg_epilogue* epi,
                                    void* dx, void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);
@@ -642,13 +708,6 @@ extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const
         if (epi->residual && epi->ld_residual == 0) p.epi.ld_res = d->ldx;
     }
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
-}
-
-// BiasAddGrad of dy [N*OH*OW][K] when the filter-gradient kernel did not fuse it.
-static int bias_grad_fallback(const seg_conv_desc* d, const void* dy, float* dbias, void* ws, size_t ws_bytes,
-                              void* stream) {
-    return seg_bias_relu_bwd(dy, d->ldy, nullptr, 0, const_cast<void*>(dy), d->ldy, dbias,
-                             (long)d->N * d->OH * d->OW, d->K, d->k_valid, 0, 1.f, d->dtype, ws, ws_bytes, stream);
 }
 
 extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias,

@@ -23,6 +23,18 @@ struct EpiParams {
     float mask_scale;
 };
 
+// Optional A-operand prologue: the operand is relu(x * gamma[c] * inv + beta[c])
+// (frozen-statistics BatchNorm + ReLU of the producing layer, applied while
+// staging; zero-padded (out-of-image) elements stay zero, as TF pads the BN
+// output) -- FC-DenseNet's BN -> ReLU -> conv (Network/model/FCDenseNet.py:25-28).
+struct ProParams {
+    const float* gamma;   // null: off
+    const float* beta;
+    float inv;            // 1 / sqrt(1 + eps), as seg_bn_relu_fwd
+    int relu;
+    int cv;               // valid channels
+};
+
 // C[m][n] = sum_k A[m][k] B[n][k].  Row m -> (img, a, b) on an Ha x Wa grid;
 // reduction k -> (tap=(j,i), channel c), taps_w taps along w.
 // A element: x[img, a*ish + j*tsh + ioh, b*isw + i*tsw + iow, c]  (0 outside)
@@ -45,6 +57,7 @@ struct NTParams {
     int kt_per_split;
     // conv2d_transpose phase split: blockIdx.z = ph*st_w + pw
     int phase, st_h, st_w, pad_t, pad_l, Nimg;
+    ProParams pro;
 };
 
 // C[m][n] = sum_p A[p][m] B[p][n].  p -> (img, a, b) on an Ha x Wa grid;
@@ -87,6 +100,7 @@ struct TNParams {
         int first_round;       // blocks of the first dispatch round (2 per CU)
         int* cu_slots;         // per-CU arrival counters (zeroed per launch)
     } adam;
+    ProParams pro;             // A = x operand prologue (igemm_tn only)
 };
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
@@ -102,12 +116,65 @@ extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
 extern int g_tn_variant;
+extern int g_tn_fill;
+extern int g_tn_split_cap;
+extern int g_tn2_smallm;
+extern int g_tn_reduce_sl;
 extern int g_nt2_ablate;
 void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype = SEG_BF16);
 
 // 256 x 256 NT tiles (igemm3.hip) for bf16 with N > 128
 extern int g_nt3;
 bool nt3_ok(const NTParams& p, int dtype);
+// the 16-byte chunk v of channels c0..c0+EPC-1 through the prologue
+template <typename T>
+__device__ __forceinline__ uint4 apply_pro(const ProParams& pro, uint4 v, int c0) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    float f[EPC];
+    Chunk<T>::unpack(v, f);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+        const int c = c0 + e;
+        const float sc = c < pro.cv ? pro.gamma[c] * pro.inv : 0.f;
+        const float sh = c < pro.cv ? pro.beta[c] : 0.f;
+        float o = f[e] * sc + sh;
+        if (pro.relu) o = fmaxf(o, 0.f);
+        f[e] = o;
+    }
+    return Chunk<T>::pack(f);
+}
+
+// LDS-DMA kernels (igemm2.hip) apply the prologue after the LDS read, so only
+// where no operand element is zero padding: single-tap (1x1) problems.
+// tn2: the transposed A fragment is 8 pixels of ONE channel -> scalar pair.
+template <typename T>
+__device__ __forceinline__ uint4 pro_affine(uint4 v, float sc, float sh, int relu) {
+    float f[8];
+    Chunk<T>::unpack(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float o = f[e] * sc + sh;
+        f[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+    return Chunk<T>::pack(f);
+}
+// nt2: the A fragment is 8 channels of one pixel; ss = (scale, shift) x 8
+template <typename T>
+__device__ __forceinline__ uint4 pro_affine8(uint4 v, const float* ss, int relu) {
+    float f[8];
+    Chunk<T>::unpack(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float o = f[e] * ss[2 * e] + ss[2 * e + 1];
+        f[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+    return Chunk<T>::pack(f);
+}
+constexpr int NT2_PRO_MAXK = 1024;    // (scale, shift) table in LDS
+bool nt2_pro_ok(const NTParams& p, int dtype, int nphases);
+void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s);
+void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype);
+
 inline bool nt3_applies(int N, int dtype) { return g_nt3 && dtype == SEG_BF16 && N > 128; }
 void nt3_info(int M, int N, int K, int cus, int* splits);
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s);

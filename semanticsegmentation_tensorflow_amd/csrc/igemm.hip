@@ -172,6 +172,7 @@ __global__ __launch_bounds__(256) void igemm_nt(NTParams p) {
             const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
             const T* src = X + a_off[i] + ((long)ih * p.IW + iw) * p.ldx + cc;
             uint4 v = ld16(ok ? src : X);
+            if (p.pro.gamma && ok) v = apply_pro<T>(p.pro, v, cc);
             ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
         }
         const long wtap = (long)((rb + p.rstep * tj) * p.Sfull + (sb + p.sstep * ti)) * p.w_tap + cc;
@@ -412,6 +413,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
             const bool ok = a_mok && pp[i] < p.P && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
             const T* src = X + (long)pimg[i] * p.x_img + ((long)ih * p.IW + iw) * p.ldx + ac;
             uint4 v = ld16(ok ? src : X);
+            if (p.pro.gamma && ok) v = apply_pro<T>(p.pro, v, ac);
             ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
             // advance by one k tile
             pp[i] += BKP;
@@ -556,49 +558,74 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
         }
 }
 
-__global__ void splitk_reduce_tn(TNParams p, int splits) {
+// Split-K slab sum of the filter gradients.  A wave holds VW = 64 / SL output
+// float4s x SL split-lanes: lane sl sums slabs sl, sl+SL, ... and the SL
+// partial sums meet by cross-lane shuffles (no LDS allocation, so the reducer
+// can share a CU with an LDS-heavy conv kernel when it runs on the side
+// stream), so a 256-slab reduction of a small gradient (wgrad_halo: 576 x 16)
+// runs on ~150 blocks instead of 9 latency-bound ones.
+// Row M of the output range is the fused BiasAddGrad: slab rows M..Mp-1.
+__global__ __launch_bounds__(256) void splitk_reduce_tn(TNParams p, int splits, int SL) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int VW = 64 / SL;
+    const int v = lane % VW, sl = lane / VW;
     const int c4 = p.N / 4;
-    const long total = (long)(p.Mp > p.M ? p.M + 1 : p.M) * c4;   // slab rows M..Mp-1: BiasAddGrad partials
+    const long total = (long)(p.Mp > p.M ? p.M + 1 : p.M) * c4;
     const long slab = (long)p.Mp * p.N;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int m = (int)(i / c4);
-        const int n0 = (int)(i - (long)m * c4) * 4;
-        float4 s = {0.f, 0.f, 0.f, 0.f};
-        const float* src = p.partial + (long)m * p.N + n0;
-        int z = 0;
-        for (; z + 4 <= splits; z += 4) {   // 4 independent slab loads in flight
-            const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
-            const float4 b = *reinterpret_cast<const float4*>(src + (z + 1) * slab);
-            const float4 c = *reinterpret_cast<const float4*>(src + (z + 2) * slab);
-            const float4 d = *reinterpret_cast<const float4*>(src + (z + 3) * slab);
-            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-            s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
-            s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
-            s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
-        }
-        for (; z < splits; ++z) {
-            const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
-            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-        }
-        for (int r = p.M + 1; m == p.M && r < p.Mp; ++r)   // further BiasAddGrad partial rows
-            for (int zz = 0; zz < splits; ++zz) {
-                const float4 a = *reinterpret_cast<const float4*>(p.partial + zz * slab + (long)r * p.N + n0);
+    const long i = ((long)blockIdx.x * 4 + wave) * VW + v;
+    const bool live = i < total;
+    const int m = live ? (int)(i / c4) : 0;
+    const int n0 = live ? (int)(i - (long)m * c4) * 4 : 0;
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        const int r_end = m == p.M ? p.Mp : m + 1;     // bias row: all partial rows
+        for (int r = m; r < r_end; ++r) {
+            const float* src = p.partial + (long)r * p.N + n0;
+            int z = sl;
+            for (; z + 3 * SL < splits; z += 4 * SL) {  // 4 independent slab loads in flight
+                const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
+                const float4 b = *reinterpret_cast<const float4*>(src + (z + SL) * slab);
+                const float4 c = *reinterpret_cast<const float4*>(src + (z + 2 * SL) * slab);
+                const float4 d = *reinterpret_cast<const float4*>(src + (z + 3 * SL) * slab);
+                s.x += (a.x + b.x) + (c.x + d.x);
+                s.y += (a.y + b.y) + (c.y + d.y);
+                s.z += (a.z + b.z) + (c.z + d.z);
+                s.w += (a.w + b.w) + (c.w + d.w);
+            }
+            for (; z < splits; z += SL) {
+                const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
                 s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
             }
-        const float vv[4] = {s.x, s.y, s.z, s.w};
-        if (m == p.M) {               // fused BiasAddGrad row
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (n0 + j < p.n_valid) p.dbias[n0 + j] = vv[j];
-            continue;
         }
-        bool ok;
-        float* orow = tn_row(p, m, ok);
-        if (!ok) continue;
+    }
+    for (int off = VW; off < 64; off <<= 1) {         // all lanes take part
+        s.x += __shfl_xor(s.x, off);
+        s.y += __shfl_xor(s.y, off);
+        s.z += __shfl_xor(s.z, off);
+        s.w += __shfl_xor(s.w, off);
+    }
+    if (!live || sl) return;
+    const float vv[4] = {s.x, s.y, s.z, s.w};
+    if (m == p.M) {               // fused BiasAddGrad row
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (n0 + j < p.n_valid) orow[(long)(n0 + j) * p.o_n] = vv[j];
+            if (n0 + j < p.n_valid) p.dbias[n0 + j] = vv[j];
+        return;
     }
+    bool ok;
+    float* orow = tn_row(p, m, ok);
+    if (!ok) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (n0 + j < p.n_valid) orow[(long)(n0 + j) * p.o_n] = vv[j];
+}
+
+static void launch_splitk_reduce_tn(TNParams& p, int splits, hipStream_t s) {
+    int SL = 1;                  // ~8 slabs per lane, at most g_tn_reduce_sl lanes
+    while (SL < g_tn_reduce_sl && SL * 8 < splits) SL *= 2;
+    const long total = (long)(p.Mp > p.M ? p.M + 1 : p.M) * (p.N / 4);
+    const long blocks = (total + 256 / SL - 1) / (256 / SL);
+    hipLaunchKernelGGL(splitk_reduce_tn, dim3((unsigned)blocks), dim3(256), 0, s, p, splits, SL);
 }
 
 // ---------------------------------------------------------------------------
@@ -690,6 +717,39 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
     if (nphases > 1) splits = 1;
     p.partial = nullptr;
+    if (p.pro.gamma && g_nt_variant == 2 && nt2_pro_ok(p, dt_traits<T>::id, nphases)) {
+        launch_nt2_pro(p, dt_traits<T>::id, 1, max_m, s);    // 1x1: K <= 1024, no split-K
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
+    if (p.pro.gamma) {                     // operand prologue: the register-staged kernel
+        bm = 128;
+        const long tiles = (long)((max_m + 127) / 128) * ((p.N + bn - 1) / bn);
+        splits = 1;
+        if (tiles < 2 * num_cus()) {
+            const int kt = (p.K + BK - 1) / BK;
+            splits = std::min<int>(std::max(1, kt / 8), (int)((2 * num_cus() + tiles - 1) / tiles));
+        }
+        int gridz = nphases;
+        if (splits > 1) {
+            const int kt = (p.K + BK - 1) / BK;
+            p.kt_per_split = (kt + splits - 1) / splits;
+            splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
+            if (!ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float)) return SEG_EWORKSPACE;
+            p.partial = reinterpret_cast<float*>(ws);
+            gridz = splits;
+        }
+        if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
+        else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
+        SEG_CHECK_LAUNCH();
+        if (p.partial) {
+            const long total = (long)p.M * (p.N / 8);
+            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+            SEG_CHECK_LAUNCH();
+            p.partial = nullptr;
+        }
+        return SEG_OK;
+    }
     if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dt_traits<T>::id)) {
         launch_res64(p, num_cus(), s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
@@ -780,9 +840,14 @@ int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t w
 }
 
 int g_tn_variant = 2;
+int g_tn_fill = 2;          // split-K target: g_tn_fill blocks per CU
+int g_tn_split_cap = 256;   // max split-K slabs
+int g_tn2_smallm = 0;       // 16-bit M < 128: igemm_tn2 (padded 128-row tiles) instead of igemm_tn
+int g_tn_reduce_sl = 16;    // max split-lanes of splitk_reduce_tn (1 = one thread per output float4)
 
-static void choose_tn(int M, int N, int P, int bkp, bool v2, int& bm, int& bn, int& splits) {
-    if (g_tn_variant == 2 && v2 && M >= 128) {
+// v2: 0 = igemm_tn tiles, 1 = igemm_tn2 tiles when M >= 128, 2 = igemm_tn2 tiles
+static void choose_tn(int M, int N, int P, int bkp, int v2, int& bm, int& bn, int& splits) {
+    if (g_tn_variant == 2 && (v2 == 2 || (v2 && (M >= 128 || g_tn2_smallm)))) {
         // v2 tiles: minimise padded work / relative tile efficiency
         static const int cand[5][2] = {{128, 256}, {256, 128}, {128, 128}, {256, 64}, {128, 64}};
         static const double eff[5] = {1.0, 1.0, 0.85, 0.85, 0.8};
@@ -797,13 +862,13 @@ static void choose_tn(int M, int N, int P, int bkp, bool v2, int& bm, int& bn, i
         bn = N <= 64 ? 64 : 128;
     }
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-    const int target = 2 * num_cus();
+    const int target = g_tn_fill * num_cus();
     const int kt = (P + bkp - 1) / bkp;
     splits = 1;
     if (tiles < target) {
         splits = (int)((target + tiles - 1) / tiles);
         splits = std::min(splits, std::max(1, kt / 8));
-        splits = std::min(splits, 256);
+        splits = std::min(splits, g_tn_split_cap);
     }
 }
 
@@ -814,6 +879,11 @@ void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits) {
 size_t tn_workspace(int M, int N, int P, int dtype) {
     int bm, bn, splits;
     choose_tn(M, N, P, dtype == SEG_F32 ? 32 : 64, dtype != SEG_F32, bm, bn, splits);
+    if (dtype != SEG_F32) {        // prologue (folded BatchNorm) launches: tn2 tiles at any M
+        int b2m, b2n, s2;
+        choose_tn(M, N, P, 64, 2, b2m, b2n, s2);
+        splits = std::max(splits, s2);
+    }
     if (g_tn_variant == 2 && tn3_applies(M, N, dtype)) {
         int s3;
         tn3_info(M, N, P, num_cus(), &s3);
@@ -837,21 +907,40 @@ static void tn_finish(TNParams& p, int splits, hipStream_t s) {
         return;
     }
     if (!p.partial) return;
-    const long total = (long)p.Mp * (p.N / 4);
-    hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+    launch_splitk_reduce_tn(p, splits, s);
     p.partial = nullptr;
 }
 
-void tn_reduce(TNParams& p, int splits, hipStream_t s) {
-    const long total = (long)p.Mp * (p.N / 4);
-    hipLaunchKernelGGL(splitk_reduce_tn, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
-}
+void tn_reduce(TNParams& p, int splits, hipStream_t s) { launch_splitk_reduce_tn(p, splits, s); }
 
 template <typename T>
 static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BKP = sizeof(T) == 2 ? 64 : 32;
     p.partial = nullptr;
     p.Mp = p.M;
+    if (p.pro.gamma) {       // operand prologue: tn2 for single-tap 16-bit problems, else igemm_tn
+        const bool v2 = sizeof(T) == 2 && g_tn_variant == 2 && p.M == p.Cg;
+        int bm, bn, splits;
+        choose_tn(p.M, p.N, p.P, BKP, v2 ? 2 : 0, bm, bn, splits);
+        int gridz = 1;
+        if (splits > 1) {
+            const int kt = (p.P + BKP - 1) / BKP;
+            p.kt_per_split = (kt + splits - 1) / splits;
+            splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
+            if (!ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float)) return SEG_EWORKSPACE;
+            p.partial = reinterpret_cast<float*>(ws);
+            gridz = splits;
+        }
+        if (v2) launch_tn2_pro(p, bm, bn, gridz, s, dt_traits<T>::id);
+        else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
+        else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);
+        else if (bn == 64) launch_tn_t<T, 128, 64>(p, gridz, s);
+        else launch_tn_t<T, 128, 128>(p, gridz, s);
+        SEG_CHECK_LAUNCH();
+        tn_finish(p, splits, s);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     if (smallc_wgrad_ok(p, dt_traits<T>::id)) {
         const int splits = smallc_wgrad_splits(p, num_cus());
         if (p.dbias) p.Mp = p.M + 1;
@@ -896,7 +985,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     if (tn3) {
         launch_tn3(p, gridz, s);
-    } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128)) {
+    } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128 || g_tn2_smallm)) {
         launch_tn2(p, bm, bn, gridz, s, dt_traits<T>::id);
     } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);
     else if (bm == 64) launch_tn_t<T, 64, 128>(p, gridz, s);

@@ -51,7 +51,10 @@ template <typename T>
 // <= 128 channels: one or two k tiles per block), where the smaller LDS
 // footprint lets two blocks share a CU so one block's loads overlap the
 // other's epilogue -- with one block per CU those blocks are pure latency.
-template <typename T, int BM, int BN, int WM, int WN, int ABL = 0, int NSTG = 3>
+// PRO: the A operand goes through p.pro (BatchNorm + ReLU) between the LDS
+// read and the MFMA; the per-channel (scale, shift) table is staged in LDS
+// once per block (single-tap problems, K <= NT2_PRO_MAXK).
+template <typename T, int BM, int BN, int WM, int WN, int ABL = 0, int NSTG = 3, bool PRO = false>
 __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTParams p) {
     constexpr int NW = WM * WN;
     constexpr int EPC = dt_traits<T>::EPC;
@@ -154,6 +157,18 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
 
     const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
 
+    const float* ptab = nullptr;
+    if constexpr (PRO) {
+        // before the first DMA: the table loads' wait drains nothing else
+        __shared__ __attribute__((aligned(16))) float ptab_s[2 * NT2_PRO_MAXK];
+        for (int k = tid; k < KT * BK; k += NW * 64) {
+            const bool v = k < p.pro.cv;
+            ptab_s[2 * k] = v ? p.pro.gamma[k] * p.pro.inv : 0.f;
+            ptab_s[2 * k + 1] = v ? p.pro.beta[k] : 0.f;
+        }
+        ptab = ptab_s;      // visible after the first iteration's barrier
+    }
+
     auto load_stage = [&](int stage) {
         const unsigned sb_ = lds0 + stage * STAGE;
         const bool kok = kg < p.K;
@@ -208,6 +223,17 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
             for (int mi = 0; mi < TM; ++mi) {
                 const int row = wm * WTM + mi * 16 + fr;
                 af[mi] = *reinterpret_cast<const uint4*>(As + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+            }
+            if constexpr (PRO) {
+                float ss[16];
+                const float4* tp = reinterpret_cast<const float4*>(ptab + 2 * (kt * BK + chunk * 8));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = tp[q];
+                    ss[4 * q] = t.x; ss[4 * q + 1] = t.y; ss[4 * q + 2] = t.z; ss[4 * q + 3] = t.w;
+                }
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi) af[mi] = pro_affine8<T>(af[mi], ss, p.pro.relu);
             }
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
@@ -334,7 +360,9 @@ __device__ __forceinline__ int tn2_swz(int row) {
     else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+// PRO: A (= x) through p.pro after the transposed LDS read; a lane's A rows
+// are fixed channels, so its (scale, shift) pairs load once (single-tap only).
+template <typename T, int BM, int BN, int WM, int WN, bool PRO = false>
 __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m, int tiles_n, int splits) {
     constexpr int NW = WM * WN;
     constexpr int BKP = 64;
@@ -431,6 +459,17 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float psc[PRO ? TM : 1], psh[PRO ? TM : 1];
+    if constexpr (PRO) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+            const int m = m0 + wm * WTM + mi * 16 + (lane & 15);
+            const bool v = m < p.M && m < p.pro.cv;
+            psc[mi] = v ? p.pro.gamma[m] * p.pro.inv : 0.f;
+            psh[mi] = v ? p.pro.beta[m] : 0.f;
+            asm volatile("" ::"v"(psc[mi]), "v"(psh[mi]));   // loaded before the first DMA
+        }
+    }
     if (kt_begin < kt_end) load_stage(0);
     if (kt_begin + 1 < kt_end) load_stage(1);
     const int fr = lane & 15, fg = lane >> 4;
@@ -457,6 +496,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(As + (r1 + 4) * AROWB + 16 * c2 + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 af[mi] = __builtin_bit_cast(uint4, v);
+                if constexpr (PRO) af[mi] = pro_affine<T>(af[mi], psc[mi], psh[mi], p.pro.relu);
             }
             const int t1 = tn2_swz<BROWB>(r1), t2 = tn2_swz<BROWB>(r1 + 4);
 #pragma unroll
@@ -504,25 +544,30 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
         }
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN, bool PRO = false>
 void launch_tn2_t(TNParams& p, int splits, hipStream_t s) {
     const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
-    hipLaunchKernelGGL((igemm_tn2<T, BM, BN, WM, WN>), dim3(tm * tn * splits), dim3(WM * WN * 64), 0, s, p, tm, tn,
-                       splits);
+    hipLaunchKernelGGL((igemm_tn2<T, BM, BN, WM, WN, PRO>), dim3(tm * tn * splits), dim3(WM * WN * 64), 0, s, p, tm,
+                       tn, splits);
 }
 
-template <typename T>
+template <typename T, bool PRO = false>
 static void launch_tn2_typed(TNParams& p, int bm, int bn, int splits, hipStream_t s) {
-    if (bm == 256 && bn == 128) launch_tn2_t<T, 256, 128, 4, 2>(p, splits, s);
-    else if (bm == 128 && bn == 256) launch_tn2_t<T, 128, 256, 2, 4>(p, splits, s);
-    else if (bm == 256 && bn == 64) launch_tn2_t<T, 256, 64, 4, 2>(p, splits, s);
-    else if (bm == 128 && bn == 64) launch_tn2_t<T, 128, 64, 4, 2>(p, splits, s);
-    else launch_tn2_t<T, 128, 128, 2, 4>(p, splits, s);
+    if (bm == 256 && bn == 128) launch_tn2_t<T, 256, 128, 4, 2, PRO>(p, splits, s);
+    else if (bm == 128 && bn == 256) launch_tn2_t<T, 128, 256, 2, 4, PRO>(p, splits, s);
+    else if (bm == 256 && bn == 64) launch_tn2_t<T, 256, 64, 4, 2, PRO>(p, splits, s);
+    else if (bm == 128 && bn == 64) launch_tn2_t<T, 128, 64, 4, 2, PRO>(p, splits, s);
+    else launch_tn2_t<T, 128, 128, 2, 4, PRO>(p, splits, s);
 }
 
 void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype) {
     if (dtype == SEG_F16) launch_tn2_typed<f16>(p, bm, bn, splits, s);
     else launch_tn2_typed<bf16>(p, bm, bn, splits, s);
+}
+
+void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype) {
+    if (dtype == SEG_F16) launch_tn2_typed<f16, true>(p, bm, bn, splits, s);
+    else launch_tn2_typed<bf16, true>(p, bm, bn, splits, s);
 }
 
 int g_nt2_ablate = 0;
@@ -547,6 +592,28 @@ int g_nt2_short = 8;
 
 bool nt2_short(const NTParams& p, int dtype) {
     return dtype == SEG_BF16 && !p.partial && p.K <= 64 * g_nt2_short && g_nt2_ablate == 0;
+}
+
+bool nt2_pro_ok(const NTParams& p, int dtype, int nphases) {
+    return (dtype == SEG_BF16 || dtype == SEG_F16) && nphases == 1 && g_nt2_ablate == 0 && p.K == p.C &&
+           (p.K + 63) / 64 * 64 <= NT2_PRO_MAXK;
+}
+
+// 192-row tiles: the 2-stage ring (64 KiB) + the 8 KiB table leave room for
+// two blocks per CU at 64 columns.
+template <typename T>
+static void launch_nt2_pro_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
+    const int tm = (max_m + 191) / 192;
+    if (p.N <= 64)
+        hipLaunchKernelGGL((igemm_nt2<T, 192, 64, 4, 2, 0, 2, true>), dim3(tm, 1, gridz), dim3(512), 0, s, p);
+    else
+        hipLaunchKernelGGL((igemm_nt2<T, 192, 128, 4, 2, 0, 3, true>), dim3(tm * ((p.N + 127) / 128), 1, gridz),
+                           dim3(512), 0, s, p);
+}
+
+void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s) {
+    if (dtype == SEG_F16) launch_nt2_pro_t<f16>(p, gridz, max_m, s);
+    else launch_nt2_pro_t<bf16>(p, gridz, max_m, s);
 }
 
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s) {

@@ -13,7 +13,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import SegConvDesc, SegEpilogue, check
+from ._lib import SegConvDesc, SegEpilogue, SegPrologue, check
 
 F32, BF16, F16 = 0, 1, 2
 _TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
@@ -153,6 +153,34 @@ def conv2d_fwd(desc, x, w_krsc, y, epi=None, ws=None, stream=None):
                                     None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
                                     stream_ptr(stream)), "conv2d")
     return y
+
+
+def prologue(gamma, beta, eps=1e-3, relu=True):
+    """The conv input is relu(x * gamma / sqrt(1 + eps) + beta) (frozen BN + ReLU).
+    The struct keeps gamma / beta alive (it holds raw device pointers)."""
+    pro = SegPrologue(gamma.data_ptr(), beta.data_ptr(), float(eps), 1 if relu else 0)
+    pro._keep = (gamma, beta)
+    return pro
+
+
+def conv2d_fwd_pro(desc, x, pro, w_krsc, y, epi=None, ws=None, stream=None):
+    """Conv2D of relu(BN(x)) with the BN + ReLU applied while staging x."""
+    d = _with_ld(desc, x, y)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_FWD))
+    check(_lib.lib().seg_conv2d_fwd_pro(ctypes.byref(d), ptr(x), ctypes.byref(pro), ptr(w_krsc),
+                                        None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
+                                        stream_ptr(stream)), "conv2d")
+    return y
+
+
+def conv2d_bwd_filter_pro(desc, x, pro, dy, dw, ws=None, stream=None, dbias=None):
+    """Conv2DBackpropFilter with input relu(BN(x)) recomputed from x."""
+    d = _with_ld(desc, x, dy)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_BWD_FILTER))
+    check(_lib.lib().seg_conv2d_bwd_filter_pro(ctypes.byref(d), ptr(x), ctypes.byref(pro), ptr(dy), ptr(dw),
+                                               None if dbias is None else ptr(dbias), wsp, wss,
+                                               stream_ptr(stream)), "conv2d_backprop_filter")
+    return dw
 
 
 def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None, epi=None):

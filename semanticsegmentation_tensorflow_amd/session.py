@@ -188,6 +188,8 @@ class Session:
         self.fuse_dropout = True
         # DenseBlock concatenations as channel views of one block buffer
         self.alias_concat = True
+        # BatchNorm(+ReLU) feeding a single 1x1 conv folded into its operand prologue
+        self.fold_bn = True
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -495,8 +497,37 @@ class Session:
             else:
                 raise NotImplementedError(f"op {t} is not on the hot path")
         p.nodes = nodes
+        self._fold_bn_prologues(p, fetched)
         self._allocate(p, consumers, feeds)
         return p
+
+    def _fold_bn_prologues(self, p, fetched):
+        """FC-DenseNet's pre-activation BN -> ReLU -> 1x1 conv
+        (Network/model/FCDenseNet.py:25-28, :39-41): a BatchNorm(+ReLU) node
+        whose output feeds exactly one 1x1 conv becomes that conv's operand
+        prologue -- the BN output is never written (forward) and the filter
+        gradient recomputes it from x while staging.  Its backward is
+        unchanged (the BN gradient re-derives the mask from x)."""
+        p.folded = set()
+        if not self.fold_bn:
+            return
+        users = {}
+        for n in p.nodes:
+            for t in list(n.inputs) + [getattr(n, "residual", None)]:
+                if t is not None:
+                    users.setdefault(id(t), []).append(n)
+        for b in p.nodes:
+            if b.kind != "bn" or id(b.output) in fetched:
+                continue
+            us = users.get(id(b.output), [])
+            if len(us) != 1 or us[0].kind != "conv" or us[0].inputs[0] is not b.output:
+                continue
+            c = us[0]
+            R, S_, C, _ = c.w.shape
+            if (R, S_) != (1, 1) or c.stride != 1 or C % 8:
+                continue
+            c.pro = b
+            p.folded.add(id(b))
 
     def _infer(self, op, shp):
         t = op.type
@@ -661,7 +692,9 @@ class Session:
                 buf[id(y)] = src if len(shp[id(y)]) == 4 and src.dim() == 4 else src.unsqueeze(-1)
                 continue
             s = shp[id(y)]
-            if id(y) in p.alias:
+            if id(n) in p.folded:
+                buf[id(y)] = buf[id(n.inputs[0])]    # never written: its consumer reads x through the prologue
+            elif id(y) in p.alias:
                 r, off = p.alias[id(y)]
                 buf[id(y)] = roots[r][..., off:off + s[3]]
             else:
@@ -891,8 +924,13 @@ class Session:
                 n.seed_val = (step_seed + i * 131) & 0xFFFFFFFF
                 epi = ops.epilogue(bias=store.param(n.bias.var_name) if n.bias is not None else None,
                                    relu=n.relu, keep_prob=kp, seed=n.seed_val)
-                self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
-                            store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
+                if getattr(n, "pro", None) is not None:
+                    b = n.pro
+                    self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd_pro, n.desc, buf[id(b.inputs[0])],
+                                self._prologue(b), store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
+                else:
+                    self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
+                                store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
             elif k == "tconv":
                 x = buf[id(n.inputs[0])]
                 res = buf[id(n.residual)] if n.residual is not None else None
@@ -907,6 +945,8 @@ class Session:
             elif k == "Add":
                 ops.add(buf[id(n.inputs[0])], buf[id(n.inputs[1])], y)
             elif k == "bn":
+                if id(n) in p.folded:
+                    continue                        # applied by its conv's operand prologue
                 C = p.shapes[id(n.inputs[0])][3]
                 ops.bn_relu_fwd(buf[id(n.inputs[0])], y, store.param(n.gamma.var_name),
                                 store.param(n.beta.var_name), C, n.relu, n.eps)
@@ -1199,8 +1239,12 @@ class Session:
                     # tests: the buffers of this layer's three kernels (they persist
                     # after the step; dx before any accumulation of other consumers)
                     mask = self._mask_epi(p, x) if dx is not None else None
+                    pro = getattr(n, "pro", None)
                     self.capture.append({"kind": "conv", "name": n.w.var_name, "bias": getattr(n.bias, "var_name", None),
-                                         "x": buf[id(x)], "y": buf[id(n.output)], "dz": dz, "dx": dx,
+                                         "x": buf[id(x)] if pro is None else buf[id(pro.inputs[0])],
+                                         "pro": None if pro is None else (pro.gamma.var_name, pro.beta.var_name,
+                                                                          pro.eps, pro.relu),
+                                         "y": buf[id(n.output)], "dz": dz, "dx": dx,
                                          "dx_masked": mask is not None, "relu": n.relu, "desc": n.desc,
                                          "stride": n.stride, "dilation": n.dilation, "padding": n.padding})
                 want_w = n.w.var_name in p.var_set
@@ -1208,6 +1252,11 @@ class Session:
                 gw = store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w)
                 if not (want_w or want_b):
                     pass          # frozen layer (outside var_list): no filter gradient
+                elif getattr(n, "pro", None) is not None:
+                    # input relu(BN(x)) recomputed from x while staging (folded BatchNorm)
+                    b = n.pro
+                    self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_pro, n.desc, buf[id(b.inputs[0])],
+                                self._prologue(b), dz, gw, ws, None, fused_db)
                 elif self._fused is not None and id(n) in p.adam_fusable and want_w:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
@@ -1363,6 +1412,10 @@ class Session:
             import torch.distributed as dist
             dist.all_reduce(self._finite_flag, op=dist.ReduceOp.MAX, group=self.dp.group)
         return int(self._finite_flag.item()) == 0
+
+    def _prologue(self, b):
+        st = self.store
+        return ops.prologue(st.param(b.gamma.var_name), st.param(b.beta.var_name), b.eps, b.relu)
 
     def _scratch_grad(self, p, var):
         """fp32 gradient sink for a filter outside var_list whose layer still

@@ -88,10 +88,18 @@ def _host(t, c):
     return t[..., :c].float().cpu()
 
 
-def _layer_local(rec, w, b, sess):
-    """Oracle fwd / dgrad / wgrad of one conv from the device's own operands."""
+def _layer_local(rec, w, b, sess, weights=None):
+    """Oracle fwd / dgrad / wgrad of one conv from the device's own operands
+    (`weights`: the pre-step values of a folded BatchNorm's gamma / beta --
+    the store holds the post-Adam ones)."""
     C, K = w.shape[2], w.shape[3]
-    x = _host(rec["x"], C).requires_grad_(True)
+    x = _host(rec["x"], C)
+    if rec.get("pro"):          # BatchNorm + ReLU folded into this conv's operand prologue
+        gname, bname, eps, relu = rec["pro"]
+        gamma, beta = (torch.from_numpy(weights[gname]), torch.from_numpy(weights[bname]))
+        x = x * (gamma / np.sqrt(1.0 + eps)) + beta
+        x = bf16r(torch.relu(x) if relu else x)
+    x = x.requires_grad_(True)
     wt = bf16r(torch.from_numpy(w)).requires_grad_(True)
     z = T.conv2d(x, wt, rec["stride"], rec["padding"], rec["dilation"])
     y = z + torch.from_numpy(b) if b is not None else z
@@ -232,7 +240,7 @@ def test_c3_layer_local_parity(c3):
     sample = recs[:6] + recs[len(recs) // 2:len(recs) // 2 + 4] + recs[-6:]
     bad = []
     for rec in sample:
-        r = _layer_local(rec, weights[rec["name"]], None, sess)
+        r = _layer_local(rec, weights[rec["name"]], None, sess, weights)
         if "dgrad" in r:
             del r["dgrad"]      # dense-block input gradients accumulate in place (concat views)
         print(rec["name"], {k: f"{v:+.2e}" for k, v in r.items()})

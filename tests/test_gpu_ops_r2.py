@@ -55,3 +55,64 @@ def test_axpy(dev):
     ref = y + 1.5 * x
     ops.axpy(y, x, 1.5)
     np.testing.assert_allclose(y.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------
+# A-operand prologue (frozen BN + ReLU folded into the consuming conv):
+# seg_conv2d_fwd_pro / seg_conv2d_bwd_filter_pro vs the oracle's
+# conv2d(relu(batch_norm_frozen(x))) (Network/model/FCDenseNet.py:25-28)
+# ---------------------------------------------------------------------------
+from tests.gpu_utils import assert_close, from_dev, rnd, to_dev  # noqa: E402
+
+# 1x1 cases run the LDS-DMA prologue kernels in 16-bit (igemm_nt2 192x64 / 192x128,
+# igemm_tn2 at any channel count), 3x3 ones the register-staged kernels
+PRO_CASES = [(2, 9, 11, 48, 64, 1), (1, 12, 10, 136, 64, 1), (1, 7, 9, 16, 24, 3), (2, 16, 20, 64, 16, 3),
+             (1, 33, 41, 200, 136, 1), (2, 20, 30, 520, 64, 1), (1, 17, 19, 24, 8, 1)]
+PRO_DT = {torch.float32: ops.F32, torch.bfloat16: ops.BF16, torch.float16: ops.F16}
+
+
+def _pro_case(case, dtype, dev):
+    N, H, W, C, K, R = case
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    w = torch.randn(R, R, C, K, generator=g, dtype=torch.float64) / np.sqrt(R * R * C)
+    gamma = (1.0 + 0.3 * torch.randn(C, generator=g)).float()
+    beta = (0.5 * torch.randn(C, generator=g)).float()
+    xr, wr = rnd(x, dtype), rnd(w, dtype)
+    # the device's BN output in the compute dtype (what the materialised path stores)
+    a = rnd(T.relu(T.batch_norm_frozen(xr, gamma.double(), beta.double())), dtype)
+    return x, w, gamma, beta, xr, wr, a
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", PRO_CASES)
+def test_conv2d_fwd_with_bn_relu_prologue(dev, case, dtype):
+    N, H, W, C, K, R = case
+    x, w, gamma, beta, xr, wr, a = _pro_case(case, dtype, dev)
+    ref = T.conv2d(a, wr)                                   # zero SAME padding of the BN output
+    d = ops.conv_desc(N, H, W, C, K, R, R, 1, 1, "SAME", PRO_DT[dtype])
+    wk = torch.empty(ops.packed_shape(R, R, C, K, ops.PACK_KRSC), dtype=dtype, device=dev)
+    ops.pack_filter(w.float().to(dev).contiguous(), wk, ops.round8(C), ops.round8(K), ops.PACK_KRSC)
+    y = torch.empty(N, H, W, d.K, dtype=dtype, device=dev)
+    gd, bd = gamma.to(dev), beta.to(dev)
+    ops.conv2d_fwd_pro(d, to_dev(x, dtype, dev), ops.prologue(gd, bd), wk, y)
+    torch.cuda.synchronize()
+    assert_close(from_dev(y, K), ref, dtype, f"conv fwd pro {case}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", PRO_CASES)
+def test_conv2d_bwd_filter_with_bn_relu_prologue(dev, case, dtype):
+    N, H, W, C, K, R = case
+    x, w, gamma, beta, xr, wr, a = _pro_case(case, dtype, dev)
+    g = torch.Generator().manual_seed(8)
+    dy = rnd(torch.randn(N, H, W, K, generator=g, dtype=torch.float64), dtype)
+    wv = wr.clone().requires_grad_(True)
+    T.conv2d(a, wv).backward(dy)
+    d = ops.conv_desc(N, H, W, C, K, R, R, 1, 1, "SAME", PRO_DT[dtype])
+    dw = torch.zeros(R, R, C, K, device=dev)
+    ops.conv2d_bwd_filter_pro(d, to_dev(x, dtype, dev), ops.prologue(gamma.to(dev), beta.to(dev)),
+                              to_dev(dy, dtype, dev), dw)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dtype == torch.float32 else 2e-3
+    assert_close(dw.double().cpu(), wv.grad, torch.float32, f"conv wgrad pro {case}", tol)

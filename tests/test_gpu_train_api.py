@@ -96,6 +96,8 @@ def test_accumulate_template_is_adam_on_9g(dev):
         if step == 0:
             acc0 = [sess.store.aux[a.var_name].cpu().numpy() for a in accum]
         sess.run(train_step, feed_dict=feed)
+        if step == 0:   # the parameters batch 2 accumulates its gradient at
+            w1 = {k: sess.variable_value(k) for k in weights}
     assert sess.store.step == 2
 
     # the same two steps computed once per batch with grad_scale = 9: the
@@ -113,16 +115,22 @@ def test_accumulate_template_is_adam_on_9g(dev):
     for i, v in enumerate(t_vars):
         _close_updates(sess.variable_value(v.var_name), ref.variable_value(v.var_name), v.var_name, 2)
 
-    # the oracle: TF1 Adam on 9 * g, two steps; the accumulators hold 9 * g of step 2
+    # the oracle: the batch-2 accumulators hold 9 * g at the device's step-1
+    # parameters (its own trajectory drifts by TF1 Adam's 1/eps rounding gain).
+    # fp32 vs float64: a pre-activation within rounding of 0 flips its ReLU
+    # and moves a few gradient entries by ~1e-3 of the max -> L2 + tail bound
+    _, _, g1 = _oracle_grads(w1, img, lab)
+    for i, v in enumerate(t_vars):
+        a = sess.store.aux[accum[i].var_name].cpu().numpy().astype(np.float64)
+        gr = 9.0 * g1[v.var_name].numpy()
+        rel = np.linalg.norm(a - gr) / max(np.linalg.norm(gr), 1e-300)
+        tail = np.mean(np.abs(a - gr) > 2e-3 * max(np.abs(gr).max(), 1e-30))
+        assert rel <= 2e-3 and tail <= 1e-3, (v.var_name, rel, tail)
+    # and TF1 Adam on 9 * g for two steps, along the oracle's own trajectory
     adam = T.AdamTF1(lr=LR)
     w = {k: torch.from_numpy(v).double() for k, v in weights.items()}
     for step in range(2):
         _, _, g = _oracle_grads({k: v.numpy().astype(np.float32) for k, v in w.items()}, img, lab)
-        if step == 1:
-            for i, v in enumerate(t_vars):
-                a = sess.store.aux[accum[i].var_name].cpu().numpy()
-                gr = 9.0 * g[v.var_name].numpy()
-                assert np.abs(a - gr).max() <= 2e-3 * max(np.abs(gr).max(), 1e-30), v.var_name
         w = adam.apply(w, {k: 9.0 * g[k] for k in w})
     for k in ["conv1_1/weights", "conv4_2/weights", "conv6/weights", "conv8/biases", "conv_t3/bias"]:
         _close_updates(sess.variable_value(k), w[k].numpy(), k, 2)

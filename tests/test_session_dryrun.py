@@ -153,11 +153,19 @@ def test_fcdensenet_train_plan(dry):
     sess.run([train, loss], feed_dict={image: np.zeros((1, H, W, 3), np.float32),
                                        labels: np.zeros((1, H, W), np.uint8), keep: 0.8})
     c = dry.calls
-    assert c.count("seg_conv2d_fwd") == 125          # stem + 118 bottleneck + 5 transition + head
+    # stem + 118 bottleneck + 5 transition + head = 125 convs; the 1x1 convs
+    # whose input has a multiple of 8 channels read BN+ReLU through their
+    # operand prologue (the BatchNorm is folded, its output never written):
+    # dense blocks 1-4 (5 + 6 + 8 + 11 bottlenecks) and 4 transitions -- blocks
+    # 5 and 6 start from 140 / 174 channels (140 + 16 i, 174 + 16 i)
+    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pro") == 125
+    n_fold = 5 + 6 + 8 + 11 + 4
+    assert c.count("seg_conv2d_fwd_pro") == n_fold
     assert c.count("seg_tconv2d_fwd") == 5
     assert c.count("seg_concat_fwd") == 5 * 1 + (12 + 1) + (15 + 1)
     assert c.count("seg_concat_bwd") == c.count("seg_concat_fwd")
-    assert c.count("seg_bn_relu_fwd") == 123 and c.count("seg_bn_relu_bwd") == 123
+    assert c.count("seg_bn_relu_fwd") == 123 - n_fold and c.count("seg_bn_relu_bwd") == 123
     assert c.count("seg_avgpool2x2_fwd") == 5
-    assert c.count("seg_conv2d_bwd_filter") == 125
+    assert c.count("seg_conv2d_bwd_filter") + c.count("seg_conv2d_bwd_filter_pro") == 125
+    assert c.count("seg_conv2d_bwd_filter_pro") == n_fold
     assert c.count("seg_adam_tf1_pack") == 1
