@@ -79,6 +79,7 @@ CONV_CASES = [
     (2, 33, 45, 64, 328, 3, 3, 1, 1, "SAME"),   # 256-wide halo tiles: 2 N tiles + tail
     (2, 19, 131, 3, 48, 3, 3, 1, 1, "SAME"),    # first-layer kernel (C=3->8): ragged 8x64 tiles, K=48
     (1, 17, 70, 64, 48, 3, 3, 1, 1, "VALID"),   # resident-filter kernel: VALID, N=48 < 64
+    (2, 21, 67, 64, 16, 3, 3, 1, 1, "SAME"),    # resident-filter kernel, FC-DenseNet growth conv (K=16)
     # 256x256-tile GEMM (N > 128): K tiles straddling taps, N tail, split-K
     (1, 5, 7, 40, 264, 7, 7, 1, 1, "SAME"),     # conv6-like, C=40: a 64-deep K tile spans taps
     (2, 6, 9, 512, 512, 1, 1, 1, 1, "SAME"),    # conv7-like 1x1
