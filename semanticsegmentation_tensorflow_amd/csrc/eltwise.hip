@@ -634,52 +634,88 @@ __global__ __launch_bounds__(256) void bn_finish_k(const float* __restrict__ par
 // ---------------------------------------------------------------------------
 // resize_bilinear(align_corners=True)
 // ---------------------------------------------------------------------------
+// One block row = one output row (n, oy): the row's source rows and weight
+// are computed once, threads walk (ox, c) with 32-bit index math (the 64-bit
+// divisions of a flat-index decomposition dominated this pass).
 template <typename T>
-__global__ void resize_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int OH, int OW) {
+__global__ __launch_bounds__(256) void resize_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W,
+                                                    int C, int OH, int OW) {
     const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
     const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
-    const long total = (long)N * OH * OW * C;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C);
-        long t = i / C;
-        const int ow = (int)(t % OW);
-        t /= OW;
-        const int oh = (int)(t % OH);
-        const int n = (int)(t / OH);
-        const float fy = oh * sh, fx = ow * sw;
-        const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
-        const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
-        const float ly = fy - y0, lx = fx - x0;
-        const T* b = x + (long)n * H * W * C + c;
-        const float tl = to_f32(b[((long)y0 * W + x0) * C]), tr = to_f32(b[((long)y0 * W + x1) * C]);
-        const float bl = to_f32(b[((long)y1 * W + x0) * C]), br = to_f32(b[((long)y1 * W + x1) * C]);
+    const int row = blockIdx.x;                   // n * OH + oy
+    const int n = row / OH, oh = row - n * OH;
+    const float fy = oh * sh;
+    const int y0 = (int)floorf(fy);
+    const int y1 = min(y0 + 1, H - 1);
+    const float ly = fy - y0;
+    const T* r0 = x + ((long)n * H + y0) * W * C;
+    const T* r1 = x + ((long)n * H + y1) * W * C;
+    T* yr = y + (long)row * OW * C;
+    const int rowlen = OW * C;
+    for (int j = blockIdx.y * blockDim.x + threadIdx.x; j < rowlen; j += gridDim.y * blockDim.x) {
+        const int ow = j / C, c = j - (j / C) * C;
+        const float fx = ow * sw;
+        const int x0 = (int)floorf(fx);
+        const int x1 = min(x0 + 1, W - 1);
+        const float lx = fx - x0;
+        const float tl = to_f32(r0[x0 * C + c]), tr = to_f32(r0[x1 * C + c]);
+        const float bl = to_f32(r1[x0 * C + c]), br = to_f32(r1[x1 * C + c]);
         const float top = tl + (tr - tl) * lx, bot = bl + (br - bl) * lx;
-        y[i] = from_f32<T>(top + (bot - top) * ly);
+        yr[j] = from_f32<T>(top + (bot - top) * ly);
     }
 }
 
+// Output positions o (of n_out) whose bilinear source pair (floor(o*s),
+// min(floor(o*s)+1, n_in-1)) includes i: a contiguous range, found from a
+// generous analytic bracket and then tested with the forward's own float
+// arithmetic, so weights match resize_fwd_k exactly.
+__device__ __forceinline__ void resize_src_range(int i, float s, int n_out, int& lo, int& hi) {
+    if (s <= 0.f) {
+        lo = 0;
+        hi = n_out - 1;
+        return;
+    }
+    lo = max(0, (int)floorf((i - 1) / s) - 1);
+    hi = min(n_out - 1, (int)ceilf((i + 1) / s) + 1);
+}
+
+__device__ __forceinline__ float resize_weight(int o, int i, float s, int n_in) {
+    const float f = o * s;
+    const int a = (int)floorf(f);
+    const int b = min(a + 1, n_in - 1);
+    const float l = f - a;
+    return (a == i ? 1.f - l : 0.f) + (b == i ? l : 0.f);
+}
+
+// Gradient as a gather (deterministic, no atomics): dx[n, y, x, c] =
+// sum over the output rows / columns that read (y, x) of wy * wx * dy.
 template <typename T>
-__global__ void resize_bwd_k(const T* __restrict__ dy, float* __restrict__ dx, int N, int H, int W, int C, int OH, int OW) {
+__global__ __launch_bounds__(256) void resize_bwd_k(const T* __restrict__ dy, float* __restrict__ dx, int N, int H,
+                                                    int W, int C, int OH, int OW) {
     const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
     const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
-    const long total = (long)N * OH * OW * C;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C);
-        long t = i / C;
-        const int ow = (int)(t % OW);
-        t /= OW;
-        const int oh = (int)(t % OH);
-        const int n = (int)(t / OH);
-        const float fy = oh * sh, fx = ow * sw;
-        const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
-        const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
-        const float ly = fy - y0, lx = fx - x0;
-        const float g = to_f32(dy[i]);
-        float* b = dx + (long)n * H * W * C + c;
-        atomicAdd(b + ((long)y0 * W + x0) * C, g * (1.f - ly) * (1.f - lx));
-        atomicAdd(b + ((long)y0 * W + x1) * C, g * (1.f - ly) * lx);
-        atomicAdd(b + ((long)y1 * W + x0) * C, g * ly * (1.f - lx));
-        atomicAdd(b + ((long)y1 * W + x1) * C, g * ly * lx);
+    const int row = blockIdx.x;                   // n * H + y
+    const int n = row / H, yy = row - n * H;
+    int oy_lo, oy_hi;
+    resize_src_range(yy, sh, OH, oy_lo, oy_hi);
+    const int rowlen = W * C;
+    for (int j = blockIdx.y * blockDim.x + threadIdx.x; j < rowlen; j += gridDim.y * blockDim.x) {
+        const int xx = j / C, c = j - (j / C) * C;
+        int ox_lo, ox_hi;
+        resize_src_range(xx, sw, OW, ox_lo, ox_hi);
+        float acc = 0.f;
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const float wy = resize_weight(oy, yy, sh, H);
+            if (wy == 0.f) continue;
+            const T* dr = dy + ((long)n * OH + oy) * OW * C + c;
+            float racc = 0.f;
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const float wx = resize_weight(ox, xx, sw, W);
+                if (wx != 0.f) racc += wx * to_f32(dr[ox * C]);
+            }
+            acc += wy * racc;
+        }
+        dx[(long)row * rowlen + j] = acc;
     }
 }
 
@@ -1229,22 +1265,25 @@ extern "C" int seg_spatial_broadcast(const void* x, void* y, int ldy, int N, int
 
 extern "C" int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
                                        void* stream) {
-    if (!x || !y) return SEG_EINVAL;
-    const long total = (long)N * OH * OW * C;
-    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_fwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
-                                         (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, OH, OW));
+    if (!x || !y || N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return SEG_EINVAL;
+    if ((long)W * C > 0x7fffffffL || (long)OW * C > 0x7fffffffL || (long)N * OH > 0x7fffffffL) return SEG_EINVAL;
+    const int rowlen = OW * C;
+    const dim3 grid((unsigned)(N * OH), (unsigned)std::min((rowlen + 255) / 256, 64));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_fwd_k<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y,
+                                         N, H, W, C, OH, OW));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }
 
 extern "C" int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, int W, int C, int OH, int OW,
                                        int dtype, void* stream) {
-    if (!dy || !dx) return SEG_EINVAL;
+    if (!dy || !dx || N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return SEG_EINVAL;
+    if ((long)W * C > 0x7fffffffL || (long)OW * C > 0x7fffffffL || (long)N * H > 0x7fffffffL) return SEG_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(dx, 0, (size_t)N * H * W * C * sizeof(float), s) != hipSuccess) return SEG_ELAUNCH;
-    const long total = (long)N * OH * OW * C;
-    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s,
-                                         (const T*)dy, dx, N, H, W, C, OH, OW));
+    const int rowlen = W * C;                       // every dx element is written: no memset
+    const dim3 grid((unsigned)(N * H), (unsigned)std::min((rowlen + 255) / 256, 64));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(resize_bwd_k<T>, grid, dim3(256), 0, s, (const T*)dy, dx, N, H, W, C, OH,
+                                         OW));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

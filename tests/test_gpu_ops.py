@@ -511,8 +511,19 @@ def test_prepare_input(dev, dtype, shape):
     assert torch.equal(x.cpu(), ref.to(dtype))
 
 
-def test_resize_bilinear(dev):
-    N, H, W, C, OH, OW = 1, 5, 7, 3, 9, 15
+RESIZE_CASES = [(1, 5, 7, 3, 9, 15),
+                (2, 6, 9, 2, 41, 65),      # x8-style upsample of 2-class logits (DeepLab head)
+                (1, 9, 15, 4, 5, 7),       # downsample
+                (2, 1, 6, 3, 4, 11),       # single source row
+                (1, 4, 5, 2, 1, 1),        # single output pixel
+                (1, 3, 3, 8, 128, 96)]     # large factor, C = 8
+
+
+@pytest.mark.parametrize("case", RESIZE_CASES)
+def test_resize_bilinear(dev, case):
+    """ResizeBilinear(align_corners=True) forward and its gather-form gradient
+    (every source pixel sums the output positions that read it)."""
+    N, H, W, C, OH, OW = case
     g = torch.Generator().manual_seed(17)
     x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).float().double().requires_grad_(True)
     y = tf.resize_bilinear(x, (OH, OW))
