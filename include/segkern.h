@@ -241,6 +241,16 @@ int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* 
                     void* dx, int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
                     float* dbeta, long P, int C, int c_valid, int flags, int dtype, void* ws,
                     size_t ws_bytes, void* stream);
+/* seg_bn_relu_bwd whose x is the output of a conv epilogue with a fused TF1
+ * dropout and no ReLU (Conv2D_Block -> Dropout -> Batch_Normalization,
+ * Network/model/FCDenseNet.py:28-30): dx is additionally multiplied by that
+ * dropout's mask / keep_prob (counter pixel * drop_c_valid + c, as
+ * seg_dropout_bwd_ch), so the conv's separate dropout-gradient pass goes
+ * away.  No accumulation (flags bit 1 must be 0). */
+int seg_bn_relu_dropout_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy,
+                            void* dx, int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
+                            float* dbeta, long P, int C, int c_valid, int flags, float keep_prob, uint64_t seed,
+                            int drop_c_valid, int dtype, void* ws, size_t ws_bytes, void* stream);
 /* resize_bilinear(align_corners=True) (Network/utils/utils.py:329-330). */
 int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int W, int C, int OH, int OW,
                             int dtype, void* stream);

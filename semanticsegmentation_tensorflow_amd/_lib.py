@@ -153,6 +153,8 @@ SIGNATURES = {
     "seg_bn_relu_fwd": (_I, [_P, _I, _P, _I, _P, _P, _F, _L, _I, _I, _I, _I, _P]),
     "seg_bn_relu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _F, _P, _P, _L, _I, _I, _I, _I,
                              _P, _Z, _P]),
+    "seg_bn_relu_dropout_bwd": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _F, _P, _P, _L, _I, _I, _I,
+                                     _F, ctypes.c_uint64, _I, _I, _P, _Z, _P]),
     "seg_resize_bilinear_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_resize_bilinear_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_copy_channels": (_I, [_P, _I, _P, _I, _L, _I, _I, _P]),

@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                                                      const T* __restrict__ dy, int lddy, T* __restrict__ dx, int lddx,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float inv, float* __restrict__ part, long P, int C, int cv,
-                                                     int flags) {
+                                                     int flags, float dkp, uint64_t dseed, int dcv) {
     // ReLU mask from y, or (y == null) re-derived from x with the forward's
     // own arithmetic (x * gamma*inv + beta > 0): 2 bytes per element less
     constexpr int EPC = dt_traits<T>::EPC;
@@ -558,8 +558,10 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
             sc[j][e] = ok ? gamma[c] * inv : 0.f;
             sh[j][e] = ok && remask ? beta[c] : 0.f;
         }
+    const float rdkp = dkp < 1.f ? 1.f / dkp : 1.f;
     if (active) {
         for (long pix = p0 + prow; pix < p1; pix += g.rows) {
+            const uint64_t dbase = (uint64_t)pix * dcv;
 #pragma unroll
             for (int j = 0; j < MAXIT; ++j) {
                 if (j >= g.iters) break;
@@ -580,6 +582,9 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                     sg[j][e] += dz * xv[e];
                     d[e] = dz * sc[j][e];
                     if (acc) d[e] += old[e];
+                    // dropout of the conv epilogue that produced x (no ReLU
+                    // between): its gradient, same counter as the forward draw
+                    if (dkp < 1.f) d[e] = c < dcv ? (d[e] * rdkp) * floorf(dkp + seg_uniform(dseed, dbase + c)) : 0.f;
                 }
                 stc(dx + pix * lddx + cc * EPC, Chunk<T>::pack(d));
             }
@@ -1150,10 +1155,10 @@ extern "C" int seg_bn_relu_fwd(const void* x, int ldx, void* y, int ldy, const f
     return SEG_OK;
 }
 
-extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
-                               int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
-                               float* dbeta, long P, int C, int cv, int flags, int dtype, void* ws, size_t ws_bytes,
-                               void* stream) {
+static int bn_relu_bwd_impl(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
+                            int lddx, const float* gamma, const float* beta, float eps, float* dgamma, float* dbeta,
+                            long P, int C, int cv, int flags, int dtype, void* ws, size_t ws_bytes, void* stream,
+                            float dkp, uint64_t dseed, int dcv) {
     if (!x || !dy || !dx || !gamma || !dgamma || !dbeta || (C & 7) || (flags & ~3)) return SEG_EINVAL;
     if ((flags & 1) && !y && !beta) return SEG_EINVAL;
     if (C > 4096) return SEG_EINVAL;
@@ -1165,11 +1170,32 @@ extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, c
     if (shm > 64 * 1024) return SEG_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     DISPATCH_T(dtype, hipLaunchKernelGGL(bn_relu_bwd_k<T>, dim3(nb), dim3(256), shm, s, (const T*)x, ldx, (const T*)y,
-                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, beta, inv, (float*)ws, P, C, cv, flags));
+                                         ldy, (const T*)dy, lddy, (T*)dx, lddx, gamma, beta, inv, (float*)ws, P, C, cv, flags,
+                                         dkp, dseed, dcv));
     SEG_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_finish_k, dim3((cv + 7) / 8), dim3(256), 0, s, (const float*)ws, nb, C, cv, inv, dgamma, dbeta);
     SEG_CHECK_LAUNCH();
     return SEG_OK;
+}
+
+extern "C" int seg_bn_relu_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy, void* dx,
+                               int lddx, const float* gamma, const float* beta, float eps, float* dgamma,
+                               float* dbeta, long P, int C, int cv, int flags, int dtype, void* ws, size_t ws_bytes,
+                               void* stream) {
+    return bn_relu_bwd_impl(x, ldx, y, ldy, dy, lddy, dx, lddx, gamma, beta, eps, dgamma, dbeta, P, C, cv, flags,
+                            dtype, ws, ws_bytes, stream, 1.f, 0, 0);
+}
+
+extern "C" int seg_bn_relu_dropout_bwd(const void* x, int ldx, const void* y, int ldy, const void* dy, int lddy,
+                                       void* dx, int lddx, const float* gamma, const float* beta, float eps,
+                                       float* dgamma, float* dbeta, long P, int C, int cv, int flags,
+                                       float keep_prob, uint64_t seed, int drop_c_valid, int dtype, void* ws,
+                                       size_t ws_bytes, void* stream) {
+    // the dropout gradient applies to this BN's contribution alone: no accumulation
+    if ((flags & 2) || !(keep_prob > 0.f && keep_prob <= 1.f) || drop_c_valid <= 0 || drop_c_valid > C)
+        return SEG_EINVAL;
+    return bn_relu_bwd_impl(x, ldx, y, ldy, dy, lddy, dx, lddx, gamma, beta, eps, dgamma, dbeta, P, C, cv, flags,
+                            dtype, ws, ws_bytes, stream, keep_prob, seed, drop_c_valid);
 }
 
 // ---------------------------------------------------------------------------

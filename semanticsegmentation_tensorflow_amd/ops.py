@@ -389,14 +389,24 @@ def bn_relu_fwd(x, y, gamma, beta, c_valid, relu=True, eps=1e-3, stream=None):
 
 
 def bn_relu_bwd(x, y, dy, dx, gamma, dgamma, dbeta, c_valid, relu=True, eps=1e-3, ws=None,
-                stream=None, accumulate=False, beta=None):
+                stream=None, accumulate=False, beta=None, dropout=None):
     """accumulate: dx += the input gradient (dx a slice of a shared concat
     gradient buffer) instead of dx = ...; beta given: the ReLU mask comes from
-    x (the forward's arithmetic) and y is not read."""
+    x (the forward's arithmetic) and y is not read.  dropout = (keep_prob,
+    seed, c_valid) of the conv epilogue that produced x: dx also carries that
+    dropout's gradient (seg_bn_relu_dropout_bwd)."""
     N, H, W, C = x.shape
     P = N * H * W
     wsp, wss = (ws or Workspace(x.device)).ptr_size(1024 * 2 * C * 4)
     yp, ldy = (None, 0) if (beta is not None or y is None) else (ptr(y), pixel_stride(y))
+    if dropout is not None:
+        kp, seed, dcv = dropout
+        check(_lib.lib().seg_bn_relu_dropout_bwd(
+            ptr(x), pixel_stride(x), yp, ldy, ptr(dy), pixel_stride(dy), ptr(dx), pixel_stride(dx), ptr(gamma),
+            None if beta is None else ptr(beta), float(eps), ptr(dgamma), ptr(dbeta), P, C, c_valid,
+            (1 if relu else 0) | (2 if accumulate else 0), float(kp), int(seed) & (2 ** 64 - 1), int(dcv),
+            seg_dtype(x), wsp, wss, stream_ptr(stream)), "batch_norm_grad")
+        return dx
     check(_lib.lib().seg_bn_relu_bwd(ptr(x), pixel_stride(x), yp, ldy, ptr(dy),
                                      pixel_stride(dy), ptr(dx), pixel_stride(dx), ptr(gamma),
                                      None if beta is None else ptr(beta), float(eps), ptr(dgamma), ptr(dbeta), P, C, c_valid,

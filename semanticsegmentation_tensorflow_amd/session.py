@@ -190,6 +190,7 @@ class Session:
         self.alias_concat = True
         # BatchNorm(+ReLU) feeding a single 1x1 conv folded into its operand prologue
         self.fold_bn = True
+        self.fold_dropout_grad = True   # Conv -> Dropout -> BN: the dropout gradient inside the BN backward
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -498,6 +499,7 @@ class Session:
                 raise NotImplementedError(f"op {t} is not on the hot path")
         p.nodes = nodes
         self._fold_bn_prologues(p, fetched)
+        self._fold_dropout_grads(p, fetched)
         self._allocate(p, consumers, feeds)
         return p
 
@@ -528,6 +530,34 @@ class Session:
                 continue
             c.pro = b
             p.folded.add(id(b))
+
+    def _fold_dropout_grads(self, p, fetched):
+        """Conv2D_Block -> Dropout -> Batch_Normalization (FC-DenseNet's
+        bottleneck conv1, Network/model/FCDenseNet.py:28-30): the dropout sits
+        in the conv's forward epilogue with no ReLU, so its gradient is a
+        re-draw of the mask; when the BN is the conv output's only reader, the
+        BN backward applies it (seg_bn_relu_dropout_bwd) and the conv's own
+        dropout-gradient pass is skipped.  p.drop_fold: bn node id -> conv."""
+        p.drop_fold = {}
+        p.drop_folded = set()
+        if not self.fold_dropout_grad:
+            return
+        users = {}
+        for n in p.nodes:
+            for t in list(n.inputs) + [getattr(n, "residual", None)]:
+                if t is not None:
+                    users.setdefault(id(t), []).append(n)
+        for c in p.nodes:
+            if c.kind != "conv" or c.relu or getattr(c, "kp", None) is None:
+                continue
+            out = c.output
+            if id(out) in fetched:
+                continue
+            us = users.get(id(out), [])
+            if len(us) != 1 or us[0].kind != "bn" or us[0].inputs[0] is not out:
+                continue
+            p.drop_fold[id(us[0])] = c
+            p.drop_folded.add(id(c))
 
     def _infer(self, op, shp):
         t = op.type
@@ -1205,7 +1235,7 @@ class Session:
                 yb = buf[id(n.output)]
                 dz = dy
                 fused_db = None
-                if not n.relu and n.kp_val is not None and n.kp_val < 1.0:
+                if not n.relu and n.kp_val is not None and n.kp_val < 1.0 and id(n) not in p.drop_folded:
                     # dropout applied in the forward epilogue, no ReLU: re-draw its mask
                     dz = p.tmp.get(("dz", id(n.output)))
                     if dz is None:
@@ -1349,9 +1379,15 @@ class Session:
                     acc = None
                 else:
                     (dx, acc), accf = dest(x), False
+                drop = None
+                c = p.drop_fold.get(id(n))
+                if c is not None and c.kp_val is not None and c.kp_val < 1.0:
+                    if accf or acc is not None:
+                        raise RuntimeError(f"{n.ops[0].name}: folded dropout gradient needs a sole reader")
+                    drop = (c.kp_val, c.seed_val, c.desc.k_valid)
                 ops.bn_relu_bwd(buf[id(x)], buf[id(n.output)], dy, dx, store.param(n.gamma.var_name),
                                 store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
-                                n.eps, ws, accumulate=accf, beta=store.param(n.beta.var_name))
+                                n.eps, ws, accumulate=accf, beta=store.param(n.beta.var_name), dropout=drop)
                 done(dx, acc)
                 self._grad_ready([n.gamma.var_name, n.beta.var_name])
             elif k == "Relu":

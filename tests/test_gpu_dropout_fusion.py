@@ -71,3 +71,61 @@ def test_conv_dropout_grads(dev, fuse):
     for got, ref, nm in ((gw1, w1r.grad, "w1"), (gw2, w2r.grad, "w2")):
         err = (got - ref).abs().max().item() / ref.abs().max().item()
         assert err < 2e-4, (nm, err)
+
+
+@pytest.mark.parametrize("fold", [True, False], ids=["in-bn-backward", "separate-pass"])
+def test_conv_dropout_bn_relu_grads(dev, fold):
+    """Conv2D_Block -> Dropout -> Batch_Normalization -> ReLU -> conv
+    (FC-DenseNet bottleneck, Network/model/FCDenseNet.py:27-33): the dropout's
+    gradient folded into the BN backward (seg_bn_relu_dropout_bwd) or run as
+    its own pass, vs float64 with the same mask."""
+    from semanticsegmentation_tensorflow_amd.layers import Batch_Normalization, ReLU
+    N, H, W, C, K, kp = 2, 6, 7, 8, 16, 0.6
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [N, H, W, C], name="x")
+    labels = tf.placeholder(tf.uint8, [N, H, W], name="y")
+    keep = tf.placeholder(tf.float32, name="keep")
+    h = Dropout(Conv2D_Layer(image, K, 1, 1, name="c1"), keep_prob=keep)
+    r = ReLU(Batch_Normalization(h))
+    logits = Conv2D_Layer(r, 2, 3, 3, name="c2")
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train = tf.train.AdamOptimizer(1e-3).minimize(loss)
+    sess = tf.Session(compute_dtype="f32")
+    sess.fold_dropout_grad = fold
+    sess.store_fused_grads = True
+    sess.run(tf.global_variables_initializer())
+    names = [v.var_name for v in tf.trainable_variables()]
+    gname = next(n for n in names if n.endswith("gamma"))
+    bname = next(n for n in names if n.endswith("beta"))
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    y = torch.randint(0, 2, (N, H, W), generator=g).to(torch.uint8)
+    w1 = (torch.randn(1, 1, C, K, generator=g, dtype=torch.float64) * 0.3).float()
+    w2 = (torch.randn(3, 3, K, 2, generator=g, dtype=torch.float64) * 0.2).float()
+    gam = (1 + 0.2 * torch.randn(K, generator=g, dtype=torch.float64)).float()
+    bet = (0.1 * torch.randn(K, generator=g, dtype=torch.float64)).float()
+    for nm, v in (("c1/weights", w1), ("c2/weights", w2), (gname, gam), (bname, bet)):
+        sess.assign(nm, v.numpy())
+    feed = {image: x.float().numpy(), labels: y.numpy(), keep: kp}
+    _, lv = sess.run([train, loss], feed_dict=feed)
+    plan = list(sess.plans.values())[-1]
+    assert bool(plan.drop_fold) == fold
+    node = next(n for n in plan.nodes if n.kind == "conv" and n.kp is not None)
+    P = N * H * W
+    u = np.array([[_np_uniform(node.seed_val, p * K + c) for c in range(K)] for p in range(P)], np.float32)
+    mask = torch.from_numpy(np.floor(np.float32(kp) + u).astype(np.float64)).view(N, H, W, K)
+    w1r, w2r = w1.double().requires_grad_(True), w2.double().requires_grad_(True)
+    gr, br = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    hr = tf_ref.conv2d(x, w1r, 1, "SAME", 1) / kp * mask
+    rr = torch.relu(tf_ref.batch_norm_frozen(hr, gr, br))
+    lr = tf_ref.conv2d(rr, w2r, 1, "SAME", 1)
+    onehot = torch.nn.functional.one_hot(y.long(), 2).double()
+    ref_loss = -(onehot * torch.log_softmax(lr, dim=-1)).sum(-1).mean()
+    ref_loss.backward()
+    assert abs(float(lv) - ref_loss.item()) <= 1e-5 * abs(ref_loss.item())
+    got = {"w1": sess.store.grad("c1/weights").cpu().double().view(1, 1, C, K),
+           "w2": sess.store.grad("c2/weights").cpu().double().view(3, 3, K, 2),
+           "gamma": sess.store.grad(gname).cpu().double(), "beta": sess.store.grad(bname).cpu().double()}
+    for nm, ref in (("w1", w1r.grad), ("w2", w2r.grad), ("gamma", gr.grad), ("beta", br.grad)):
+        err = (got[nm] - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-4, (nm, err)

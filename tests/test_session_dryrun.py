@@ -164,7 +164,12 @@ def test_fcdensenet_train_plan(dry):
     assert c.count("seg_tconv2d_fwd") == 5
     assert c.count("seg_concat_fwd") == 5 * 1 + (12 + 1) + (15 + 1)
     assert c.count("seg_concat_bwd") == c.count("seg_concat_fwd")
-    assert c.count("seg_bn_relu_fwd") == 123 - n_fold and c.count("seg_bn_relu_bwd") == 123
+    assert c.count("seg_bn_relu_fwd") == 123 - n_fold
+    # the 59 bottleneck conv1 -> Dropout -> BN chains: the dropout gradient
+    # rides in the BN backward; only the growth convs' dropouts keep a pass
+    assert c.count("seg_bn_relu_bwd") + c.count("seg_bn_relu_dropout_bwd") == 123
+    assert c.count("seg_bn_relu_dropout_bwd") == 59
+    assert c.count("seg_dropout_bwd_ch") == 59
     assert c.count("seg_avgpool2x2_fwd") == 5
     assert c.count("seg_conv2d_bwd_filter") + c.count("seg_conv2d_bwd_filter_pro") == 125
     assert c.count("seg_conv2d_bwd_filter_pro") == n_fold
