@@ -39,6 +39,7 @@ int g_halo_wide = 1;
 int g_halo_stagger = 1;
 int g_halo_phases = 2;
 int g_res64 = 1;
+int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
 
 struct HaloGeom {
@@ -608,11 +609,16 @@ constexpr int R64_BH = 8, R64_BW = 32, R64_HW = R64_BW + 2, R64_HROWS = (R64_BH 
 constexpr int R64_PER = (R64_HROWS * 8 + 511) / 512;                                             // 6
 
 // ABL (diagnostics only, garbage results): 1 no halo fetch, 2 no MFMA,
-// 3 no epilogue stores, 4 no LDS fragment reads
-template <int ABL = 0, typename T = bf16>
-__global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int tiles_y, int ntiles) {
-    constexpr int NW = 8, WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2;
-    constexpr int BS = 9 * 64 * 128;                 // resident filter
+// 3 no epilogue stores, 4 no LDS fragment reads.
+// NB = output channels per block: 64, or 16 for N <= 16 (FC-DenseNet's
+// growth convs, 64 -> 16): one 16-row filter fragment, all 8 waves along the
+// pixels, a quarter of the MFMAs and a 18 KB filter, so two blocks share a CU.
+template <int ABL = 0, typename T = bf16, int NB = 64>
+__global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+    static_assert(NB == 64 || NB == 16, "output block width");
+    constexpr int NW = 8, WN = NB == 64 ? 2 : 1, WTM = 256 / (NW / WN), WTN = NB / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int BS = 9 * NB * 128;                 // resident filter
     constexpr int HS = R64_HROWS * 128;              // halo
     __shared__ __attribute__((aligned(16))) char smem[BS + HS];
     char* Bs = smem;
@@ -628,15 +634,15 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
     const int tpi = tiles_x * tiles_y;
 
     // ---- filter: Bs[tap][n][chunk ^ swz(n)]
-    for (int i = tid; i < 9 * 64 * 8; i += 512) {
-        const int c8 = i & 7, n = (i >> 3) & 63, tap = i >> 9;
+    for (int i = tid; i < 9 * NB * 8; i += 512) {
+        const int c8 = i & 7, n = (i >> 3) % NB, tap = i / (NB * 8);
         const int j = tap / 3, ii = tap - (tap / 3) * 3;
         uint4 v = {0u, 0u, 0u, 0u};
         if (n < p.N)
             v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col +
                                                 (long)((p.rb + p.rstep * j) * p.Sfull + (p.sb + p.sstep * ii)) * p.w_tap +
                                                 c8 * 8);
-        *reinterpret_cast<uint4*>(Bs + (tap * 64 + n) * 128 + 16 * (c8 ^ (n & 6))) = v;
+        *reinterpret_cast<uint4*>(Bs + (tap * NB + n) * 128 + 16 * (c8 ^ (n & 6))) = v;
     }
     // ---- halo fetch into registers: slot q -> (row q / 8, chunk q % 8)
     uint4 hv[R64_PER];
@@ -718,7 +724,7 @@ __global__ __launch_bounds__(512) void conv_res64(NTParams p, int tiles_x, int t
                 for (int ni = 0; ni < TN; ++ni) b[ni] = uint4{(unsigned)chunk, (unsigned)ni, 1u, 0u};
                 return;
             }
-            const char* Bt = Bs + tap * 64 * 128;
+            const char* Bt = Bs + tap * NB * 128;
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 const int row = rowbase[mi] + toff[tap];
@@ -903,6 +909,14 @@ bool res64_ok(const NTParams& p, int dtype) {
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
+    if (p.N <= 16 && g_res16) {               // two blocks per CU
+        const int grid = std::min(ntiles, 2 * cus);
+        if (dtype == SEG_F16)
+            hipLaunchKernelGGL((conv_res64<0, f16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        else
+            hipLaunchKernelGGL((conv_res64<0, bf16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        return;
+    }
     const int grid = std::min(ntiles, cus);
     if (dtype == SEG_F16) {
         hipLaunchKernelGGL((conv_res64<0, f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);

@@ -813,7 +813,7 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
     choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
     if (nphases > 1) *splits = 1;
     if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dtype)) {
-        *bn = 64; *splits = 1;
+        *bn = (p.N <= 16 && g_res16) ? 16 : 64; *splits = 1;
         return "conv_res64";
     }
     HaloPlan hp;
