@@ -34,6 +34,7 @@ int g_wgrad_halo = 1;
 int g_wgrad_nt = 128;
 int g_wgrad_la = 3;   // 1: per-read index arithmetic, 2: flat 36-step pipeline (spills), 3: packed per-lane offsets
 int g_wgrad_abl = 0;
+int g_wgrad_nt32 = 1;     // 32-wide dy tiles for N <= 32
 int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
 
 struct WGGeom {
@@ -45,6 +46,7 @@ struct WGGeom {
 template <int ROWB>
 __device__ __forceinline__ int wg_swz(int row) {
     if constexpr (ROWB >= 256) return ((row & 3) << 1) | (((row >> 3) & 1) << 3);
+    else if constexpr (ROWB == 64) return 0;     // 4-chunk dy rows (NT = 32): unswizzled
     else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
 }
 
@@ -98,6 +100,7 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     const int dr = lane / D_CPR, dpc = lane % D_CPR;
     int dc;
     if constexpr (DROWB >= 256) dc = dpc ^ (((dr & 3) << 1) | (((w >> 1) & 1) << 3));
+    else if constexpr (DROWB == 64) dc = dpc;
     else dc = dpc ^ ((((dr >> 1) & 1) << 1) | ((w & 1) << 2));
     const bool d_nok = n0 + dc * 8 < p.N;
 
@@ -432,6 +435,9 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     if (best < 0) return false;
     // 128-wide dy tiles (2 LDS stages, 4 halo pieces) when N allows and the halo fits
     wp->nt = (g_wgrad_nt == 128 && p.N > 64 && wp->g[4] <= 4 * 64) ? 128 : 64;
+    // <= 32 output channels (FC-DenseNet growth convs, 64 -> 16): 32-wide dy
+    // tiles instead of padding to 64 (half the MFMAs, a quarter of the dy LDS)
+    if (g_wgrad_nt32 && p.N <= 32 && g_wgrad_la == 3 && wp->bw == 16) wp->nt = 32;
     wp->g[2] = nimg;
     const int nct = p.Cg / 64, nnt = (p.N + wp->nt - 1) / wp->nt;
     const int nout = nct * nnt;
@@ -472,6 +478,16 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
     }
     if (g_wgrad_la == 2 && wp.nt == 128 && wp.bw == 16) {
         hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 2>), grid, block, 0, s, p, g);
+        return;
+    }
+    if (wp.nt == 32) {                        // wgrad_plan: la == 3, bw == 16
+        if (dtype == SEG_F16) {
+            if (small) hipLaunchKernelGGL((wgrad_halo<16, 32, 3, 4, 3, 0, f16>), grid, block, 0, s, p, g);
+            else hipLaunchKernelGGL((wgrad_halo<16, 32, 2, 5, 3, 0, f16>), grid, block, 0, s, p, g);
+        } else {
+            if (small) hipLaunchKernelGGL((wgrad_halo<16, 32, 3, 4, 3>), grid, block, 0, s, p, g);
+            else hipLaunchKernelGGL((wgrad_halo<16, 32, 2, 5, 3>), grid, block, 0, s, p, g);
+        }
         return;
     }
     if (dtype == SEG_F16) {                   // wgrad_plan: la == 3, bw == 16
