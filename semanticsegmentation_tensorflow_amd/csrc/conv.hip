@@ -575,6 +575,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_wgrad_nt32 = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "res16c")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_res16c = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "res16")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_res16 = value;

@@ -40,6 +40,7 @@ int g_halo_stagger = 1;
 int g_halo_phases = 2;
 int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
+int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
 
 struct HaloGeom {
@@ -807,6 +808,185 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
 }
 
 // ---------------------------------------------------------------------------
+// Resident-filter direct conv for 16 input channels: the input gradient of
+// FC-DenseNet's 64 -> 16 growth convs (dz: 16 channels, dx: 64), which the
+// implicit GEMM ran at ~1.7 TB/s.  One v_mfma_f32_16x16x32 k-step covers two
+// taps x 16 channels, so the 9 taps take 5 steps (tap 8 pairs with a zero
+// filter tap).  Filter [5 steps][64 n][64 B] = 20 KB and the 10 x 34 px halo
+// of 32-byte rows (10.9 KB) stay in LDS; tiles, prefetch and epilogue as
+// conv_res64.  Swizzles: filter rows chunk ^ ((n >> 2) & 3), halo rows
+// chunk ^ ((row >> 3) & 1).
+// ---------------------------------------------------------------------------
+constexpr int R16_PER = (R64_HROWS * 2 + 511) / 512;   // halo chunks per thread (2)
+
+template <typename T = bf16>
+__global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+    constexpr int WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2, KS = 5;
+    constexpr int BS = KS * 64 * 64;
+    constexpr int HS = R64_HROWS * 32;
+    __shared__ __attribute__((aligned(16))) char smem[BS + HS];
+    char* Bs = smem;
+    char* Hs = smem + BS;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const int fr = lane & 15, fg = lane >> 4;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const int hy0 = p.tsh < 0 ? 2 * p.tsh : 0, hx0 = p.tsw < 0 ? 2 * p.tsw : 0;
+    const int tpi = tiles_x * tiles_y;
+
+    // ---- filter: Bs[ks][n][q ^ swz(n)], chunk q = (tap 2ks + (q >> 1), channels 8 (q & 1)..)
+    for (int i = tid; i < KS * 64 * 4; i += 512) {
+        const int q = i & 3, n = (i >> 2) & 63, ks = i >> 8;
+        const int tap = 2 * ks + (q >> 1), c8 = q & 1;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (n < p.N && tap < 9) {
+            const int j = tap / 3, ii = tap - (tap / 3) * 3;
+            v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col +
+                                                (long)((p.rb + p.rstep * j) * p.Sfull + (p.sb + p.sstep * ii)) * p.w_tap +
+                                                c8 * 8);
+        }
+        *reinterpret_cast<uint4*>(Bs + (ks * 64 + n) * 64 + 16 * (q ^ ((n >> 2) & 3))) = v;
+    }
+    // ---- halo fetch into registers: slot q -> (row q / 2, chunk q % 2)
+    uint4 hv[R16_PER];
+    auto fetch = [&](int t) {
+        const int img = t / tpi;
+        const int rem = t - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+        const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+#pragma unroll
+        for (int k = 0; k < R16_PER; ++k) {
+            const int q = tid + k * 512;
+            const int hr = q >> 1, c8 = q & 1;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (hr < R64_HROWS) {
+                const int hy = hr / R64_HW, hx = hr - (hr / R64_HW) * R64_HW;
+                const int ih = oy0 + p.ioh + hy0 + hy, iw = ox0 + p.iow + hx0 + hx;
+                if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW)
+                    v = *reinterpret_cast<const uint4*>(X + (long)img * p.x_img + ((long)ih * p.IW + iw) * p.ldx + c8 * 8);
+            }
+            hv[k] = v;
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int k = 0; k < R16_PER; ++k) {
+            const int q = tid + k * 512;
+            const int hr = q >> 1, c8 = q & 1;
+            if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 32 + 16 * (c8 ^ ((hr >> 3) & 1))) = hv[k];
+        }
+    };
+
+    int rowbase[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+        const int ml = wm * WTM + mi * 16;
+        rowbase[mi] = (ml / R64_BW) * R64_HW + (ml % R64_BW) + fr;
+    }
+    int toff[9];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) toff[tap] = ((tap / 3) * p.tsh - hy0) * R64_HW + (tap % 3) * p.tsw - hx0;
+
+    const EpiParams& e = p.epi;
+    float bias[TN][4], scl[TN][4], shf[TN][4];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = wn * WTN + ni * 16 + 4 * fg + j;
+            const bool cv = col < e.n_valid;
+            bias[ni][j] = (e.bias && cv) ? e.bias[col] : 0.f;
+            scl[ni][j] = (e.scale && cv) ? e.scale[col] : 1.f;
+            shf[ni][j] = (e.shift && cv) ? e.shift[col] : 0.f;
+        }
+
+    int t = blockIdx.x;
+    if (t < ntiles) fetch(t);
+    commit();
+    __syncthreads();
+    const int hi_tap = fg >> 1, ach = fg & 1;
+    for (; t < ntiles; t += gridDim.x) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fetch(tn);                  // in flight during this tile's MFMAs
+        f32x4 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            // this lane's k group reads tap 2ks (groups 0, 1) or 2ks + 1 (2, 3)
+            const int to = hi_tap ? toff[ks * 2 + 1 < 9 ? ks * 2 + 1 : 8] : toff[ks * 2];
+            uint4 fa[TM], fb[TN];
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int row = rowbase[mi] + to;
+                fa[mi] = *reinterpret_cast<const uint4*>(Hs + row * 32 + 16 * (ach ^ ((row >> 3) & 1)));
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int n = wn * WTN + ni * 16 + fr;
+                fb[ni] = *reinterpret_cast<const uint4*>(Bs + (ks * 64 + n) * 64 + 16 * (fg ^ ((n >> 2) & 3)));
+            }
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)   // D^T[n][px] += W[n][k] X[px][k]
+                    acc[mi][ni] = mfma16x16x32<T>(fb[ni], fa[mi], acc[mi][ni]);
+        }
+        {
+            const int img = t / tpi;
+            const int rem = t - img * tpi;
+            const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+            const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int ml = wm * WTM + mi * 16 + fr;
+                const int oy = oy0 + ml / R64_BW, ox = ox0 + ml % R64_BW;
+                if (oy >= p.OH || ox >= p.OW) continue;
+                const long pix = (long)oy * p.OW + ox;
+                const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col0 = wn * WTN + ni * 16 + 4 * fg;
+                    if (col0 >= p.N) continue;
+                    float mk[4] = {1.f, 1.f, 1.f, 1.f}, res[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (e.mask) {
+                        const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) mk[j] = to_f32(mp[j]);
+                    }
+                    if (e.residual) {
+                        const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) res[j] = to_f32(rp[j]);
+                    }
+                    T o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int col = col0 + j;
+                        float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
+                        if (e.relu) x = fmaxf(x, 0.f);
+                        if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                        x += res[j];
+                        if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                        o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+                    }
+                    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
+                        *reinterpret_cast<const uint2*>(o);
+                }
+            }
+        }
+        __syncthreads();                             // all steps read the halo
+        commit();                                    // next tile's halo (waits for its loads)
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static constexpr int kHaloBW[3] = {16, 32, 64};
@@ -897,6 +1077,22 @@ template <int BW, int HI>
 static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s, int dtype) {
     if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s, dtype);
     else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s, dtype);
+}
+
+bool res16c_ok(const NTParams& p, int dtype) {
+    return g_res16c && g_nt_halo && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.ish == 1 &&
+           p.isw == 1 && p.osh == 1 && p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.Ha == p.OH && p.Wa == p.OW &&
+           p.C == 16 && p.K == 9 * 16 && p.taps_w == 3 && (p.tsh == 1 || p.tsh == -1) &&
+           (p.tsw == 1 || p.tsw == -1) && p.N <= 64 && p.N % 8 == 0 && p.ldx % 8 == 0 && p.OH > 0 && p.OW > 0 &&
+           p.M % (p.OH * p.OW) == 0;
+}
+
+void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype) {
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
+    const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
+    const int grid = std::min(ntiles, 2 * cus);
+    if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res16c<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    else hipLaunchKernelGGL((conv_res16c<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
 }
 
 bool res64_ok(const NTParams& p, int dtype) {

@@ -211,6 +211,9 @@ bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* 
 void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype = SEG_BF16);
 extern int g_res64;
 extern int g_res16;
+extern int g_res16c;
+bool res16c_ok(const NTParams& p, int dtype);
+void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
 extern int g_halo2_n128;
 bool res64_ok(const NTParams& p, int dtype);
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);

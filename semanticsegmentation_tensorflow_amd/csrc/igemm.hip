@@ -750,6 +750,11 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         }
         return SEG_OK;
     }
+    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res16c_ok(p, dt_traits<T>::id)) {
+        launch_res16c(p, num_cus(), s, dt_traits<T>::id);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dt_traits<T>::id)) {
         launch_res64(p, num_cus(), s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
@@ -812,6 +817,10 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
     const int bk = dtype == SEG_F32 ? 32 : 64;
     choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
     if (nphases > 1) *splits = 1;
+    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res16c_ok(p, dtype)) {
+        *bm = 256; *bn = 64; *splits = 1;
+        return "conv_res16c";
+    }
     if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dtype)) {
         *bn = (p.N <= 16 && g_res16) ? 16 : 64; *splits = 1;
         return "conv_res64";

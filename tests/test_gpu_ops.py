@@ -80,6 +80,8 @@ CONV_CASES = [
     (2, 19, 131, 3, 48, 3, 3, 1, 1, "SAME"),    # first-layer kernel (C=3->8): ragged 8x64 tiles, K=48
     (1, 17, 70, 64, 48, 3, 3, 1, 1, "VALID"),   # resident-filter kernel: VALID, N=48 < 64
     (2, 21, 67, 64, 16, 3, 3, 1, 1, "SAME"),    # resident-filter kernel, FC-DenseNet growth conv (K=16)
+    (2, 19, 37, 16, 64, 3, 3, 1, 1, "SAME"),    # 16 input channels (conv_res16c; = the growth conv's dgrad)
+    (1, 11, 70, 16, 40, 3, 3, 1, 1, "VALID"),   # conv_res16c: VALID, N = 40 < 64
     # 256x256-tile GEMM (N > 128): K tiles straddling taps, N tail, split-K
     (1, 5, 7, 40, 264, 7, 7, 1, 1, "SAME"),     # conv6-like, C=40: a 64-deep K tile spans taps
     (2, 6, 9, 512, 512, 1, 1, 1, 1, "SAME"),    # conv7-like 1x1
