@@ -122,6 +122,28 @@ int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const seg_prologue
 int seg_conv2d_bwd_filter_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro,
                               const void* dy, float* dw, float* dbias, void* ws, size_t ws_bytes,
                               void* stream);
+/* Conv2DBackpropInput of a 1x1 stride-1 conv over relu(BN(x)) (the BN folded
+ * into the forward's operand prologue), carried through the BatchNorm(+ReLU)
+ * backward in the same launch (FCDenseNet.py:25-28 backward): the ReLU mask
+ * is re-derived from x, dx = dL/dx of the BN input (accumulate != 0: added
+ * into dx, e.g. a slice of a shared concat gradient), dgamma / dbeta (fp32,
+ * overwritten) from per-tile column sums.  bf16 / fp16 only; workspace from
+ * seg_conv_bwd_data_bn_workspace, which returns 0 when the fused path does
+ * not apply (then use seg_conv2d_bwd_data + seg_bn_relu_bwd). */
+typedef struct seg_bn_bwd {
+    const void* x;          /* BN input, pixel stride ldx */
+    int ldx;
+    const float* gamma;
+    const float* beta;
+    float eps;
+    int relu;
+    int accumulate;
+    float* dgamma;
+    float* dbeta;
+} seg_bn_bwd;
+size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d);
+int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_bn_bwd* bn,
+                           void* dx, void* ws, size_t ws_bytes, void* stream);
 int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,
                         const seg_epilogue* epi, void* dx, void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropFilter: dw_f32 is the fp32 master-gradient layout

@@ -101,6 +101,12 @@ class SegPrologue(ctypes.Structure):
                 ("relu", ctypes.c_int)]
 
 
+class SegBnBwd(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("ldx", ctypes.c_int), ("gamma", ctypes.c_void_p),
+                ("beta", ctypes.c_void_p), ("eps", ctypes.c_float), ("relu", ctypes.c_int),
+                ("accumulate", ctypes.c_int), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p)]
+
+
 class SegAdamFused(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
                 ("rows_dst", ctypes.c_void_p), ("rows_ap", ctypes.c_int), ("rows_bp", ctypes.c_int),
@@ -124,6 +130,8 @@ SIGNATURES = {
     "seg_conv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_conv2d_fwd_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv_bwd_data_bn_workspace": (_Z, [_DP]),
+    "seg_conv2d_bwd_data_bn": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _Z, _P]),
     "seg_conv2d_bwd_filter_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _P, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),

@@ -725,6 +725,56 @@ extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Conv2DBackpropInput of a 1x1 conv whose input is relu(BN(x)) with the BN
+// folded into its operand prologue, continued through the BatchNorm(+ReLU)
+// backward in the GEMM epilogue: dx = dL/dx of the BN input (optionally
+// accumulated in place), dgamma / dbeta from per-tile column sums.  16-bit
+// igemm_nt2 only (seg_conv_bwd_data_bn_workspace returns 0 where it does not
+// apply).
+static bool bwd_data_bn_params(const seg_conv_desc* d, NTParams& p) {
+    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return false;
+    if (d->R != 1 || d->S != 1 || d->stride_h != 1 || d->stride_w != 1 || d->C % 8) return false;
+    p = conv_bwd_data_params(d);
+    if (d->K > 64 * 8) return false;                  // the short-K igemm_nt2 (no split-K)
+    return true;
+}
+
+extern "C" size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d) {
+    NTParams p;
+    if (!bwd_data_bn_params(d, p)) return 0;
+    const long tiles_m = (p.M + 255) / 256;
+    return (size_t)tiles_m * 2 * d->C * sizeof(float) + seg::bn_grad_finish_scratch(d->C);
+}
+
+extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w, const seg_bn_bwd* bn,
+                                      void* dx, void* ws, size_t ws_bytes, void* stream) {
+    NTParams p;
+    if (!bwd_data_bn_params(d, p)) return SEG_EINVAL;
+    if (!dy || !w || !dx || !bn || !bn->x || !bn->gamma || !bn->beta || !bn->dgamma || !bn->dbeta) return SEG_EINVAL;
+    if (bn->ldx % 8 || bn->ldx < d->C) return SEG_EINVAL;
+    const size_t need = seg_conv_bwd_data_bn_workspace(d);
+    if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
+    const long tiles_m = (p.M + 255) / 256;
+    float* part = reinterpret_cast<float*>(ws);
+    float* scratch = part + tiles_m * 2 * d->C;
+    p.x = dy; p.w = w; p.y = dx;
+    const float inv = 1.0f / sqrtf(1.0f + bn->eps);
+    seg::EpiParams& e = p.epi;
+    e.n_valid = d->C;
+    e.keep_prob = 1.f;
+    e.mask_scale = 1.f;
+    if (bn->accumulate) {                             // dx += ... (concat gradient slice)
+        e.residual = dx; e.ld_res = d->ldx; e.res_img = (long)d->H * d->W * d->ldx;
+    }
+    e.bn_x = bn->x; e.ld_bn_x = bn->ldx; e.bn_x_img = (long)d->H * d->W * bn->ldx;
+    e.bn_gamma = bn->gamma; e.bn_beta = bn->beta; e.bn_inv = inv; e.bn_relu = bn->relu ? 1 : 0;
+    e.bn_cv = d->c_valid; e.bn_part = part; e.bn_C = d->C;
+    hipStream_t s = (hipStream_t)stream;
+    seg::launch_nt2_bn(p, d->dtype, s);
+    SEG_CHECK_LAUNCH();
+    return seg::bn_grad_finish(part, (int)tiles_m, d->C, d->c_valid, inv, bn->dgamma, bn->dbeta, scratch, s);
+}
+
 extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias,
                                      void* ws, size_t ws_bytes, void* stream) {
     int st = check_desc(d);

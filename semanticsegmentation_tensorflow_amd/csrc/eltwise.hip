@@ -636,6 +636,17 @@ __global__ __launch_bounds__(256) void bn_finish_k(const float* __restrict__ par
     }
 }
 
+// per-tile partial rows [nrows][width] -> [groups][width]: rows r = g, g + groups, ...
+__global__ __launch_bounds__(256) void part_rows_reduce_k(const float* __restrict__ part, int nrows, int width,
+                                                          float* __restrict__ out, int groups) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int gi = blockIdx.y;
+    if (c >= width) return;
+    float s = 0.f;
+    for (int r = gi; r < nrows; r += groups) s += part[(long)r * width + c];
+    out[(long)gi * width + c] = s;
+}
+
 // ---------------------------------------------------------------------------
 // resize_bilinear(align_corners=True)
 // ---------------------------------------------------------------------------
@@ -1406,3 +1417,29 @@ extern "C" const char* seg_status_string(int s) {
 }
 
 extern "C" int seg_version(void) { return 1; }
+
+namespace seg {
+
+constexpr int kBnFinishGroups = 128;
+
+size_t bn_grad_finish_scratch(int C) { return (size_t)kBnFinishGroups * 2 * C * sizeof(float); }
+
+int bn_grad_finish(const float* part, int nrows, int C, int cv, float inv, float* dgamma, float* dbeta,
+                   float* scratch, hipStream_t s) {
+    if (!part || !dgamma || !dbeta || !scratch || nrows <= 0 || C <= 0 || cv > C) return SEG_EINVAL;
+    const float* rows = part;
+    int n = nrows;
+    if (nrows > kBnFinishGroups) {   // thousands of tile rows: fold them first (coalesced)
+        const int width = 2 * C;
+        hipLaunchKernelGGL(part_rows_reduce_k, dim3((width + 255) / 256, kBnFinishGroups), dim3(256), 0, s, part,
+                           nrows, width, scratch, kBnFinishGroups);
+        SEG_CHECK_LAUNCH();
+        rows = scratch;
+        n = kBnFinishGroups;
+    }
+    hipLaunchKernelGGL(bn_finish_k, dim3((cv + 7) / 8), dim3(256), 0, s, rows, n, C, cv, inv, dgamma, dbeta);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+}  // namespace seg

@@ -21,7 +21,27 @@ struct EpiParams {
     long mask_img;
     int ld_mask;
     float mask_scale;
+    // BatchNorm(+ReLU) backward of the BN folded into this conv's operand
+    // prologue (input gradients, igemm_nt2 only): v = acc = dL/d relu(BN(x));
+    // dz = v * [x*g*inv + beta > 0 or !bn_relu]; out = dz*g*inv (+ residual);
+    // column sums of dz*x and dz -> bn_part[M tile][2 * bn_C]
+    const void* bn_x;
+    long bn_x_img;
+    int ld_bn_x;
+    const float* bn_gamma;
+    const float* bn_beta;
+    float bn_inv;
+    int bn_relu;
+    int bn_cv;
+    float* bn_part;
+    int bn_C;
 };
+
+// dgamma / dbeta from per-tile partial rows [nrows][2C] (eltwise.hip);
+// scratch: bn_grad_finish_scratch(C) bytes
+size_t bn_grad_finish_scratch(int C);
+int bn_grad_finish(const float* part, int nrows, int C, int cv, float inv, float* dgamma, float* dbeta,
+                   float* scratch, hipStream_t s);
 
 // Optional A-operand prologue: the operand is relu(x * gamma[c] * inv + beta[c])
 // (frozen-statistics BatchNorm + ReLU of the producing layer, applied while
@@ -112,6 +132,7 @@ void nt_info(int M, int N, int K, int dtype, int phase, int* bm, int* bn, int* s
 const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits);
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
+void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
 extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;

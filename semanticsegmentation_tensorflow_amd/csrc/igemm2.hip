@@ -54,7 +54,10 @@ template <typename T>
 // PRO: the A operand goes through p.pro (BatchNorm + ReLU) between the LDS
 // read and the MFMA; the per-channel (scale, shift) table is staged in LDS
 // once per block (single-tap problems, K <= NT2_PRO_MAXK).
-template <typename T, int BM, int BN, int WM, int WN, int ABL = 0, int NSTG = 3, bool PRO = false>
+// BNB: the epilogue continues through the folded BatchNorm(+ReLU) backward
+// (EpiParams.bn_*): its own instantiation, so the plain kernels keep their
+// register budget (two blocks per CU for the short-K form).
+template <typename T, int BM, int BN, int WM, int WN, int ABL = 0, int NSTG = 3, bool PRO = false, bool BNB = false>
 __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTParams p) {
     constexpr int NW = WM * WN;
     constexpr int EPC = dt_traits<T>::EPC;
@@ -303,6 +306,18 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
         scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
+    constexpr bool bnb = BNB;                          // folded BatchNorm backward (see EpiParams)
+    float bsc[8], bsh[8], sgm[8], sbt[8];
+    if constexpr (BNB) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = col0 + j;
+            const bool cv = col < e.bn_cv;
+            bsc[j] = cv ? e.bn_gamma[col] * e.bn_inv : 0.f;
+            bsh[j] = cv ? e.bn_beta[col] : 0.f;
+            sgm[j] = sbt[j] = 0.f;
+        }
+    }
     const int hw2 = Ha * Wa;
 #pragma unroll 2
     for (int rr = rsub; rr < WTM; rr += RPP) {
@@ -328,19 +343,62 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
             if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), res + 4);
         }
         const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+        if constexpr (BNB) {
+            // dL/da -> dL/dx of a = relu(BN(x)): mask re-derived from x with
+            // the forward's arithmetic, BN scale, accumulation, column sums
+            float xv[8];
+            const T* xp = reinterpret_cast<const T*>(e.bn_x) + img * e.bn_x_img + pix * e.ld_bn_x + col0;
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp), xv);
+            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp + 4), xv + 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int col = col0 + j;
-            float x = v[j] * scl[j] + shf[j] + bias[j];
-            if (e.relu) x = fmaxf(x, 0.f);
-            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
-            if (e.residual) x += res[j];
-            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
-            v[j] = col < e.n_valid ? x : 0.f;
+            for (int j = 0; j < 8; ++j) {
+                const int col = col0 + j;
+                const bool on = col < e.bn_cv && (!e.bn_relu || xv[j] * bsc[j] + bsh[j] > 0.f);
+                const float dz = on ? v[j] : 0.f;
+                sgm[j] += dz * xv[j];
+                sbt[j] += dz;
+                float x = dz * bsc[j];
+                if (e.residual) x += res[j];
+                v[j] = col < e.n_valid ? x : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int col = col0 + j;
+                float x = v[j] * scl[j] + shf[j] + bias[j];
+                if (e.relu) x = fmaxf(x, 0.f);
+                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.residual) x += res[j];
+                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                v[j] = col < e.n_valid ? x : 0.f;
+            }
         }
         T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
         *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
         if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
+    }
+    if constexpr (BNB) {
+        // block column sums of dz*x / dz -> one partial row per M tile
+        constexpr int WMW = NW / WN;
+        __syncthreads();                              // staging reads done: reuse smem
+        float* red = reinterpret_cast<float*>(smem);  // [NW * 64][16]
+        static_assert(NW * 64 * 16 * 4 <= SMEM, "column-sum staging must fit");
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[tid * 16 + j] = sgm[j];
+            red[tid * 16 + 8 + j] = sbt[j];
+        }
+        __syncthreads();
+        for (int q = tid; q < 2 * BN; q += NW * 64) {
+            const int kind = q / BN, lc = q - (q / BN) * BN;
+            const int wn_ = lc / WTN, cch_ = (lc % WTN) / 8, j = lc % 8;
+            float sum = 0.f;
+            for (int wm_ = 0; wm_ < WMW; ++wm_)
+                for (int rs = 0; rs < RPP; ++rs)
+                    sum += red[((wm_ * WN + wn_) * 64 + rs * CPR + cch_) * 16 + kind * 8 + j];
+            const int col = n0 + lc;
+            if (col < e.bn_C) e.bn_part[(long)tm * 2 * e.bn_C + kind * e.bn_C + col] = sum;
+        }
     }
 }
 
@@ -592,6 +650,15 @@ int g_nt2_short = 8;
 
 bool nt2_short(const NTParams& p, int dtype) {
     return dtype == SEG_BF16 && !p.partial && p.K <= 64 * g_nt2_short && g_nt2_ablate == 0;
+}
+
+// input gradient + folded BN backward (EpiParams.bn_*): short-K 2-stage form
+void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s) {
+    const int tiles = ((p.M + 255) / 256) * ((p.N + 63) / 64);
+    if (dtype == SEG_F16)
+        hipLaunchKernelGGL((igemm_nt2<f16, 256, 64, 4, 2, 0, 2, false, true>), dim3(tiles), dim3(512), 0, s, p);
+    else
+        hipLaunchKernelGGL((igemm_nt2<bf16, 256, 64, 4, 2, 0, 2, false, true>), dim3(tiles), dim3(512), 0, s, p);
 }
 
 bool nt2_pro_ok(const NTParams& p, int dtype, int nphases) {

@@ -13,7 +13,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import SegConvDesc, SegEpilogue, SegPrologue, check
+from ._lib import SegBnBwd, SegConvDesc, SegEpilogue, SegKernelError, SegPrologue, check
 
 F32, BF16, F16 = 0, 1, 2
 _TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
@@ -171,6 +171,28 @@ def conv2d_fwd_pro(desc, x, pro, w_krsc, y, epi=None, ws=None, stream=None):
                                         None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
                                         stream_ptr(stream)), "conv2d")
     return y
+
+
+def conv_bwd_data_bn_workspace(desc):
+    """Bytes for conv2d_bwd_data_bn, 0 where the fused path does not apply."""
+    return int(_lib.lib().seg_conv_bwd_data_bn_workspace(ctypes.byref(desc)))
+
+
+def conv2d_bwd_data_bn(desc, dy, w_hwio, x, gamma, beta, dx, dgamma, dbeta, eps=1e-3, relu=True,
+                       accumulate=False, ws=None, stream=None):
+    """Conv2DBackpropInput of a 1x1 conv over relu(BN(x)) continued through the
+    BatchNorm(+ReLU) backward: dx = dL/dx of the BN input (+= with
+    accumulate), dgamma / dbeta overwritten (seg_conv2d_bwd_data_bn)."""
+    d = _with_ld(desc, dx, dy)
+    need = conv_bwd_data_bn_workspace(d)
+    if need == 0:
+        raise SegKernelError("conv2d_bwd_data_bn: fused BatchNorm backward does not apply to this conv")
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(need)
+    bn = SegBnBwd(x.data_ptr(), pixel_stride(x), gamma.data_ptr(), beta.data_ptr(), float(eps), 1 if relu else 0,
+                  1 if accumulate else 0, dgamma.data_ptr(), dbeta.data_ptr())
+    check(_lib.lib().seg_conv2d_bwd_data_bn(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(bn), ptr(dx),
+                                            wsp, wss, stream_ptr(stream)), "conv2d_backprop_input_bn")
+    return dx
 
 
 def conv2d_bwd_filter_pro(desc, x, pro, dy, dw, ws=None, stream=None, dbias=None):

@@ -191,6 +191,7 @@ class Session:
         # BatchNorm(+ReLU) feeding a single 1x1 conv folded into its operand prologue
         self.fold_bn = True
         self.fold_dropout_grad = True   # Conv -> Dropout -> BN: the dropout gradient inside the BN backward
+        self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -1259,7 +1260,25 @@ class Session:
                     K = n.desc.k_valid
                     self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
                 dx = None
-                if id(x) in ng:
+                pro = getattr(n, "pro", None)
+                if (id(x) in ng and pro is not None and self.fuse_bn_bwd and id(pro.inputs[0]) in ng
+                        and ops.conv_bwd_data_bn_workspace(n.desc) > 0):
+                    # input gradient carried through the folded BatchNorm(+ReLU)
+                    # backward in the same launch: the BN node's own backward is
+                    # skipped (its output gradient is never materialised)
+                    xb = pro.inputs[0]
+                    if id(xb) in p.alias:
+                        dxb, accf = adest(xb)
+                        acc = None
+                    else:
+                        (dxb, acc), accf = dest(xb), False
+                    gn, bn_ = pro.gamma.var_name, pro.beta.var_name
+                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bn, n.desc, dz,
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                store.param(bn_), dxb, store.grad(gn), store.grad(bn_), pro.eps, pro.relu, accf, ws)
+                    done(dxb, acc)
+                    self._grad_ready([gn, bn_])
+                elif id(x) in ng:
                     dx, acc = dest(x)
                     self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
@@ -1267,9 +1286,9 @@ class Session:
                     done(dx, acc)
                 if self.capture is not None:
                     # tests: the buffers of this layer's three kernels (they persist
-                    # after the step; dx before any accumulation of other consumers)
+                    # after the step; dx before any accumulation of other consumers;
+                    # None when it went straight through a folded BN backward)
                     mask = self._mask_epi(p, x) if dx is not None else None
-                    pro = getattr(n, "pro", None)
                     self.capture.append({"kind": "conv", "name": n.w.var_name, "bias": getattr(n.bias, "var_name", None),
                                          "x": buf[id(x)] if pro is None else buf[id(pro.inputs[0])],
                                          "pro": None if pro is None else (pro.gamma.var_name, pro.beta.var_name,

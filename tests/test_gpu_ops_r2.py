@@ -116,3 +116,43 @@ def test_conv2d_bwd_filter_with_bn_relu_prologue(dev, case, dtype):
     torch.cuda.synchronize()
     tol = 2e-5 if dtype == torch.float32 else 2e-3
     assert_close(dw.double().cpu(), wv.grad, torch.float32, f"conv wgrad pro {case}", tol)
+
+
+# input gradient of the same folded convs carried through the BN(+ReLU)
+# backward (seg_conv2d_bwd_data_bn) vs float64: dL/dx, dgamma, dbeta
+BNB_CASES = [(2, 9, 11, 48, 64, 1), (1, 12, 10, 136, 64, 1), (1, 33, 41, 200, 136, 1), (2, 20, 30, 520, 64, 1),
+             (1, 17, 19, 24, 8, 1), (2, 40, 52, 112, 64, 1)]
+
+
+@pytest.mark.parametrize("accumulate", [False, True], ids=["write", "accumulate"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", BNB_CASES)
+def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate):
+    N, H, W, C, K, R = case
+    x, w, gamma, beta, xr, wr, a = _pro_case(case, dtype, dev)
+    g = torch.Generator().manual_seed(9)
+    dy = rnd(torch.randn(N, H, W, K, generator=g, dtype=torch.float64), dtype)
+    # float64: a = relu(BN(x)), y = conv(a); backprop dy to x, gamma, beta
+    xv = xr.clone().requires_grad_(True)
+    gv, bv = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    av = T.relu(T.batch_norm_frozen(xv, gv, bv))
+    T.conv2d(av, wr).backward(dy)
+    d = ops.conv_desc(N, H, W, C, K, R, R, 1, 1, "SAME", PRO_DT[dtype])
+    assert ops.conv_bwd_data_bn_workspace(d) > 0
+    wh = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_HWIO), dtype=dtype, device=dev)
+    ops.pack_filter(w.float().to(dev).contiguous(), wh, ops.round8(C), ops.round8(K), ops.PACK_HWIO)
+    # the input gradient lands in a channel slice of a wider buffer (concat gradient)
+    old = rnd(torch.randn(N, H, W, C + 16, generator=g, dtype=torch.float64), dtype)
+    wide = to_dev(old, dtype, dev) if accumulate else torch.full((N, H, W, C + 16), float("nan"), dtype=dtype,
+                                                                   device=dev)
+    dx = wide[..., 8:8 + C]
+    dg, db = torch.full((C,), float("nan"), device=dev), torch.full((C,), float("nan"), device=dev)
+    ops.conv2d_bwd_data_bn(d, to_dev(dy, dtype, dev), wh, to_dev(x, dtype, dev), gamma.to(dev), beta.to(dev), dx,
+                           dg, db, accumulate=accumulate)
+    torch.cuda.synchronize()
+    want = xv.grad + (old[..., 8:8 + C] if accumulate else 0.0)
+    assert_close(from_dev(wide[..., 8:8 + C].contiguous(), C), want, dtype, f"bn-dgrad dx {case}")
+    if accumulate:   # the neighbouring channels of the shared buffer are untouched
+        assert torch.equal(wide[..., :8].cpu(), to_dev(old, dtype, dev)[..., :8].cpu())
+    assert_close(dg.double().cpu(), gv.grad, torch.float32, f"bn-dgrad dgamma {case}", 2e-3)
+    assert_close(db.double().cpu(), bv.grad, torch.float32, f"bn-dgrad dbeta {case}", 2e-3)

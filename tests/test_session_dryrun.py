@@ -23,7 +23,7 @@ class _Rec:
         host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
                              "seg_adam_segments_plan", "seg_tconv_filter_apad",
-                             "seg_conv_wgrad_adam_fusable")
+                             "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace")
 
         def fn(*a):
             if host_only:
@@ -167,7 +167,9 @@ def test_fcdensenet_train_plan(dry):
     assert c.count("seg_bn_relu_fwd") == 123 - n_fold
     # the 59 bottleneck conv1 -> Dropout -> BN chains: the dropout gradient
     # rides in the BN backward; only the growth convs' dropouts keep a pass
-    assert c.count("seg_bn_relu_bwd") + c.count("seg_bn_relu_dropout_bwd") == 123
+    # the folded BNs' backward runs in their 1x1 convs' input-gradient epilogue
+    assert c.count("seg_conv2d_bwd_data_bn") == n_fold
+    assert c.count("seg_bn_relu_bwd") + c.count("seg_bn_relu_dropout_bwd") == 123 - n_fold
     assert c.count("seg_bn_relu_dropout_bwd") == 59
     assert c.count("seg_dropout_bwd_ch") == 59
     assert c.count("seg_avgpool2x2_fwd") == 5
