@@ -122,14 +122,18 @@ int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const seg_prologue
 int seg_conv2d_bwd_filter_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro,
                               const void* dy, float* dw, float* dbias, void* ws, size_t ws_bytes,
                               void* stream);
-/* Conv2DBackpropInput of a 1x1 stride-1 conv over relu(BN(x)) (the BN folded
- * into the forward's operand prologue), carried through the BatchNorm(+ReLU)
- * backward in the same launch (FCDenseNet.py:25-28 backward): the ReLU mask
- * is re-derived from x, dx = dL/dx of the BN input (accumulate != 0: added
- * into dx, e.g. a slice of a shared concat gradient), dgamma / dbeta (fp32,
- * overwritten) from per-tile column sums.  bf16 / fp16 only; workspace from
- * seg_conv_bwd_data_bn_workspace, which returns 0 when the fused path does
- * not apply (then use seg_conv2d_bwd_data + seg_bn_relu_bwd). */
+/* Conv2DBackpropInput of a stride-1 conv over relu(BN(x)), carried through
+ * the BatchNorm(+ReLU) backward in the same launch (FCDenseNet.py:25-33
+ * backward): the ReLU mask is re-derived from x, dx = dL/dx of the BN input,
+ * dgamma / dbeta (fp32, overwritten) from per-tile column sums.  Applies to
+ * 1x1 convs (the BN folded into the forward's operand prologue; accumulate
+ * != 0 adds into dx, e.g. a slice of a shared concat gradient) and to 3x3
+ * convs with 16 output channels (FC-DenseNet's growth convs; keep_prob < 1
+ * then also applies the gradient of the TF1 dropout fused into the epilogue
+ * of the conv that produced x, counter pixel * C + c; no accumulate).
+ * bf16 / fp16 only; workspace from seg_conv_bwd_data_bn_workspace, which
+ * returns 0 when the fused path does not apply (then seg_conv2d_bwd_data +
+ * seg_bn_relu_bwd / seg_bn_relu_dropout_bwd). */
 typedef struct seg_bn_bwd {
     const void* x;          /* BN input, pixel stride ldx */
     int ldx;
@@ -140,6 +144,8 @@ typedef struct seg_bn_bwd {
     int accumulate;
     float* dgamma;
     float* dbeta;
+    float keep_prob;        /* 3x3 form: dropout before the BN (>= 1 or 0: none) */
+    uint64_t seed;
 } seg_bn_bwd;
 size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d);
 int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_bn_bwd* bn,

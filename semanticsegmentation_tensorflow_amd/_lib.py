@@ -104,7 +104,8 @@ class SegPrologue(ctypes.Structure):
 class SegBnBwd(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("ldx", ctypes.c_int), ("gamma", ctypes.c_void_p),
                 ("beta", ctypes.c_void_p), ("eps", ctypes.c_float), ("relu", ctypes.c_int),
-                ("accumulate", ctypes.c_int), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p)]
+                ("accumulate", ctypes.c_int), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64)]
 
 
 class SegAdamFused(ctypes.Structure):

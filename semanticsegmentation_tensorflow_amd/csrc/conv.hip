@@ -731,32 +731,43 @@ extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const
 // accumulated in place), dgamma / dbeta from per-tile column sums.  16-bit
 // igemm_nt2 only (seg_conv_bwd_data_bn_workspace returns 0 where it does not
 // apply).
-static bool bwd_data_bn_params(const seg_conv_desc* d, NTParams& p) {
-    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return false;
-    if (d->R != 1 || d->S != 1 || d->stride_h != 1 || d->stride_w != 1 || d->C % 8) return false;
+// kind: 1 = 1x1 (short-K igemm_nt2), 2 = 3x3 over 16 output channels (conv_res16c)
+static int bwd_data_bn_params(const seg_conv_desc* d, NTParams& p) {
+    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return 0;
+    if (d->stride_h != 1 || d->stride_w != 1 || d->C % 8) return 0;
     p = conv_bwd_data_params(d);
-    if (d->K > 64 * 8) return false;                  // the short-K igemm_nt2 (no split-K)
-    return true;
+    if (d->R == 1 && d->S == 1 && d->K <= 64 * 8) return 1;   // no split-K
+    if (seg::res16c_ok(p, d->dtype)) return 2;
+    return 0;
+}
+
+// per-tile (1x1) or per-block (3x3) partial rows + the finish scratch
+static long bwd_data_bn_rows(const seg_conv_desc* d, const NTParams& p, int kind) {
+    return kind == 1 ? (p.M + 255) / 256 : seg::res16c_grid(p, seg::device_cus());
 }
 
 extern "C" size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d) {
     NTParams p;
-    if (!bwd_data_bn_params(d, p)) return 0;
-    const long tiles_m = (p.M + 255) / 256;
-    return (size_t)tiles_m * 2 * d->C * sizeof(float) + seg::bn_grad_finish_scratch(d->C);
+    const int kind = bwd_data_bn_params(d, p);
+    if (!kind) return 0;
+    return (size_t)bwd_data_bn_rows(d, p, kind) * 2 * d->C * sizeof(float) + seg::bn_grad_finish_scratch(d->C);
 }
 
 extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w, const seg_bn_bwd* bn,
                                       void* dx, void* ws, size_t ws_bytes, void* stream) {
     NTParams p;
-    if (!bwd_data_bn_params(d, p)) return SEG_EINVAL;
+    const int kind = bwd_data_bn_params(d, p);
+    if (!kind) return SEG_EINVAL;
     if (!dy || !w || !dx || !bn || !bn->x || !bn->gamma || !bn->beta || !bn->dgamma || !bn->dbeta) return SEG_EINVAL;
     if (bn->ldx % 8 || bn->ldx < d->C) return SEG_EINVAL;
+    const bool drop = bn->keep_prob > 0.f && bn->keep_prob < 1.f;
+    if ((drop || kind == 2) && bn->accumulate) return SEG_EINVAL;   // the 3x3 / dropout forms write dx
+    if (drop && kind != 2) return SEG_EINVAL;
     const size_t need = seg_conv_bwd_data_bn_workspace(d);
     if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
-    const long tiles_m = (p.M + 255) / 256;
+    const long nrows = bwd_data_bn_rows(d, p, kind);
     float* part = reinterpret_cast<float*>(ws);
-    float* scratch = part + tiles_m * 2 * d->C;
+    float* scratch = part + nrows * 2 * d->C;
     p.x = dy; p.w = w; p.y = dx;
     const float inv = 1.0f / sqrtf(1.0f + bn->eps);
     seg::EpiParams& e = p.epi;
@@ -769,10 +780,15 @@ extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, co
     e.bn_x = bn->x; e.ld_bn_x = bn->ldx; e.bn_x_img = (long)d->H * d->W * bn->ldx;
     e.bn_gamma = bn->gamma; e.bn_beta = bn->beta; e.bn_inv = inv; e.bn_relu = bn->relu ? 1 : 0;
     e.bn_cv = d->c_valid; e.bn_part = part; e.bn_C = d->C;
+    if (drop) {          // the dropout of the conv that produced x (counter pixel * C + c)
+        e.keep_prob = bn->keep_prob;
+        e.seed = bn->seed;
+    }
     hipStream_t s = (hipStream_t)stream;
-    seg::launch_nt2_bn(p, d->dtype, s);
+    if (kind == 1) seg::launch_nt2_bn(p, d->dtype, s);
+    else seg::launch_res16c_bn(p, seg::device_cus(), s, d->dtype);
     SEG_CHECK_LAUNCH();
-    return seg::bn_grad_finish(part, (int)tiles_m, d->C, d->c_valid, inv, bn->dgamma, bn->dbeta, scratch, s);
+    return seg::bn_grad_finish(part, (int)nrows, d->C, d->c_valid, inv, bn->dgamma, bn->dbeta, scratch, s);
 }
 
 extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias,

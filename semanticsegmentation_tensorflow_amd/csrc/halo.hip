@@ -819,7 +819,11 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
 // ---------------------------------------------------------------------------
 constexpr int R16_PER = (R64_HROWS * 2 + 511) / 512;   // halo chunks per thread (2)
 
-template <typename T = bf16>
+// BNB: the epilogue continues through the BatchNorm(+ReLU) backward of the
+// layer whose output this conv read (EpiParams.bn_*; then the standard
+// dropout fields re-draw the dropout of the conv before that BN), and the
+// block's column sums of dz*x / dz over all its tiles go to bn_part[block].
+template <typename T = bf16, bool BNB = false>
 __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, int tiles_y, int ntiles) {
     constexpr int WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2, KS = 5;
     constexpr int BS = KS * 64 * 64;
@@ -903,6 +907,20 @@ __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, i
             shf[ni][j] = (e.shift && cv) ? e.shift[col] : 0.f;
         }
 
+    float bsc[TN][4], bsh[TN][4], sgm[TN][4], sbt[TN][4];
+    if constexpr (BNB) {
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = wn * WTN + ni * 16 + 4 * fg + j;
+                const bool cv = col < e.bn_cv;
+                bsc[ni][j] = cv ? e.bn_gamma[col] * e.bn_inv : 0.f;
+                bsh[ni][j] = cv ? e.bn_beta[col] : 0.f;
+                sgm[ni][j] = sbt[ni][j] = 0.f;
+            }
+    }
+
     int t = blockIdx.x;
     if (t < ntiles) fetch(t);
     commit();
@@ -965,15 +983,33 @@ __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, i
                         for (int j = 0; j < 4; ++j) res[j] = to_f32(rp[j]);
                     }
                     T o[4];
+                    if constexpr (BNB) {
+                        const T* xp = reinterpret_cast<const T*>(e.bn_x) + img * e.bn_x_img + pix * e.ld_bn_x + col0;
+                        const uint2 xr = *reinterpret_cast<const uint2*>(xp);
+                        const T* xh = reinterpret_cast<const T*>(&xr);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int col = col0 + j;
-                        float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
-                        if (e.relu) x = fmaxf(x, 0.f);
-                        if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
-                        x += res[j];
-                        if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
-                        o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+                        for (int j = 0; j < 4; ++j) {
+                            const int col = col0 + j;
+                            const float xv = to_f32(xh[j]);
+                            const bool on = col < e.bn_cv && (!e.bn_relu || xv * bsc[ni][j] + bsh[ni][j] > 0.f);
+                            const float dz = on ? acc[mi][ni][j] : 0.f;
+                            sgm[ni][j] += dz * xv;
+                            sbt[ni][j] += dz;
+                            float x = dz * bsc[ni][j];
+                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int col = col0 + j;
+                            float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
+                            if (e.relu) x = fmaxf(x, 0.f);
+                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            x += res[j];
+                            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                            o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+                        }
                     }
                     *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
                         *reinterpret_cast<const uint2*>(o);
@@ -983,6 +1019,37 @@ __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, i
         __syncthreads();                             // all steps read the halo
         commit();                                    // next tile's halo (waits for its loads)
         __syncthreads();
+    }
+    if constexpr (BNB) {
+        // lanes fr = 0..15 share channels: butterfly over them, then the
+        // four M waves of each column half meet in LDS (the halo is free)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int off = 1; off < 16; off <<= 1) {
+                    sgm[ni][j] += __shfl_xor(sgm[ni][j], off);
+                    sbt[ni][j] += __shfl_xor(sbt[ni][j], off);
+                }
+        float* red = reinterpret_cast<float*>(Hs);   // [8 waves][2 kinds][32 columns]
+        if (fr == 0) {
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int lc = ni * 16 + 4 * fg + j;
+                    red[(w * 2 + 0) * 32 + lc] = sgm[ni][j];
+                    red[(w * 2 + 1) * 32 + lc] = sbt[ni][j];
+                }
+        }
+        __syncthreads();
+        if (tid < 2 * 64) {
+            const int kind = tid / 64, c = tid % 64, wn_ = c / 32, lc = c % 32;
+            float sum = 0.f;
+            for (int wm_ = 0; wm_ < 4; ++wm_) sum += red[((wm_ * WN + wn_) * 2 + kind) * 32 + lc];
+            if (c < e.bn_C) e.bn_part[(long)blockIdx.x * 2 * e.bn_C + kind * e.bn_C + c] = sum;
+        }
     }
 }
 
@@ -1093,6 +1160,21 @@ void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int grid = std::min(ntiles, 2 * cus);
     if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res16c<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
     else hipLaunchKernelGGL((conv_res16c<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+}
+
+int res16c_grid(const NTParams& p, int cus) {
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
+    return std::min((p.M / (p.OH * p.OW)) * tx * ty, 2 * cus);
+}
+
+void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype) {
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
+    const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
+    const int grid = res16c_grid(p, cus);
+    if (dtype == SEG_F16)
+        hipLaunchKernelGGL((conv_res16c<f16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    else
+        hipLaunchKernelGGL((conv_res16c<bf16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
 }
 
 bool res64_ok(const NTParams& p, int dtype) {

@@ -235,6 +235,8 @@ extern int g_res16;
 extern int g_res16c;
 bool res16c_ok(const NTParams& p, int dtype);
 void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
+int res16c_grid(const NTParams& p, int cus);
+void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype);
 extern int g_halo2_n128;
 bool res64_ok(const NTParams& p, int dtype);
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);

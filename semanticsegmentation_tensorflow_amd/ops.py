@@ -179,17 +179,20 @@ def conv_bwd_data_bn_workspace(desc):
 
 
 def conv2d_bwd_data_bn(desc, dy, w_hwio, x, gamma, beta, dx, dgamma, dbeta, eps=1e-3, relu=True,
-                       accumulate=False, ws=None, stream=None):
-    """Conv2DBackpropInput of a 1x1 conv over relu(BN(x)) continued through the
+                       accumulate=False, ws=None, stream=None, dropout=None):
+    """Conv2DBackpropInput of a conv over relu(BN(x)) continued through the
     BatchNorm(+ReLU) backward: dx = dL/dx of the BN input (+= with
-    accumulate), dgamma / dbeta overwritten (seg_conv2d_bwd_data_bn)."""
+    accumulate), dgamma / dbeta overwritten (seg_conv2d_bwd_data_bn).
+    dropout = (keep_prob, seed): the 3x3 form also applies the gradient of
+    the dropout fused into the conv that produced x."""
     d = _with_ld(desc, dx, dy)
     need = conv_bwd_data_bn_workspace(d)
     if need == 0:
         raise SegKernelError("conv2d_bwd_data_bn: fused BatchNorm backward does not apply to this conv")
     wsp, wss = (ws or Workspace(dy.device)).ptr_size(need)
+    kp, seed = dropout if dropout is not None else (1.0, 0)
     bn = SegBnBwd(x.data_ptr(), pixel_stride(x), gamma.data_ptr(), beta.data_ptr(), float(eps), 1 if relu else 0,
-                  1 if accumulate else 0, dgamma.data_ptr(), dbeta.data_ptr())
+                  1 if accumulate else 0, dgamma.data_ptr(), dbeta.data_ptr(), float(kp), int(seed) & (2 ** 64 - 1))
     check(_lib.lib().seg_conv2d_bwd_data_bn(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(bn), ptr(dx),
                                             wsp, wss, stream_ptr(stream)), "conv2d_backprop_input_bn")
     return dx

@@ -541,6 +541,7 @@ class Session:
         dropout-gradient pass is skipped.  p.drop_fold: bn node id -> conv."""
         p.drop_fold = {}
         p.drop_folded = set()
+        p.bn_before = {}
         if not self.fold_dropout_grad:
             return
         users = {}
@@ -559,6 +560,21 @@ class Session:
                 continue
             p.drop_fold[id(us[0])] = c
             p.drop_folded.add(id(c))
+        # BN(+ReLU) -> 3x3 conv (FC-DenseNet's growth conv): the conv's input
+        # gradient kernel can continue through that BN's backward when the BN
+        # output has no other reader and its input gradient is not shared
+        p.bn_before = {}
+        for c in p.nodes:
+            if c.kind != "conv" or getattr(c, "pro", None) is not None:
+                continue
+            t = c.inputs[0]
+            us = users.get(id(t), [])
+            b = next((n for n in p.nodes if n.kind == "bn" and n.output is t), None)
+            if b is None or len(us) != 1 or id(t) in fetched:
+                continue
+            xb = b.inputs[0]
+            if len(users.get(id(xb), [])) == 1 and id(xb) not in fetched:
+                p.bn_before[id(c)] = b
 
     def _infer(self, op, shp):
         t = op.type
@@ -1276,6 +1292,25 @@ class Session:
                     self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
                                 store.param(bn_), dxb, store.grad(gn), store.grad(bn_), pro.eps, pro.relu, accf, ws)
+                    done(dxb, acc)
+                    self._grad_ready([gn, bn_])
+                elif (id(x) in ng and id(n) in p.bn_before and self.fuse_bn_bwd
+                      and id(p.bn_before[id(n)].inputs[0]) in ng and id(p.bn_before[id(n)].inputs[0]) not in p.alias
+                      and id(p.bn_before[id(n)].inputs[0]) not in grad
+                      and ops.conv_bwd_data_bn_workspace(n.desc) > 0):
+                    # growth conv: its input gradient continues through the BN
+                    # (+ the dropout before it) that produced its input
+                    b = p.bn_before[id(n)]
+                    xb = b.inputs[0]
+                    dxb, acc = dest(xb)
+                    c1 = p.drop_fold.get(id(b))
+                    drop = (c1.kp_val, c1.seed_val) if (c1 is not None and c1.kp_val is not None
+                                                         and c1.kp_val < 1.0) else None
+                    gn, bn_ = b.gamma.var_name, b.beta.var_name
+                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bn, n.desc, dz,
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                store.param(bn_), dxb, store.grad(gn), store.grad(bn_), b.eps, b.relu, False, ws,
+                                None, drop)
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
                 elif id(x) in ng:

@@ -156,3 +156,42 @@ def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate):
         assert torch.equal(wide[..., :8].cpu(), to_dev(old, dtype, dev)[..., :8].cpu())
     assert_close(dg.double().cpu(), gv.grad, torch.float32, f"bn-dgrad dgamma {case}", 2e-3)
     assert_close(db.double().cpu(), bv.grad, torch.float32, f"bn-dgrad dbeta {case}", 2e-3)
+
+
+# the 3x3 form (FC-DenseNet growth conv, 64 -> 16): the input gradient runs on
+# conv_res16c and continues through the BN(+ReLU) that produced the conv's
+# input and, with keep_prob < 1, the dropout of the conv before that BN
+BNB3_CASES = [(2, 21, 67, 64, 16), (1, 30, 70, 64, 16), (2, 9, 11, 32, 16)]
+
+
+@pytest.mark.parametrize("kp", [1.0, 0.6], ids=["no-dropout", "dropout"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", BNB3_CASES)
+def test_conv3x3_bwd_data_through_bn_relu_dropout(dev, case, dtype, kp):
+    from tests.test_gpu_ops import _np_uniform
+    N, H, W, C, K = case
+    x, w, gamma, beta, xr, wr, a = _pro_case((N, H, W, C, K, 3), dtype, dev)
+    g = torch.Generator().manual_seed(10)
+    dy = rnd(torch.randn(N, H, W, K, generator=g, dtype=torch.float64), dtype)
+    xv = xr.clone().requires_grad_(True)
+    gv, bv = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    T.conv2d(T.relu(T.batch_norm_frozen(xv, gv, bv)), wr).backward(dy)
+    seed = 12345
+    want = xv.grad
+    if kp < 1.0:
+        P = N * H * W
+        u = np.array([[_np_uniform(seed, p * C + c) for c in range(C)] for p in range(P)], np.float32)
+        mask = torch.from_numpy(np.floor(np.float32(kp) + u).astype(np.float64)).view(N, H, W, C)
+        want = want / kp * mask
+    d = ops.conv_desc(N, H, W, C, K, 3, 3, 1, 1, "SAME", PRO_DT[dtype])
+    assert ops.conv_bwd_data_bn_workspace(d) > 0
+    wh = torch.zeros(ops.packed_shape(3, 3, C, K, ops.PACK_HWIO), dtype=dtype, device=dev)
+    ops.pack_filter(w.float().to(dev).contiguous(), wh, ops.round8(C), ops.round8(K), ops.PACK_HWIO)
+    dx = torch.full((N, H, W, C), float("nan"), dtype=dtype, device=dev)
+    dg, db = torch.full((C,), float("nan"), device=dev), torch.full((C,), float("nan"), device=dev)
+    ops.conv2d_bwd_data_bn(d, to_dev(dy, dtype, dev), wh, to_dev(x, dtype, dev), gamma.to(dev), beta.to(dev), dx,
+                           dg, db, dropout=(kp, seed) if kp < 1.0 else None)
+    torch.cuda.synchronize()
+    assert_close(from_dev(dx, C), want, dtype, f"bn3-dgrad dx {case}")
+    assert_close(dg.double().cpu(), gv.grad, torch.float32, f"bn3-dgrad dgamma {case}", 2e-3)
+    assert_close(db.double().cpu(), bv.grad, torch.float32, f"bn3-dgrad dbeta {case}", 2e-3)

@@ -167,10 +167,13 @@ def test_fcdensenet_train_plan(dry):
     assert c.count("seg_bn_relu_fwd") == 123 - n_fold
     # the 59 bottleneck conv1 -> Dropout -> BN chains: the dropout gradient
     # rides in the BN backward; only the growth convs' dropouts keep a pass
-    # the folded BNs' backward runs in their 1x1 convs' input-gradient epilogue
-    assert c.count("seg_conv2d_bwd_data_bn") == n_fold
-    assert c.count("seg_bn_relu_bwd") + c.count("seg_bn_relu_dropout_bwd") == 123 - n_fold
-    assert c.count("seg_bn_relu_dropout_bwd") == 59
+    # BN backward inside the consuming conv's input-gradient launch: the n_fold
+    # folded 1x1 convs, the 59 growth convs (3x3 over BN -> ReLU, with the
+    # bottleneck conv1's dropout gradient) and the 27 decoder-block 1x1 convs
+    # whose BN stays materialised in the forward (input is a copying concat)
+    assert c.count("seg_conv2d_bwd_data_bn") == n_fold + 59 + 27
+    assert c.count("seg_bn_relu_bwd") + c.count("seg_bn_relu_dropout_bwd") == 123 - (n_fold + 59 + 27)
+    assert c.count("seg_bn_relu_dropout_bwd") == 0
     assert c.count("seg_dropout_bwd_ch") == 59
     assert c.count("seg_avgpool2x2_fwd") == 5
     assert c.count("seg_conv2d_bwd_filter") + c.count("seg_conv2d_bwd_filter_pro") == 125
