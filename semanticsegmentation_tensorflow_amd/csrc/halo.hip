@@ -687,19 +687,16 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
     for (int tap = 0; tap < 9; ++tap) toff[tap] = ((tap / 3) * p.tsh - hy0) * R64_HW + (tap % 3) * p.tsw - hx0;
 
     // epilogue constants: the MFMA computes D^T (filter rows x pixels), so a
-    // lane holds 4 consecutive channels of one pixel -> 8-byte stores
+    // lane holds 4 consecutive channels of one pixel -> 8-byte stores.  The
+    // per-column scale / (shift + bias) sit in LDS (read as float4 per
+    // fragment), not in 24 VGPRs across the whole kernel.
     const EpiParams& e = p.epi;
-    float bias[TN][4], scl[TN][4], shf[TN][4];
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int col = wn * WTN + ni * 16 + 4 * fg + j;
-            const bool cv = col < e.n_valid;
-            bias[ni][j] = (e.bias && cv) ? e.bias[col] : 0.f;
-            scl[ni][j] = (e.scale && cv) ? e.scale[col] : 1.f;
-            shf[ni][j] = (e.shift && cv) ? e.shift[col] : 0.f;
-        }
+    __shared__ __attribute__((aligned(16))) float etab[2][NB];
+    if (tid < NB) {
+        const bool cv = tid < e.n_valid;
+        etab[0][tid] = (e.scale && cv) ? e.scale[tid] : 1.f;
+        etab[1][tid] = ((e.shift && cv) ? e.shift[tid] : 0.f) + ((e.bias && cv) ? e.bias[tid] : 0.f);
+    }
 
     int t = blockIdx.x;
     if (t < ntiles) fetch(t);
@@ -782,10 +779,12 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                         for (int j = 0; j < 4; ++j) res[j] = to_f32(rp[j]);
                     }
                     T o[4];
+                    const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
+                    const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int col = col0 + j;
-                        float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
+                        float x = acc[mi][ni][j] * sc4[j] + ad4[j];
                         if (e.relu) x = fmaxf(x, 0.f);
                         if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                         x += res[j];
@@ -824,7 +823,7 @@ constexpr int R16_PER = (R64_HROWS * 2 + 511) / 512;   // halo chunks per thread
 // dropout fields re-draw the dropout of the conv before that BN), and the
 // block's column sums of dz*x / dz over all its tiles go to bn_part[block].
 template <typename T = bf16, bool BNB = false>
-__global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+__global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int tiles_x, int tiles_y, int ntiles) {
     constexpr int WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2, KS = 5;
     constexpr int BS = KS * 64 * 64;
     constexpr int HS = R64_HROWS * 32;
@@ -894,31 +893,26 @@ __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, i
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) toff[tap] = ((tap / 3) * p.tsh - hy0) * R64_HW + (tap % 3) * p.tsw - hx0;
 
+    // per-column epilogue constants in LDS (float4 per fragment): scale,
+    // shift + bias, and for BNB the BN's gamma * inv and beta
     const EpiParams& e = p.epi;
-    float bias[TN][4], scl[TN][4], shf[TN][4];
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int col = wn * WTN + ni * 16 + 4 * fg + j;
-            const bool cv = col < e.n_valid;
-            bias[ni][j] = (e.bias && cv) ? e.bias[col] : 0.f;
-            scl[ni][j] = (e.scale && cv) ? e.scale[col] : 1.f;
-            shf[ni][j] = (e.shift && cv) ? e.shift[col] : 0.f;
+    __shared__ __attribute__((aligned(16))) float etab[4][64];
+    if (tid < 64) {
+        const bool cv = tid < e.n_valid;
+        etab[0][tid] = (e.scale && cv) ? e.scale[tid] : 1.f;
+        etab[1][tid] = ((e.shift && cv) ? e.shift[tid] : 0.f) + ((e.bias && cv) ? e.bias[tid] : 0.f);
+        if constexpr (BNB) {
+            const bool bv = tid < e.bn_cv;
+            etab[2][tid] = bv ? e.bn_gamma[tid] * e.bn_inv : 0.f;
+            etab[3][tid] = bv ? e.bn_beta[tid] : 0.f;
         }
-
-    float bsc[TN][4], bsh[TN][4], sgm[TN][4], sbt[TN][4];
+    }
+    float sgm[TN][4], sbt[TN][4];
     if constexpr (BNB) {
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = wn * WTN + ni * 16 + 4 * fg + j;
-                const bool cv = col < e.bn_cv;
-                bsc[ni][j] = cv ? e.bn_gamma[col] * e.bn_inv : 0.f;
-                bsh[ni][j] = cv ? e.bn_beta[col] : 0.f;
-                sgm[ni][j] = sbt[ni][j] = 0.f;
-            }
+            for (int j = 0; j < 4; ++j) sgm[ni][j] = sbt[ni][j] = 0.f;
     }
 
     int t = blockIdx.x;
@@ -987,23 +981,27 @@ __global__ __launch_bounds__(512, 2) void conv_res16c(NTParams p, int tiles_x, i
                         const T* xp = reinterpret_cast<const T*>(e.bn_x) + img * e.bn_x_img + pix * e.ld_bn_x + col0;
                         const uint2 xr = *reinterpret_cast<const uint2*>(xp);
                         const T* xh = reinterpret_cast<const T*>(&xr);
+                        const f32x4 bs4 = *reinterpret_cast<const f32x4*>(&etab[2][col0]);
+                        const f32x4 bb4 = *reinterpret_cast<const f32x4*>(&etab[3][col0]);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int col = col0 + j;
                             const float xv = to_f32(xh[j]);
-                            const bool on = col < e.bn_cv && (!e.bn_relu || xv * bsc[ni][j] + bsh[ni][j] > 0.f);
+                            const bool on = col < e.bn_cv && (!e.bn_relu || xv * bs4[j] + bb4[j] > 0.f);
                             const float dz = on ? acc[mi][ni][j] : 0.f;
                             sgm[ni][j] += dz * xv;
                             sbt[ni][j] += dz;
-                            float x = dz * bsc[ni][j];
+                            float x = dz * bs4[j];
                             if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
                         }
                     } else {
+                        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
+                        const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int col = col0 + j;
-                            float x = acc[mi][ni][j] * scl[ni][j] + shf[ni][j] + bias[ni][j];
+                            float x = acc[mi][ni][j] * sc4[j] + ad4[j];
                             if (e.relu) x = fmaxf(x, 0.f);
                             if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
                             x += res[j];
@@ -1187,7 +1185,7 @@ bool res64_ok(const NTParams& p, int dtype) {
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
-    if (p.N <= 16 && g_res16) {               // two blocks per CU
+    if (p.N <= 16 && g_res16) {               // two blocks per CU (launch bounds: 4 waves / SIMD)
         const int grid = std::min(ntiles, 2 * cus);
         if (dtype == SEG_F16)
             hipLaunchKernelGGL((conv_res64<0, f16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
