@@ -392,7 +392,10 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
         # algorithmic HBM bytes: input + output activations once, the filter once
         # (fp32 filter gradient for the wgrad ops)
         nbytes = esz * (desc.N * desc.H * desc.W * desc.c_valid + desc.N * desc.OH * desc.OW * desc.k_valid) \
-            + (4 if op in (ops.OP_BWD_FILTER, ops.OP_TBWD_FILTER) else esz) * desc.R * desc.S * desc.c_valid * desc.k_valid
+            + (4 if op in (ops.OP_BWD_FILTER, ops.OP_TBWD_FILTER, ops.OP_BWD_FILTER_PRO) else esz) \
+            * desc.R * desc.S * desc.c_valid * desc.k_valid
+        if op == ops.OP_BWD_DATA_BN:        # + the BN input read to re-derive the mask / dgamma
+            nbytes += esz * desc.N * desc.H * desc.W * desc.c_valid
         rows.append((name, op, splits, flops, ms, desc.N, desc.H, desc.W, desc.c_valid, desc.k_valid, desc.R))
         a = per.setdefault(name, [0, 0.0, 0.0, 0.0])
         a[0] += 1

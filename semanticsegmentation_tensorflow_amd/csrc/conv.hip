@@ -132,6 +132,8 @@ static NTParams conv_bwd_data_params(const seg_conv_desc* d) {
     return p;
 }
 
+static int bwd_data_bn_params(const seg_conv_desc* d, NTParams& p);
+
 static TNParams conv_bwd_filter_params(const seg_conv_desc* d) {
     TNParams p = {};
     p.M = d->R * d->S * d->C; p.N = d->K; p.P = d->N * d->OH * d->OW;
@@ -454,6 +456,32 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
                 fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(Mt, d->C, d->N * d->H * d->W, seg::device_cus(), &sp);
             }
             macs = macs_t;
+            break;
+        }
+        case 6: {        // Conv2DBackpropInput through the BN(+ReLU) backward (seg_conv2d_bwd_data_bn)
+            NTParams p;
+            const int kind = bwd_data_bn_params(d, p);
+            if (!kind) return SEG_EINVAL;
+            macs = macs_conv;
+            if (kind == 1) { fam = "igemm_nt2_bn"; bm = 256; bn = 64; }
+            else { fam = "conv_res16c_bn"; bm = 256; bn = 64; }
+            break;
+        }
+        case 7: {        // Conv2D over relu(BN(x)) (seg_conv2d_fwd_pro)
+            NTParams p = conv_fwd_params(d);
+            macs = macs_conv;
+            if (seg::g_nt_variant == 2 && seg::nt2_pro_ok(p, d->dtype, 1)) {
+                fam = "igemm_nt2_pro"; bm = 192; bn = p.N <= 64 ? 64 : 128;
+            } else {
+                fam = "igemm_nt_pro"; bm = 128; bn = p.N <= 64 ? 64 : 128;
+            }
+            break;
+        }
+        case 8: {        // Conv2DBackpropFilter with relu(BN(x)) recomputed (seg_conv2d_bwd_filter_pro)
+            TNParams p = conv_bwd_filter_params(d);
+            macs = macs_conv;
+            seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp);
+            fam = (d->dtype != SEG_F32 && seg::g_tn_variant == 2 && p.M == p.Cg) ? "igemm_tn2_pro" : "igemm_tn_pro";
             break;
         }
         default: return SEG_EINVAL;

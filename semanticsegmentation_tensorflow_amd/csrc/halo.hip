@@ -923,6 +923,29 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
     for (; t < ntiles; t += gridDim.x) {
         const int tn = t + gridDim.x;
         if (tn < ntiles) fetch(tn);                  // in flight during this tile's MFMAs
+        // BNB: this tile's BN inputs for the lane's epilogue elements, also
+        // requested now so their latency hides under the MFMAs
+        uint2 pxb[BNB ? TM : 1][BNB ? TN : 1];
+        if constexpr (BNB) {
+            const int img = t / tpi;
+            const int rem = t - img * tpi;
+            const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int ml = wm * WTM + mi * 16 + fr;
+                const int oy = ty * R64_BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
+                const bool ok = oy < p.OH && ox < p.OW;
+                const long pix = ok ? (long)oy * p.OW + ox : 0;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col0 = wn * WTN + ni * 16 + 4 * fg;
+                    pxb[mi][ni] = uint2{0u, 0u};
+                    if (ok && col0 < p.N)
+                        pxb[mi][ni] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.bn_x) +
+                                                                       img * e.bn_x_img + pix * e.ld_bn_x + col0);
+                }
+            }
+        }
         f32x4 acc[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -978,8 +1001,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
                     }
                     T o[4];
                     if constexpr (BNB) {
-                        const T* xp = reinterpret_cast<const T*>(e.bn_x) + img * e.bn_x_img + pix * e.ld_bn_x + col0;
-                        const uint2 xr = *reinterpret_cast<const uint2*>(xp);
+                        const uint2 xr = pxb[mi][ni];
                         const T* xh = reinterpret_cast<const T*>(&xr);
                         const f32x4 bs4 = *reinterpret_cast<const f32x4*>(&etab[2][col0]);
                         const f32x4 bb4 = *reinterpret_cast<const f32x4*>(&etab[3][col0]);

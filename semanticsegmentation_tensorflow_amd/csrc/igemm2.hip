@@ -206,6 +206,34 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // BNB: the epilogue's BN input and accumulation operands (x, old dx) for
+    // this lane's rows are requested before the first DMA, so their HBM
+    // latency overlaps the operand staging and MFMAs instead of following it
+    constexpr int ECPR = WTN / 8, ERPP = 64 / ECPR, ENPR = WTM / ERPP;   // epilogue: rows per lane
+    uint4 pfx[BNB ? ENPR : 1], pfr[BNB ? ENPR : 1];
+    if constexpr (BNB) {
+        static_assert(sizeof(T) == 2, "BNB epilogue: 16-bit operands");
+        const int ecol0 = n0 + wn * WTN + (lane % ECPR) * 8;
+        const int ersub = lane / ECPR;
+#pragma unroll
+        for (int k = 0; k < ENPR; ++k) {
+            const int row = m0 + wm * WTM + ersub + k * ERPP;
+            pfx[k] = pfr[k] = uint4{0u, 0u, 0u, 0u};
+            if (row >= M || ecol0 >= p.N) continue;
+            const int hw = Ha * Wa;
+            const int img = row / hw;
+            const int rem = row - img * hw;
+            const int a = rem / Wa;
+            const int b = rem - a * Wa;
+            const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
+            pfx[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p.epi.bn_x) + img * p.epi.bn_x_img +
+                                                     pix * p.epi.ld_bn_x + ecol0);
+            if (p.epi.residual)
+                pfr[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p.epi.residual) +
+                                                         img * p.epi.res_img + pix * p.epi.ld_res + ecol0);
+        }
+    }
+
     if (kt_begin < kt_end) load_stage(0);
     if (NSTG == 3 && kt_begin + 1 < kt_end) load_stage(1);
 
@@ -319,10 +347,9 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
         }
     }
     const int hw2 = Ha * Wa;
-#pragma unroll 2
-    for (int rr = rsub; rr < WTM; rr += RPP) {
+    auto erow = [&](const int rr, const int k) {
         const int row = m0 + wm * WTM + rr;
-        if (row >= M || col0 >= p.N) continue;
+        if (row >= M || col0 >= p.N) return;
         const int img = row / hw2;
         const int rem = row - img * hw2;
         const int a = rem / Wa;
@@ -337,7 +364,9 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
             if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
         }
-        if (e.residual) {
+        if constexpr (BNB) {
+            if (e.residual) Chunk<T>::unpack(pfr[k], res);
+        } else if (e.residual) {
             const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp + 4), res + 4);
@@ -347,9 +376,7 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
             // dL/da -> dL/dx of a = relu(BN(x)): mask re-derived from x with
             // the forward's arithmetic, BN scale, accumulation, column sums
             float xv[8];
-            const T* xp = reinterpret_cast<const T*>(e.bn_x) + img * e.bn_x_img + pix * e.ld_bn_x + col0;
-            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp), xv);
-            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xp + 4), xv + 4);
+            Chunk<T>::unpack(pfx[k], xv);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
@@ -376,6 +403,14 @@ __global__ __launch_bounds__(WM* WN * 64, NSTG == 2 ? 2 : 1) void igemm_nt2(NTPa
         T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
         *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
         if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
+    };
+    if constexpr (BNB) {
+        static_assert(ERPP == RPP && ENPR * RPP == WTM, "prefetch rows = epilogue rows");
+#pragma unroll
+        for (int k = 0; k < ENPR; ++k) erow(rsub + k * RPP, k);
+    } else {
+#pragma unroll 2
+        for (int rr = rsub; rr < WTM; rr += RPP) erow(rr, 0);
     }
     if constexpr (BNB) {
         // block column sums of dz*x / dz -> one partial row per M tile

@@ -114,6 +114,8 @@ def epilogue(bias=None, scale=None, shift=None, residual=None, relu=False, keep_
 
 
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER, OP_TFWD, OP_TBWD_DATA, OP_TBWD_FILTER = range(6)
+# kernel-table only (seg_conv_kernel_info): the folded-BatchNorm forms
+OP_BWD_DATA_BN, OP_FWD_PRO, OP_BWD_FILTER_PRO = 6, 7, 8
 
 
 def conv_kernel_info(desc, op):

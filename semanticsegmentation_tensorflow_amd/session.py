@@ -973,7 +973,7 @@ class Session:
                                    relu=n.relu, keep_prob=kp, seed=n.seed_val)
                 if getattr(n, "pro", None) is not None:
                     b = n.pro
-                    self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd_pro, n.desc, buf[id(b.inputs[0])],
+                    self._timed(n.desc, ops.OP_FWD_PRO, ops.conv2d_fwd_pro, n.desc, buf[id(b.inputs[0])],
                                 self._prologue(b), store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
                 else:
                     self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
@@ -1289,7 +1289,7 @@ class Session:
                     else:
                         (dxb, acc), accf = dest(xb), False
                     gn, bn_ = pro.gamma.var_name, pro.beta.var_name
-                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bn, n.desc, dz,
+                    self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
                                 store.param(bn_), dxb, store.grad(gn), store.grad(bn_), pro.eps, pro.relu, accf, ws)
                     done(dxb, acc)
@@ -1307,7 +1307,7 @@ class Session:
                     drop = (c1.kp_val, c1.seed_val) if (c1 is not None and c1.kp_val is not None
                                                          and c1.kp_val < 1.0) else None
                     gn, bn_ = b.gamma.var_name, b.beta.var_name
-                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bn, n.desc, dz,
+                    self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
                                 store.param(bn_), dxb, store.grad(gn), store.grad(bn_), b.eps, b.relu, False, ws,
                                 None, drop)
@@ -1339,7 +1339,7 @@ class Session:
                 elif getattr(n, "pro", None) is not None:
                     # input relu(BN(x)) recomputed from x while staging (folded BatchNorm)
                     b = n.pro
-                    self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_pro, n.desc, buf[id(b.inputs[0])],
+                    self._timed(n.desc, ops.OP_BWD_FILTER_PRO, ops.conv2d_bwd_filter_pro, n.desc, buf[id(b.inputs[0])],
                                 self._prologue(b), dz, gw, ws, None, fused_db)
                 elif self._fused is not None and id(n) in p.adam_fusable and want_w:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
