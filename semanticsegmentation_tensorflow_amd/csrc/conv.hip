@@ -685,7 +685,7 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     p.x = x; p.w = w; p.y = y;
     p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
     if (d->dil_w == d->dil_h && seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) {
-        seg::launch_smallc_fwd(p, (hipStream_t)stream);
+        seg::launch_smallc_fwd(p, d->dtype, (hipStream_t)stream);
         SEG_CHECK_LAUNCH();
         return SEG_OK;
     }

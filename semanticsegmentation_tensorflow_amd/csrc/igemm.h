@@ -244,10 +244,10 @@ void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 // 8-input-channel first layer (smallc.hip)
 extern int g_smallc;
 bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil);
-void launch_smallc_fwd(NTParams& p, hipStream_t s);
+void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s);
 bool smallc_wgrad_ok(const TNParams& p, int dtype);
 int smallc_wgrad_splits(const TNParams& p, int cus);
-void launch_smallc_wgrad(TNParams& p, int splits, hipStream_t s);
+void launch_smallc_wgrad(TNParams& p, int dtype, int splits, hipStream_t s);
 
 // halo-tiled filter gradient (wgrad.hip) for stride-1 3x3 TN problems
 struct WgradPlan {

@@ -957,7 +957,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
             if (!ws || ws_bytes < (size_t)splits * p.Mp * p.N * sizeof(float)) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
         }
-        launch_smallc_wgrad(p, splits, s);
+        launch_smallc_wgrad(p, dt_traits<T>::id, splits, s);
         SEG_CHECK_LAUNCH();
         tn_finish(p, splits, s);
         SEG_CHECK_LAUNCH();

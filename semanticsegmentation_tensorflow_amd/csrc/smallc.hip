@@ -21,9 +21,8 @@ constexpr int SC_BH = 8, SC_BW = 64;
 constexpr int SC_HW = SC_BW + 2;                       // halo width (3x3, dilation 1)
 constexpr int SC_HROWS = (SC_BH + 2) * SC_HW;          // 660 halo pixels
 
-template <int NF>
+template <int NF, typename T>
 __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int tiles_y) {
-    using T = bf16;
     constexpr int KN = NF * 16;
     constexpr int SROW = KN + 8;                       // staged bf16 row (pad vs bank conflicts)
     __shared__ __attribute__((aligned(16))) uint4 halo[SC_HROWS + 1];    // + zero slot
@@ -87,9 +86,7 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
             const uint4 a = halo[hr];
 #pragma unroll
             for (int nf = 0; nf < NF; ++nf)
-                acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                                  __builtin_bit_cast(bf16x8, bw[ks][nf]), acc[nf],
-                                                                  0, 0, 0);
+                acc[nf] = mfma16x16x32<T>(a, bw[ks][nf], acc[nf]);
         }
         // D: lane holds rows (pixels) 4*fg + j, column n = nf*16 + fr
 #pragma unroll
@@ -100,7 +97,7 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
             for (int j = 0; j < 4; ++j) {
                 float v = acc[nf][j] + b;
                 if (e.relu) v = fmaxf(v, 0.f);
-                st[(4 * fg + j) * SROW + n] = (T)(n < e.n_valid ? v : 0.f);
+                st[(4 * fg + j) * SROW + n] = from_f32<T>(n < e.n_valid ? v : 0.f);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own wave's stage writes
@@ -125,22 +122,28 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
 int g_smallc = 1;
 
 bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil) {
-    return g_smallc && dtype == SEG_BF16 && p.C == 8 && p.K == 72 && R == 3 && S == 3 && dil == 1 && p.ish == 1 &&
+    return g_smallc && (dtype == SEG_BF16 || dtype == SEG_F16) && p.C == 8 && p.K == 72 && R == 3 && S == 3 && dil == 1 && p.ish == 1 &&
            p.isw == 1 && !p.phase && p.N % 16 == 0 && p.N <= 64 && p.N >= 16 && p.ldx == 8 &&
            p.ldy % 8 == 0 && !p.epi.residual && !p.epi.mask && !p.epi.scale && !p.epi.shift &&
            p.epi.keep_prob >= 1.f;
 }
 
-void launch_smallc_fwd(NTParams& p, hipStream_t s) {
+template <typename T>
+void launch_smallc_fwd_t(NTParams& p, hipStream_t s) {
     const int tx = (p.OW + SC_BW - 1) / SC_BW, ty = (p.OH + SC_BH - 1) / SC_BH;
     const int nimg = p.M / (p.OH * p.OW);
     const dim3 grid(nimg * tx * ty), block(256);
     switch (p.N / 16) {
-        case 1: hipLaunchKernelGGL(conv_c8_fwd<1>, grid, block, 0, s, p, tx, ty); break;
-        case 2: hipLaunchKernelGGL(conv_c8_fwd<2>, grid, block, 0, s, p, tx, ty); break;
-        case 3: hipLaunchKernelGGL(conv_c8_fwd<3>, grid, block, 0, s, p, tx, ty); break;
-        default: hipLaunchKernelGGL(conv_c8_fwd<4>, grid, block, 0, s, p, tx, ty); break;
+        case 1: hipLaunchKernelGGL((conv_c8_fwd<1, T>), grid, block, 0, s, p, tx, ty); break;
+        case 2: hipLaunchKernelGGL((conv_c8_fwd<2, T>), grid, block, 0, s, p, tx, ty); break;
+        case 3: hipLaunchKernelGGL((conv_c8_fwd<3, T>), grid, block, 0, s, p, tx, ty); break;
+        default: hipLaunchKernelGGL((conv_c8_fwd<4, T>), grid, block, 0, s, p, tx, ty); break;
     }
+}
+
+void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s) {
+    if (dtype == SEG_F16) launch_smallc_fwd_t<f16>(p, s);
+    else launch_smallc_fwd_t<bf16>(p, s);
 }
 
 
@@ -178,8 +181,8 @@ __device__ __forceinline__ void wc_glds16(const void* gsrc, unsigned lds_dst) {
 __device__ uint4 wc_zero_page[4];
 
 // N = 64 (4 n fragments); 6 tap-pair fragments: (r, 0..1), (r, 2..3*) for r = 0..2
+template <typename T>
 __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
-    using T = bf16;
     constexpr int DROWB = 128;                          // 64 dz channels
     constexpr int HBUF = WC_HPAD * 16, DBUF = WC_TP * DROWB, STAGE = HBUF + DBUF;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
         for (int ks = 0; ks < WC_TP / 32; ++ks) {
             const int kk = ks * 32 + 8 * fg + tq;                  // pixel of this lane's lo row
             const int py = kk / WC_BW, px = kk - (kk / WC_BW) * WC_BW;
-            bf16x8 af[2], bfr[3];
+            vec8_t<T> af[2], bfr[3];
             const int d1 = (((kk >> 1) & 1) << 1) | (((kk >> 3) & 1) << 2);
             const int d2 = ((((kk + 4) >> 1) & 1) << 1) | ((((kk + 4) >> 3) & 1) << 2);
 #pragma unroll
@@ -260,10 +263,10 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * (chk ^ d1) + 8 * (tpp & 1)));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * (chk ^ d2) + 8 * (tpp & 1)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                af[ni] = __builtin_bit_cast(bf16x8, v);
+                af[ni] = __builtin_bit_cast(vec8_t<T>, v);
                 if (do_bias) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) dsum[ni] += __uint_as_float((unsigned)(unsigned short)v[e] << 16);
+                    for (int e = 0; e < 8; ++e) dsum[ni] += bits16_to_f32<T>((unsigned short)v[e]);
                 }
             }
             const int hb = py * WC_HW + px;
@@ -273,13 +276,13 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + h1 * 16 + 8 * tpp));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (h1 + 4) * 16 + 8 * tpp));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bfr[i] = __builtin_bit_cast(bf16x8, v);
+                bfr[i] = __builtin_bit_cast(vec8_t<T>, v);
             }
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
-                    acc[ni][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bfr[i], acc[ni][i], 0, 0, 0);
+                    acc[ni][i] = mfma_v8<T>(af[ni], bfr[i], acc[ni][i]);
         }
         buf ^= 1;
     }
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
 }  // namespace
 
 bool smallc_wgrad_ok(const TNParams& p, int dtype) {
-    return g_smallc && dtype == SEG_BF16 && p.Cg == 8 && p.M == 72 && p.taps_w == 3 && p.ish == 1 && p.isw == 1 &&
+    return g_smallc && (dtype == SEG_BF16 || dtype == SEG_F16) && p.Cg == 8 && p.M == 72 && p.taps_w == 3 && p.ish == 1 && p.isw == 1 &&
            p.tsh == 1 && p.tsw == 1 && p.N == 64 && p.ldx == 8 && p.ldb == 64 && p.Ha > 0 && p.Wa > 0 &&
            p.P % (p.Ha * p.Wa) == 0;
 }
@@ -338,14 +341,15 @@ int smallc_wgrad_splits(const TNParams& p, int cus) {
     return (ptiles + tps - 1) / tps;
 }
 
-void launch_smallc_wgrad(TNParams& p, int splits, hipStream_t s) {
+void launch_smallc_wgrad(TNParams& p, int dtype, int splits, hipStream_t s) {
     WCGeom g;
     g.tiles_x = (p.Wa + WC_BW - 1) / WC_BW;
     g.tiles_y = (p.Ha + WC_BH - 1) / WC_BH;
     g.ptiles = (p.P / (p.Ha * p.Wa)) * g.tiles_x * g.tiles_y;
     g.tps = (g.ptiles + splits - 1) / splits;
     g.splits = splits;
-    hipLaunchKernelGGL(wgrad_c8, dim3(splits), dim3(256), 0, s, p, g);
+    if (dtype == SEG_F16) hipLaunchKernelGGL(wgrad_c8<f16>, dim3(splits), dim3(256), 0, s, p, g);
+    else hipLaunchKernelGGL(wgrad_c8<bf16>, dim3(splits), dim3(256), 0, s, p, g);
 }
 
 }  // namespace seg

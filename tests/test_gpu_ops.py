@@ -125,6 +125,16 @@ def test_conv2d_fwd_bias_relu(dev, ntv, case, dtype):
         assert y[..., K:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_first_layer_kernels_cover_16bit(dev, dtype):
+    """conv1_1 (C = 3 -> 8, 3x3) runs the small-channel kernels in both 16-bit
+    storage types (the parity of both is in the CONV_CASES / SPLIT_WGRAD_CASES
+    first-layer rows above and below)."""
+    d = ops.conv_desc(2, 19, 131, 3, 64, 3, 3, dtype=DT[dtype])
+    assert ops.conv_kernel_info(d, ops.OP_FWD)[0].startswith("conv_c8")
+    assert ops.conv_kernel_info(d, ops.OP_BWD_FILTER)[0].startswith("wgrad_c8")
+
+
 @pytest.mark.parametrize("masked", [False, True], ids=["plain", "relu_mask"])
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[7] == 1])
@@ -675,6 +685,7 @@ def test_conv2d_bwd_filter_adam_fused(dev, case, adam_tiles):
 SPLIT_WGRAD_CASES = [
     (2, 24, 40, 64, 128, 3),
     (2, 19, 131, 3, 48, 3),
+    (2, 19, 131, 3, 64, 3),     # wgrad_c8 (K = 64): ragged 4x64 tiles, split-K
     (1, 6, 9, 512, 264, 7),
     (2, 6, 9, 40, 24, 1),
 ]
