@@ -229,6 +229,26 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     // ---- epilogue: wave tile -> LDS (fp32), then 8 columns x one row per lane
     constexpr int SROW = WTN * 4 + 16;
     static_assert(NW * WTM * SROW <= SMEM, "epilogue staging must fit");
+    constexpr int CPR = WTN / 8;
+    constexpr int RPP = 64 / CPR, NRR = WTM / RPP;
+    const int cch = lane % CPR, rsub = lane / CPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
+    const EpiParams& e = p.epi;
+    // 16-bit ReluGrad mask rows of this lane, requested before the staging
+    uint4 mkv[NRR];
+    if constexpr (sizeof(T) == 2) {
+        if (e.mask) {
+#pragma unroll
+            for (int k = 0; k < NRR; ++k) {
+                const int ml = wm * WTM + rsub + k * RPP;
+                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+                mkv[k] = uint4{0u, 0u, 0u, 0u};
+                if (oy < p.OH && ox < p.OW && col0 < p.N)
+                    mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
+                                                             ((long)oy * p.OW + ox) * e.ld_mask + col0);
+            }
+        }
+    }
     lds_barrier();
     char* wbuf = smem + w * WTM * SROW;
 #pragma unroll
@@ -239,11 +259,6 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             for (int ni = 0; ni < TN; ++ni)
                 *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) = acc[mi][ni][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    constexpr int CPR = WTN / 8;
-    constexpr int RPP = 64 / CPR;
-    const int cch = lane % CPR, rsub = lane / CPR;
-    const int col0 = n0 + wn * WTN + cch * 8;
-    const EpiParams& e = p.epi;
     float bias[8], scl[8], shf[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -253,8 +268,9 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
-#pragma unroll 2
-    for (int rr = rsub; rr < WTM; rr += RPP) {
+#pragma unroll
+    for (int k = 0; k < NRR; ++k) {
+        const int rr = rsub + k * RPP;
         const int ml = wm * WTM + rr;
         const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
         if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
@@ -264,9 +280,13 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         float res[8], mk[8];
         if (e.mask) {
-            const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
-            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
-            if constexpr (sizeof(T) == 4) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
+            if constexpr (sizeof(T) == 2) {
+                Chunk<T>::unpack(mkv[k], mk);
+            } else {
+                const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp + 4), mk + 4);
+            }
         }
         if (e.residual) {
             const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
@@ -549,6 +569,22 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
     char* wbuf = smem + w * 64 * SROW;
+    // ReluGrad mask rows: the first half's requested before its staging, the
+    // second half's row by row as the first half's are consumed
+    constexpr int NRR = 64 / RPP;
+    uint4 mkv[NRR];
+    auto load_mask = [&](int mh, int k) {
+        const int ml = wm * 128 + mh * 64 + rsub + k * RPP;
+        const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+        mkv[k] = uint4{0u, 0u, 0u, 0u};
+        if (oy < p.OH && ox < p.OW && col0 < p.N)
+            mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
+                                                     ((long)oy * p.OW + ox) * e.ld_mask + col0);
+    };
+    if (e.mask) {
+#pragma unroll
+        for (int k = 0; k < NRR; ++k) load_mask(0, k);
+    }
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
         lds_barrier();
@@ -561,20 +597,22 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                     *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
                         acc[mh * 4 + mi][ni][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll 2
-        for (int rr = rsub; rr < 64; rr += RPP) {
+#pragma unroll
+        for (int k = 0; k < NRR; ++k) {
+            const int rr = rsub + k * RPP;
             const int ml = wm * 128 + mh * 64 + rr;
             const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+            float mk[8];
+            if (e.mask) {
+                Chunk<T>::unpack(mkv[k], mk);
+                if (mh == 0) load_mask(1, k);
+            }
             if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
             const long pix = (long)oy * p.OW + ox;
             const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
             const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
             float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-            float res[8], mk[8];
-            if (e.mask) {
-                const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
-                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(mp), mk);
-            }
+            float res[8];
             if (e.residual) {
                 const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
@@ -704,6 +742,28 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
     __syncthreads();
     for (; t < ntiles; t += gridDim.x) {
         const int tn = t + gridDim.x;
+        // ReluGrad mask of this tile (the input gradient's epilogue), requested
+        // before the next tile's halo so the epilogue waits only for it
+        uint2 mpre[TM][TN];
+        if (e.mask) {
+            const int img = t / tpi;
+            const int rem = t - img * tpi;
+            const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int ml = wm * WTM + mi * 16 + fr;
+                const int oy = ty * R64_BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
+                const bool ok = oy < p.OH && ox < p.OW;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int col0 = wn * WTN + ni * 16 + 4 * fg;
+                    mpre[mi][ni] = uint2{0u, 0u};
+                    if (ok && col0 < p.N)
+                        mpre[mi][ni] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
+                                                                       ((long)oy * p.OW + ox) * e.ld_mask + col0);
+                }
+            }
+        }
         if (tn < ntiles) fetch(tn);                  // in flight during this tile's MFMAs
         f32x4 acc[TM][TN];
 #pragma unroll
@@ -769,9 +829,9 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                     if (col0 >= p.N) continue;
                     float mk[4] = {1.f, 1.f, 1.f, 1.f}, res[4] = {0.f, 0.f, 0.f, 0.f};
                     if (e.mask) {
-                        const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
+                        const unsigned short* mh = reinterpret_cast<const unsigned short*>(&mpre[mi][ni]);
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) mk[j] = to_f32(mp[j]);
+                        for (int j = 0; j < 4; ++j) mk[j] = bits16_to_f32<T>(mh[j]);
                     }
                     if (e.residual) {
                         const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
@@ -1201,7 +1261,8 @@ bool res64_ok(const NTParams& p, int dtype) {
     return g_res64 && g_nt_halo && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.ish == 1 && p.isw == 1 && p.osh == 1 &&
            p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.Ha == p.OH && p.Wa == p.OW && p.C == 64 && p.K == 9 * 64 &&
            p.taps_w == 3 && (p.tsh == 1 || p.tsh == -1) && (p.tsw == 1 || p.tsw == -1) && p.N <= 64 &&
-           p.N % 8 == 0 && p.OH > 0 && p.OW > 0 && p.M % (p.OH * p.OW) == 0;
+           p.N % 8 == 0 && p.OH > 0 && p.OW > 0 && p.M % (p.OH * p.OW) == 0 &&
+           (!p.epi.mask || ((uintptr_t)p.epi.mask % 8 == 0 && p.epi.ld_mask % 4 == 0 && p.epi.mask_img % 4 == 0));
 }
 
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
