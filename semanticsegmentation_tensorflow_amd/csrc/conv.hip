@@ -568,6 +568,16 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_stagger_us = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "nt3_stag")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_nt3_stag = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "tn3_stag")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_tn3_stag = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "tn3_half")) {
         if (value < 0 || value > 7) return SEG_EINVAL;
         seg::g_tn3_half = value;

@@ -509,15 +509,24 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             mma(0, 0);
             mma(0, 1);
             __builtin_amdgcn_s_barrier();
-            // h1: A1, halo piece; slice it+1 must land before the next h0
+            // h1: A1, halo piece; slice it+1 must land before the next h0.
+            // Staggered groups wait one barrier early (the lagging group reads
+            // after the leading group's next barrier): half an iteration for
+            // the slice to land; unstaggered, the wait closes the iteration.
             read_a(1);
             const bool hp = ABL != 1 && tap < h_n && kc + 1 < kc_end;
             if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
-            if (hp) wait_vmcnt<1>();
-            else wait_vmcnt<0>();
+            if constexpr (STAG) {
+                if (hp) wait_vmcnt<1>();
+                else wait_vmcnt<0>();
+            }
             __builtin_amdgcn_s_barrier();
             mma(1, 1);
             mma(1, 0);
+            if constexpr (!STAG) {
+                if (hp) wait_vmcnt<1>();
+                else wait_vmcnt<0>();
+            }
             __builtin_amdgcn_s_barrier();
         }
         bbuf ^= 1;
@@ -1298,8 +1307,13 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
     if (dtype == SEG_F16) {   // half: the production schedules only
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
         if (hp.bn == 256) {
-            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
-            else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+            if (g_halo_stagger) {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+            } else {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, false, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
+            }
             return;
         }
         switch (hp.bw * 10 + hp.hi) {
@@ -1327,8 +1341,13 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
             return;
         }
         if (g_halo_phases == 2) {
-            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2>), grid, dim3(512), 0, s, p, g);
-            else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_halo_stagger) {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2>), grid, dim3(512), 0, s, p, g);
+            } else {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false, 0, 2>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, false, 0, 2>), grid, dim3(512), 0, s, p, g);
+            }
             return;
         }
         if (g_halo_stagger) {

@@ -211,6 +211,8 @@ bool nt4_ok(const NTParams& p, int dtype);
 void nt4_info(int M, int N, int K, int cus, int* splits);
 void launch_nt4(NTParams& p, int gridz, int max_m, hipStream_t s);
 extern int g_tn3_stagger_us;
+extern int g_tn3_stag;
+extern int g_nt3_stag;
 bool tn3_ok(const TNParams& p, int dtype);
 inline bool tn3_applies(int M, int N, int dtype) { return g_tn3 && dtype == SEG_BF16 && M >= 256 && N > 128; }
 void tn3_info(int M, int N, int P, int cus, int* splits);

@@ -26,6 +26,7 @@
 namespace seg {
 
 int g_nt3 = 1;
+int g_nt3_stag = 1;     // wave-group stagger (0: unstaggered, DMA wait a full iteration after issue)
 __device__ uint4 g_nt3_zero[4];
 
 template <bool STAG>
@@ -223,14 +224,20 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         // then A(t+1) and B(t+1) must have landed before the next h0
         read_a(1);
         const int anext = abuf == 0 ? 2 : abuf - 1;   // (abuf + 2) % 3
-        if (it + 2 < nk) {
-            issue_a(anext);
-            wait_vmcnt<A_INS>();
-        } else {
-            wait_vmcnt<0>();
+        if (it + 2 < nk) issue_a(anext);
+        // staggered: the wait precedes the barrier the lagging group passes
+        // before its next reads (half an iteration for B(t+1) to land);
+        // unstaggered: right before the iteration's last barrier
+        if constexpr (STAG) {
+            if (it + 2 < nk) wait_vmcnt<A_INS>();
+            else wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
         mma(1);
+        if constexpr (!STAG) {
+            if (it + 2 < nk) wait_vmcnt<A_INS>();
+            else wait_vmcnt<0>();
+        }
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
         bbuf ^= 1;
@@ -340,7 +347,8 @@ bool nt3_ok(const NTParams& p, int dtype) {
 
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + 255) / 256) * ((p.N + 255) / 256);
-    hipLaunchKernelGGL((igemm_nt3<true>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    if (g_nt3_stag) hipLaunchKernelGGL((igemm_nt3<true>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((igemm_nt3<false>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
 }
 
 
@@ -357,11 +365,18 @@ __device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((r
 
 int g_tn3 = 1;
 int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
-int g_tn3_mfast = 0;
+int g_tn3_mfast = 0;       // tile order: M fastest when the B (dy) panel is the larger operand
 int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split
 int g_tn3_stagger_us = 40;  // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
+// Wave-group stagger in the main loop.  Off: the DMA wait for slice t+1 moves
+// from before h1 to the end of the iteration, a full iteration after its
+// issue instead of half of one.  The dy / x slices of a filter gradient miss
+// L2 far more often than a forward conv's filter slices, so here the longer
+// window beats the MFMA / LDS-read overlap (conv6 main loop 445 -> 307 us),
+// while conv_halo2 and igemm_nt3 stay staggered (measured slower without).
+int g_tn3_stag = 0;
 __device__ int g_tn3_cu_slots[4096];
-int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue   // tile order: M fastest when the B (dy) panel is the larger operand
+int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue
 
 // ABL: see g_tn3_abl.  MFAST: consecutive tiles walk M (share the dy panel).
 // ADAM: TF1 Adam on the parameters of the tile (p.adam) instead of (or besides)
@@ -582,22 +597,35 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         __builtin_amdgcn_s_barrier();
         read_a(1);
         const int anext = abuf == 0 ? 2 : abuf - 1;
-        if (ABL != 1 && it + 2 < nk) {
-            issue_a(anext);
-            wait_vmcnt<A_INS>();
-        } else {
-            wait_vmcnt<0>();
+        const bool more = ABL != 1 && it + 2 < nk;
+        if (more) issue_a(anext);
+        // Staggered groups: a wave's DMA wait must precede a barrier that the
+        // OTHER group passes before reading the data, i.e. one barrier early,
+        // leaving slice it+1 half an iteration to land.  Unstaggered: the wait
+        // sits right before the iteration's last barrier (a full iteration).
+        if constexpr (STAG) {
+            if (more) wait_vmcnt<A_INS>();
+            else wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(1);
         else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]) : "memory");
+        if constexpr (!STAG) {
+            if (more) wait_vmcnt<A_INS>();
+            else wait_vmcnt<0>();
+        }
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
         bbuf ^= 1;
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
-    if (ABL == 3) {
-        if (acc[0][0][0] == 12345.f && acc[7][3][3] == 54321.f) p.out[tid] = acc[3][1][2];
+    if (ABL == 3) {   // every accumulator feeds the (never taken) store: no MFMA is dead code
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (sum == 12345.f) p.out[tid] = sum;
         return;
     }
 
@@ -801,6 +829,17 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s) {
             p.adam.stagger = 0;
         }
 #define TN3H(MF, AD) hipLaunchKernelGGL((igemm_tn3<true, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
+#define TN3HU(MF, AD) hipLaunchKernelGGL((igemm_tn3<false, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
+        if (!g_tn3_stag) {
+            if (p.adam.p) {
+                if (mfast) TN3HU(true, true);
+                else TN3HU(false, true);
+            } else {
+                if (mfast) TN3HU(true, false);
+                else TN3HU(false, false);
+            }
+            return;
+        }
         if (p.adam.p) {
             if (mfast) TN3H(true, true);
             else TN3H(false, true);
@@ -808,6 +847,7 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s) {
             if (mfast) TN3H(true, false);
             else TN3H(false, false);
         }
+#undef TN3HU
 #undef TN3H
         return;
     }
@@ -815,6 +855,22 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s) {
     const dim3 g(tm * tn * splits), b(512);
     const bool mfast = g_tn3_mfast && tm > tn;
 #define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<true, A, MF>), g, b, 0, s, p, tm, tn, splits)
+#define TN3U(A, MF) hipLaunchKernelGGL((igemm_tn3<false, A, MF>), g, b, 0, s, p, tm, tn, splits)
+    if (!g_tn3_stag) {
+        switch (g_tn3_abl) {
+            case 1: TN3U(1, false); return;
+            case 2: TN3U(2, false); return;
+            case 3: TN3U(3, false); return;
+        }
+        if (p.adam.p) {
+            if (mfast) hipLaunchKernelGGL((igemm_tn3<false, 0, true, true>), g, b, 0, s, p, tm, tn, splits);
+            else hipLaunchKernelGGL((igemm_tn3<false, 0, false, true>), g, b, 0, s, p, tm, tn, splits);
+            return;
+        }
+        if (mfast) TN3U(0, true);
+        else TN3U(0, false);
+        return;
+    }
     switch (g_tn3_abl) {
         case 1: TN3(1, false); return;
         case 2: TN3(2, false); return;
@@ -827,6 +883,7 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s) {
     }
     if (mfast) TN3(0, true);
     else TN3(0, false);
+#undef TN3U
 #undef TN3
 }
 

@@ -24,8 +24,8 @@ def ntv(request, dev):
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
     (bf16, stride 1, C % 64 == 0; 256x256 four-phase tiles for N > 128),
     4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
-    stagger (two-phase schedule), 6 = 3 with four phases per iteration,
-    7 = 3 with the two-phase kernel also for N <= 128 (off by default),
+    stagger (two-phase schedule; igemm_nt3 too: DMA waits at the iteration
+    end), 6 = 3 with four phases per iteration, 7 = 3 with the two-phase kernel also for N <= 128 (off by default),
     8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
     (by default only where its grid fills half the CUs; variant 2 keeps it
     off so igemm_nt2 stays covered for wide N), 9 = 8 with the four-wave
@@ -38,6 +38,7 @@ def ntv(request, dev):
     ops.set_option("nt3", 0 if v == 2 else 1)
     ops.set_option("halo_wide", 0 if v == 4 else 1)
     ops.set_option("halo_stagger", 0 if v == 5 else 1)
+    ops.set_option("nt3_stag", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
     ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
@@ -52,6 +53,7 @@ def ntv(request, dev):
     ops.set_option("nt3", 1)
     ops.set_option("halo_wide", 1)
     ops.set_option("halo_stagger", 1)
+    ops.set_option("nt3_stag", 1)
     ops.set_option("halo_phases", 2)
     ops.set_option("halo2_n128", 0)
 
@@ -165,8 +167,8 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
-                                                      "wgrad-nbias4", "tn3-half", "wgrad-la1"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                         "wgrad-nbias4", "tn3-half", "wgrad-la1", "tn3-stag"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
@@ -176,7 +178,8 @@ def tnv(request, dev):
     BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5 with
     the 256x128 two-blocks-per-CU tiles also for plain single-split launches,
     8 = 4 with the per-fragment index arithmetic instead of packed per-lane
-    LDS offsets (wgrad_la 1 vs the default 3)."""
+    LDS offsets (wgrad_la 1 vs the default 3), 9 = 5 with the wave-group
+    staggered main loop (DMA wait one barrier early; off by default)."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
     ops.set_option("wgrad_halo", 1 if v in (3, 4, 6, 8) else 0)
@@ -185,7 +188,9 @@ def tnv(request, dev):
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
     ops.set_option("tn3_half", 7 if v == 7 else 1)
+    ops.set_option("tn3_stag", 1 if v == 9 else 0)
     yield v
+    ops.set_option("tn3_stag", 0)
     ops.set_option("wgrad_la", 3)
     ops.set_option("tn3_half", 1)
     ops.set_option("tn3", 1)

@@ -13,7 +13,9 @@ ws = ops.Workspace(dev)
 SHAPES = [("conv6", 12, 39, 512, 4096, 7), ("conv7", 12, 39, 4096, 4096, 1)]
 MODES = [("tn2", {"tn3": 0}), ("tn3-nfast", {"tn3": 1, "tn3_mfast": 0}), ("tn3-mfast", {"tn3": 1, "tn3_mfast": 1}),
          ("abl-noDMA", {"tn3": 1, "tn3_abl": 1}), ("abl-noMFMA", {"tn3": 1, "tn3_abl": 2}),
-         ("abl-noEpi", {"tn3": 1, "tn3_abl": 3})]
+         ("abl-noEpi", {"tn3": 1, "tn3_abl": 3}),
+         ("tn3-unstag", {"tn3": 1, "tn3_stag": 0}), ("unstag-noDMA", {"tn3": 1, "tn3_stag": 0, "tn3_abl": 1}),
+         ("unstag-noEpi", {"tn3": 1, "tn3_stag": 0, "tn3_abl": 3})]
 
 
 def timeit(fn, reps=10):
@@ -43,5 +45,6 @@ for name, H, W, C, K, R in SHAPES:
         t = min(timeit(lambda: ops.conv2d_bwd_filter(d, x, dy, dw, ws)) for _ in range(3))
         print(f"{name:6s} {mname:12s} {t * 1e3:8.1f} us  {gf / t:8.1f} TF/s  {ops.conv_kernel_info(d, 2)[0]}")
         ops.set_option("tn3_abl", 0)
+        ops.set_option("tn3_stag", 1)
         ops.set_option("tn3_mfast", 1)
         ops.set_option("tn3", 1)
