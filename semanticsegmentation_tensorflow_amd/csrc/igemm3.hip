@@ -207,6 +207,46 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                             acc[mh * 4 + mi][ni], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
         };
+        if constexpr (!STAG) {
+            // unstaggered: one barrier per iteration (every DMA target was last
+            // read in an earlier iteration; slice t+1 waited for at the end)
+            read_a(0);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int row = wn * WTN + ni * 16 + fr;
+                    bq[ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                }
+            if (it + 1 < nk) issue_b(bbuf ^ 1);
+            if (it + 2 < nk) issue_a(abuf == 0 ? 2 : abuf - 1);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[ks][ni]), acc[mi][ni], 0, 0, 0);
+            read_a(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[ks][ni]), acc[4 + mi][ni],
+                            0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (it + 2 < nk) wait_vmcnt<A_INS>();
+            else wait_vmcnt<0>();
+            lds_barrier();
+            abuf = abuf == 2 ? 0 : abuf + 1;
+            bbuf ^= 1;
+            continue;
+        }
         // h0: A half 0 + B slice; B(t+1) into the other B buffer (last read at h0(t-1))
         read_a(0);
 #pragma unroll
@@ -395,7 +435,10 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
     constexpr int A_INS = BKP / RPI / NW, B_INS = BKP / RPIB / NW;
     constexpr int KS = BKP / 32;
     constexpr int ABUF = BKP * ROWB, BBUF = BKP * ROWBB;
-    constexpr int RING = 3 * ABUF + 2 * BBUF;
+    // B (dy) ring depth: 3 stages for the unstaggered half tile (B(t+2) issued
+    // at t, two iterations to land; its 32-deep iterations are short), else 2
+    constexpr int BST = (BN == 128 && !STAG) ? 3 : 2;
+    constexpr int RING = 3 * ABUF + BST * BBUF;
     constexpr int EPI = ADAM ? NW * (32 * (WTN * 4 + 16) + WTN * (32 * 2 + 16)) : NW * 64 * (WTN * 4 + 16);
     constexpr int SMEM = RING > EPI ? RING : EPI;
     static_assert(A_INS * NW * RPI == BKP && B_INS * NW * RPIB == BKP, "DMA pieces must tile the stage");
@@ -528,7 +571,12 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         issue_b(0);
         if (nk > 1) {
             issue_a(1);
-            wait_vmcnt<A_INS>();
+            if constexpr (BST == 3) {
+                issue_b(1);
+                wait_vmcnt<A_INS + B_INS>();
+            } else {
+                wait_vmcnt<A_INS>();
+            }
         } else {
             wait_vmcnt<0>();
         }
@@ -585,12 +633,69 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
                                                                                        acc[mh * 4 + mi][ni], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
         };
+        if constexpr (!STAG && ABL == 0) {
+            // Unstaggered: ONE barrier per iteration.  Every buffer a DMA of
+            // this iteration writes was last read in an earlier iteration (the
+            // previous end barrier retired those reads), and slice t+1 is
+            // waited for right before this iteration's barrier.  All fragment
+            // reads are issued up front; the first half's MFMAs wait only for
+            // their own reads (the compiler counts lgkmcnt), the second half's
+            // A reads stay in flight beneath them.
+            // (64-deep full tiles: no room for both A halves, the second is
+            // read after the first half's MFMAs)
+            constexpr int KS1 = KS == 1 ? 1 : 0;
+            bf16x8 af1[KS1 ? KS : 1][4];
+            read_a(0);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, ROWBB, boff[ni], ks);
+            if constexpr (KS1) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) af1[0][mi] = frag(As, ROWB, aoff[1][mi], 0);
+            }
+            if constexpr (BST == 3) {
+                if (it + 2 < nk) issue_b(bbuf == 0 ? 2 : bbuf - 1);
+            } else {
+                if (it + 1 < nk) issue_b(bbuf ^ 1);
+            }
+            const bool more = it + 2 < nk;
+            if (more) issue_a(abuf == 0 ? 2 : abuf - 1);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][mi], bq[ks][ni], acc[mi][ni], 0, 0, 0);
+            if constexpr (!KS1) read_a(1);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(KS1 ? af1[0][mi] : af[ks][mi], bq[ks][ni],
+                                                                                  acc[4 + mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (more) wait_vmcnt<BST == 3 ? A_INS + B_INS : A_INS>();
+            else wait_vmcnt<0>();
+            lds_barrier();
+            abuf = abuf == 2 ? 0 : abuf + 1;
+            bbuf = bbuf == BST - 1 ? 0 : bbuf + 1;
+            continue;
+        }
         read_a(0);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) bq[ks][ni] = frag(Bs, ROWBB, boff[ni], ks);
-        if (ABL != 1 && it + 1 < nk) issue_b(bbuf ^ 1);
+        if constexpr (BST == 3) {
+            if (ABL != 1 && it + 2 < nk) issue_b(bbuf == 0 ? 2 : bbuf - 1);
+        } else {
+            if (ABL != 1 && it + 1 < nk) issue_b(bbuf ^ 1);
+        }
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(0);
         else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]), "v"(bq[0][0]), "v"(bq[KS - 1][3]) : "memory");
@@ -611,12 +716,13 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         if (ABL != 2) mma(1);
         else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]) : "memory");
         if constexpr (!STAG) {
-            if (more) wait_vmcnt<A_INS>();
+            // newest: B(t+2) (3-stage B ring) and A(t+2); A(t+1), B(t+1) landed
+            if (more) wait_vmcnt<BST == 3 ? A_INS + B_INS : A_INS>();
             else wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
-        bbuf ^= 1;
+        bbuf = bbuf == BST - 1 ? 0 : bbuf + 1;
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
     if (ABL == 3) {   // every accumulator feeds the (never taken) store: no MFMA is dead code

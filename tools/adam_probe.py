@@ -9,6 +9,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from semanticsegmentation_tensorflow_amd import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
+for kv in filter(None, os.environ.get("PROBE_OPTS", "").split(",")):   # e.g. PROBE_OPTS=tn3_mfast=1
+    k, v = kv.split("=")
+    ops.set_option(k, int(v))
 ws = ops.Workspace(dev)
 SHAPES = [("conv6", 12, 39, 512, 4096, 7), ("conv7", 12, 39, 4096, 4096, 1)]
 HALF = [int(h) for h in os.environ.get("PROBE_HALF", "1").split(",")]
