@@ -953,7 +953,7 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.abl = seg::g_tn3_adam_abl;
     p.Mp = p.M;
     p.partial = nullptr;
-    seg::launch_tn3(p, 1, (hipStream_t)stream);
+    seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
     SEG_CHECK_LAUNCH();
     if (tr_after) {
         const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;

@@ -196,9 +196,9 @@ bool nt2_pro_ok(const NTParams& p, int dtype, int nphases);
 void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s);
 void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype);
 
-inline bool nt3_applies(int N, int dtype) { return g_nt3 && dtype == SEG_BF16 && N > 128; }
+inline bool nt3_applies(int N, int dtype) { return g_nt3 && (dtype == SEG_BF16 || dtype == SEG_F16) && N > 128; }
 void nt3_info(int M, int N, int K, int cus, int* splits);
-void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s);
+void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype);
 extern int g_tn3;
 extern int g_tn3_abl;
 extern int g_tn3_mfast;
@@ -214,9 +214,11 @@ extern int g_tn3_stagger_us;
 extern int g_tn3_stag;
 extern int g_nt3_stag;
 bool tn3_ok(const TNParams& p, int dtype);
-inline bool tn3_applies(int M, int N, int dtype) { return g_tn3 && dtype == SEG_BF16 && M >= 256 && N > 128; }
+inline bool tn3_applies(int M, int N, int dtype) {
+    return g_tn3 && (dtype == SEG_BF16 || dtype == SEG_F16) && M >= 256 && N > 128;
+}
 void tn3_info(int M, int N, int P, int cus, int* splits);
-void launch_tn3(TNParams& p, int splits, hipStream_t s);
+void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype);
 bool tn3_adam_ok(const TNParams& p, int dtype);
 
 // halo-tiled direct conv (halo.hip) for stride-1 NT problems

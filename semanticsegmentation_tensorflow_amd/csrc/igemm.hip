@@ -692,8 +692,8 @@ int g_nt3_fill = 1;
 // 256x256 tiles only when the launch (tiles x splits x phases) fills at least
 // half the CUs; narrow problems (phased conv2d_transpose, K <= 6 k-tiles) run
 // more, smaller blocks on igemm_nt2 instead.
-static bool nt3_pick(const NTParams& p, int nphases, int max_m) {
-    if (!nt3_ok(p, SEG_BF16)) return false;
+static bool nt3_pick(const NTParams& p, int dtype, int nphases, int max_m) {
+    if (!nt3_ok(p, dtype)) return false;
     // one or two k tiles: the 2-stage igemm_nt2 (two blocks per CU) wins
     if (g_nt3_fill && g_nt2_short >= 2 && p.K <= 128) return false;
     if (!g_nt3_fill) return true;
@@ -777,8 +777,8 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         }
         return SEG_OK;
     }
-    const bool nt3 = is_bf16_v<T> && g_nt_variant == 2 && nt3_pick(p, nphases, max_m);
-    const bool nt4 = nt3 && nt4_ok(p, SEG_BF16);
+    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, dt_traits<T>::id, nphases, max_m);
+    const bool nt4 = nt3 && is_bf16_v<T> && nt4_ok(p, SEG_BF16);
     if (nt4) {
         nt4_info(max_m, p.N, p.K, num_cus(), &splits);
         if (nphases > 1) splits = 1;
@@ -798,7 +798,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         gridz = splits;
     }
     if (nt4) launch_nt4(p, gridz, max_m, s);
-    else if (nt3) launch_nt3(p, gridz, max_m, s);
+    else if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
     else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
@@ -830,8 +830,8 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
         *bm = 256; *bn = hp.bn; *splits = hp.splits;
         return "conv_halo";
     }
-    if (dtype == SEG_BF16 && g_nt_variant == 2 && nt3_pick(p, nphases, max_m)) {
-        const bool nt4 = nt4_ok(p, SEG_BF16);
+    if ((dtype == SEG_BF16 || dtype == SEG_F16) && g_nt_variant == 2 && nt3_pick(p, dtype, nphases, max_m)) {
+        const bool nt4 = dtype == SEG_BF16 && nt4_ok(p, SEG_BF16);
         if (nt4) nt4_info(max_m, p.N, p.K, num_cus(), splits);
         else nt3_info(max_m, p.N, p.K, num_cus(), splits);
         if (nphases > 1) *splits = 1;
@@ -980,7 +980,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     }
     int bm, bn, splits;
     choose_tn(p.M, p.N, p.P, BKP, sizeof(T) == 2, bm, bn, splits);
-    const bool tn3 = is_bf16_v<T> && g_tn_variant == 2 && tn3_ok(p, SEG_BF16);
+    const bool tn3 = sizeof(T) == 2 && g_tn_variant == 2 && tn3_ok(p, dt_traits<T>::id);
     if (tn3) tn3_info(p.M, p.N, p.P, num_cus(), &splits);
     int gridz = 1;
     if (splits > 1) {
@@ -993,7 +993,7 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         gridz = splits;
     }
     if (tn3) {
-        launch_tn3(p, gridz, s);
+        launch_tn3(p, gridz, s, dt_traits<T>::id);
     } else if (g_tn_variant == 2 && sizeof(T) == 2 && (bm == 256 || bn == 256 || p.M >= 128 || g_tn2_smallm)) {
         launch_tn2(p, bm, bn, gridz, s, dt_traits<T>::id);
     } else if (bm == 64 && bn == 64) launch_tn_t<T, 64, 64>(p, gridz, s);

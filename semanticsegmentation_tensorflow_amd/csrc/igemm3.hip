@@ -29,9 +29,8 @@ int g_nt3 = 1;
 int g_nt3_stag = 1;     // wave-group stagger (0: unstaggered, DMA wait a full iteration after issue)
 __device__ uint4 g_nt3_zero[4];
 
-template <bool STAG>
+template <bool STAG, typename T = bf16>
 __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
-    using T = bf16;
     constexpr int NW = 8, BM = 256, BN = 256, BK = 64;
     constexpr int WTM = 128, WTN = 64, TN = WTN / 16;   // TM = 8 (two halves of 4)
     constexpr int A_INS = BM / 8 / NW, B_INS = BN / 8 / NW;   // 4 + 4 DMA pieces per wave per tile
@@ -202,9 +201,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[mh * 4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[ks][ni]),
-                            acc[mh * 4 + mi][ni], 0, 0, 0);
+                        acc[mh * 4 + mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[mh * 4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
         };
         if constexpr (!STAG) {
@@ -227,8 +224,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[ks][ni]), acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[mi][ni]);
             read_a(1);
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -236,9 +232,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[ks][mi]), __builtin_bit_cast(bf16x8, bq[ks][ni]), acc[4 + mi][ni],
-                            0, 0, 0);
+                        acc[4 + mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
             if (it + 2 < nk) wait_vmcnt<A_INS>();
             else wait_vmcnt<0>();
@@ -382,13 +376,19 @@ void nt3_info(int M, int N, int K, int cus, int* splits) {
 }
 
 bool nt3_ok(const NTParams& p, int dtype) {
-    return g_nt3 && dtype == SEG_BF16 && p.N > 128;
+    return g_nt3 && (dtype == SEG_BF16 || dtype == SEG_F16) && p.N > 128;
 }
 
-void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s) {
+template <typename T>
+static void launch_nt3_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + 255) / 256) * ((p.N + 255) / 256);
-    if (g_nt3_stag) hipLaunchKernelGGL((igemm_nt3<true>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((igemm_nt3<false>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    if (g_nt3_stag) hipLaunchKernelGGL((igemm_nt3<true, T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((igemm_nt3<false, T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+}
+
+void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype) {
+    if (dtype == SEG_F16) launch_nt3_t<f16>(p, gridz, max_m, s);
+    else launch_nt3_t<bf16>(p, gridz, max_m, s);
 }
 
 
@@ -425,9 +425,9 @@ int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4
 // 128 / 32 is the half tile (4 waves, 64 KiB rings + 68 KiB epilogue staging)
 // that runs two blocks per CU, so one block's HBM-bound epilogue (the fused
 // Adam) overlaps the other block's MFMA main loop.
-template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false, int BN = 256, int BKP = 64>
+template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false, int BN = 256, int BKP = 64, typename T = bf16>
 __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, int tiles_n, int splits) {
-    using T = bf16;
+    static_assert(!ADAM || is_bf16_v<T>, "the fused Adam epilogue writes bf16 weight copies");
     constexpr int BM = 256, WTM = 128, WTN = 64, TN = WTN / 16;
     constexpr int NWN = BN / WTN, NW = 2 * NWN;                      // waves: 2 (M) x NWN (N)
     constexpr int ROWB = BM * 2, RPI = 1024 / ROWB, CPR = ROWB / 16; // A: 2 rows / DMA piece, 32 chunks / row
@@ -605,14 +605,14 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
     for (int it = 0; it < nk; ++it) {
         SEG_LDS char* As = (SEG_LDS char*)smem + abuf * ABUF;
         SEG_LDS char* Bs = (SEG_LDS char*)smem + 3 * ABUF + bbuf * BBUF;
-        bf16x8 af[KS][4], bq[KS][TN];
+        vec8_t<T> af[KS][4], bq[KS][TN];
         // 16 columns x 32 pixel rows fragment at lane offset `off`, k rows ks*32 ..
         auto frag = [&](SEG_LDS char* base, int rowb, unsigned off, int ks) {
             SEG_LDS char* a = base + off + ks * 32 * rowb;
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)a);
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(a + 4 * rowb));
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            return __builtin_bit_cast(bf16x8, v);
+            return __builtin_bit_cast(vec8_t<T>, v);
         };
         auto read_a = [&](int mh) {
 #pragma unroll
@@ -629,8 +629,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[mh * 4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][mi], bq[ks][ni],
-                                                                                       acc[mh * 4 + mi][ni], 0, 0, 0);
+                        acc[mh * 4 + mi][ni] = mfma_v8<T>(af[ks][mi], bq[ks][ni], acc[mh * 4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
         };
         if constexpr (!STAG && ABL == 0) {
@@ -644,7 +643,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
             // (64-deep full tiles: no room for both A halves, the second is
             // read after the first half's MFMAs)
             constexpr int KS1 = KS == 1 ? 1 : 0;
-            bf16x8 af1[KS1 ? KS : 1][4];
+            vec8_t<T> af1[KS1 ? KS : 1][4];
             read_a(0);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
@@ -668,7 +667,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][mi], bq[ks][ni], acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = mfma_v8<T>(af[ks][mi], bq[ks][ni], acc[mi][ni]);
             if constexpr (!KS1) read_a(1);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
@@ -676,8 +675,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(KS1 ? af1[0][mi] : af[ks][mi], bq[ks][ni],
-                                                                                  acc[4 + mi][ni], 0, 0, 0);
+                        acc[4 + mi][ni] = mfma_v8<T>(KS1 ? af1[0][mi] : af[ks][mi], bq[ks][ni], acc[4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
             if (more) wait_vmcnt<BST == 3 ? A_INS + B_INS : A_INS>();
             else wait_vmcnt<0>();
@@ -902,7 +900,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
     }
 }
 
-bool tn3_ok(const TNParams& p, int dtype) { return g_tn3 && dtype == SEG_BF16 && p.M >= 256 && p.N > 128; }
+bool tn3_ok(const TNParams& p, int dtype) { return tn3_applies(p.M, p.N, dtype); }
 
 void tn3_info(int M, int N, int P, int cus, int* splits) {
     const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
@@ -916,8 +914,21 @@ void tn3_info(int M, int N, int P, int cus, int* splits) {
     *splits = s;
 }
 
-void launch_tn3(TNParams& p, int splits, hipStream_t s) {
+void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {
     const int tm = (p.M + 255) / 256;
+    if (dtype == SEG_F16) {   // half storage: plain filter gradients only (loss scaling keeps Adam separate)
+        if (splits == 1 && (g_tn3_half & 2)) {
+            const int tn = (p.N + 127) / 128;
+            if (g_tn3_stag) hipLaunchKernelGGL((igemm_tn3<true, 0, false, false, 128, 32, f16>), dim3(tm * tn), dim3(256), 0, s, p, tm, tn, 1);
+            else hipLaunchKernelGGL((igemm_tn3<false, 0, false, false, 128, 32, f16>), dim3(tm * tn), dim3(256), 0, s, p, tm, tn, 1);
+            return;
+        }
+        const int tn = (p.N + 255) / 256;
+        const dim3 g(tm * tn * splits);
+        if (g_tn3_stag) hipLaunchKernelGGL((igemm_tn3<true, 0, false, false, 256, 64, f16>), g, dim3(512), 0, s, p, tm, tn, splits);
+        else hipLaunchKernelGGL((igemm_tn3<false, 0, false, false, 256, 64, f16>), g, dim3(512), 0, s, p, tm, tn, splits);
+        return;
+    }
     const bool multi_round = (long)tm * ((p.N + 255) / 256) > device_cus();
     if (splits == 1 && !g_tn3_abl && (g_tn3_half & (p.adam.p ? 1 : 2)) && (multi_round || !p.adam.p || (g_tn3_half & 4))) {
         // 256 x 128 tiles, two blocks per CU
