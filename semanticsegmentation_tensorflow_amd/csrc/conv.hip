@@ -470,7 +470,9 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 7: {        // Conv2D over relu(BN(x)) (seg_conv2d_fwd_pro)
             NTParams p = conv_fwd_params(d);
             macs = macs_conv;
-            if (seg::g_nt_variant == 2 && seg::nt2_pro_ok(p, d->dtype, 1)) {
+            if (seg::s1x1_ok(p, d->dtype, 1)) {
+                fam = "conv1x1_stream"; bm = 128; bn = 64;
+            } else if (seg::g_nt_variant == 2 && seg::nt2_pro_ok(p, d->dtype, 1)) {
                 fam = "igemm_nt2_pro"; bm = 192; bn = p.N <= 64 ? 64 : 128;
             } else {
                 fam = "igemm_nt_pro"; bm = 128; bn = p.N <= 64 ? 64 : 128;
@@ -566,6 +568,11 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "tn3_stagger_us")) {
         if (value < 0 || value > 1000) return SEG_EINVAL;
         seg::g_tn3_stagger_us = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "s1x1")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_s1x1 = value;
         return SEG_OK;
     }
     if (!strcmp(name, "nt3_stag")) {
@@ -730,6 +737,11 @@ extern "C" int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const s
     p.x = x; p.w = w; p.y = y;
     p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
     p.pro = make_pro(pro, d->c_valid);
+    if (seg::s1x1_ok(p, d->dtype, 1)) {
+        seg::launch_s1x1(p, d->dtype, seg::device_cus(), (hipStream_t)stream);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 

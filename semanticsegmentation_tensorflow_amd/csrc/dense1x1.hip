@@ -1,0 +1,212 @@
+// Persistent streaming 1x1 convolution for FC-DenseNet's bottleneck layers
+// (Network/model/FCDenseNet.py:23-35: BN -> ReLU -> 1x1 conv (4*growth = 64
+// filters) -> dropout over the dense block's concat).  The op is HBM-bound:
+// per pixel it reads C <= 256 input channels and writes <= 64 outputs, at
+// ~2*64 MACs per byte.  The tile-per-block implicit GEMM (igemm_nt2_pro) spends
+// most of each short block in load latency (1.9-2.7 TB/s); here one block per
+// CU streams pixel tiles through a 6-deep LDS-DMA ring that does not drain at
+// tile boundaries:
+//  * step s = (pixel tile i, 64-channel k tile kk) of the block's tiles
+//    t = blockIdx.x + i * gridDim.x; the DMA of step s + 5 is issued when
+//    step s starts, so ~5 k tiles (up to 80 KiB) per CU are always in flight;
+//    each wave stages and consumes its own 16 pixel rows: no barriers;
+//  * the filter (<= 64 x 256) and the BatchNorm (scale, shift) table stay in
+//    LDS for the whole kernel;
+//  * MFMA on D^T = W . relu(BN(x))^T, so a lane holds 4 consecutive output
+//    channels of one pixel: the epilogue (bias / ReLU / dropout, TF1 counter
+//    mask) stores 8 bytes per lane straight from the accumulators, no LDS
+//    staging; lanes past the last pixel store into a trash page so every
+//    wave issues the same number of vector-memory instructions per step,
+//    which keeps the counted `s_waitcnt vmcnt` exact.
+#include "common.h"
+#include "igemm.h"
+#include "ldsdma.h"
+
+namespace seg {
+
+int g_s1x1 = 1;
+static __device__ uint4 s1_zero[4];
+static __device__ uint2 s1_trash[64 * 64];
+
+namespace {
+
+constexpr int S1_TP = 128;       // pixels per tile (8 waves x 16)
+constexpr int S1_NST = 6;        // ring stages of S1_TP x 64 channels
+constexpr int S1_MAXC = 256;
+constexpr int S1_NW = 8;
+constexpr int S1_DMA = S1_TP / 8 / S1_NW;   // DMA instructions per wave per step (2)
+constexpr int S1_ST = 4;                    // epilogue stores per wave per tile (one per 16-channel block)
+
+// wait until at most n younger vector-memory instructions are outstanding
+__device__ __forceinline__ void wait_vm_rt(int n) {
+    switch (n) {
+#define W_(k) case k: wait_vmcnt<k>(); return;
+        W_(0) W_(1) W_(2) W_(3) W_(4) W_(5) W_(6) W_(7) W_(8) W_(9) W_(10) W_(11) W_(12) W_(13) W_(14) W_(15)
+        W_(16) W_(17) W_(18) W_(19) W_(20) W_(21) W_(22) W_(23) W_(24) W_(25) W_(26) W_(27) W_(28) W_(29) W_(30)
+#undef W_
+        default: wait_vmcnt<31>(); return;
+    }
+}
+
+template <typename T, bool PRO>
+__global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles, int kt) {
+    constexpr int STG = S1_TP * 128;
+    __shared__ __attribute__((aligned(16))) char ring[S1_NST * STG];            // 96 KiB
+    __shared__ __attribute__((aligned(16))) char wsm[64 * S1_MAXC * 2];          // 32 KiB
+    __shared__ __attribute__((aligned(16))) float ptab[2 * S1_MAXC];
+    __shared__ __attribute__((aligned(16))) float etab[2][64];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, fg = lane >> 4;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const EpiParams& e = p.epi;
+    const int rowb = kt * 128;                       // filter row bytes in LDS
+
+    // ---- resident filter [n][kk][chunk ^ swz(n)], BN table, epilogue table
+    for (int i = tid; i < 64 * kt * 8; i += 512) {
+        const int c8 = i & 7, kk = (i >> 3) % kt, n = i / (8 * kt);
+        const int c = kk * 64 + c8 * 8;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (n < p.N && c < p.K) v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col + c);
+        *reinterpret_cast<uint4*>(wsm + n * rowb + kk * 128 + 16 * (c8 ^ ((n >> 1) & 7))) = v;
+    }
+    if constexpr (PRO) {
+        for (int k = tid; k < kt * 64; k += 512) {
+            const bool v = k < p.pro.cv;
+            ptab[2 * k] = v ? p.pro.gamma[k] * p.pro.inv : 0.f;
+            ptab[2 * k + 1] = v ? p.pro.beta[k] : 0.f;
+        }
+    }
+    if (tid < 64) {
+        const bool cv = tid < e.n_valid;
+        etab[0][tid] = (e.scale && cv) ? e.scale[tid] : 1.f;
+        etab[1][tid] = ((e.shift && cv) ? e.shift[tid] : 0.f) + ((e.bias && cv) ? e.bias[tid] : 0.f);
+    }
+
+    // ---- x DMA: every wave stages its own 16 pixel rows (w*16 + q*8 + lr,
+    // physical chunk lane & 7, row swizzle (row >> 1) & 7), so the waves never
+    // wait for each other: no barrier in the loop, one wave's VALU epilogue /
+    // BN prologue overlaps another's load wait
+    const int lr = lane >> 3;
+    const int nmine = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int S = nmine * kt;
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)ring;
+    auto issue = [&](int s) {
+        const int i = s / kt, kk = s - (s / kt) * kt;
+        const int t = (int)blockIdx.x + i * (int)gridDim.x;
+        const unsigned sb = lds0 + (s % S1_NST) * STG;
+#pragma unroll
+        for (int q = 0; q < S1_DMA; ++q) {
+            const int row = w * 16 + q * 8 + lr;
+            const int c = (lane & 7) ^ ((q * 4 + (lr >> 1)) & 7);
+            const int ch = kk * 64 + c * 8;
+            const long m = (long)t * S1_TP + row;
+            const bool ok = m < p.M && ch < p.K;
+            const void* src = ok ? (const void*)(X + m * p.ldx + ch) : (const void*)s1_zero;
+            glds16(src, sb + (w * 2 + q) * 1024);   // lane L -> row w*16 + q*8 + L/8, chunk L%8
+        }
+    };
+    // outstanding vector-memory instructions issued after DMA(s) when step s
+    // starts: the DMAs of steps s+1 .. s+NST-2 and the epilogue stores of the
+    // steps since DMA(s) was issued
+    auto younger = [&](int s) {
+        int n = S1_DMA * (min(S - 1, s + S1_NST - 2) - s);
+        for (int j = max(0, s - S1_NST + 1); j < s; ++j)
+            if (j % kt == kt - 1) n += S1_ST;
+        return n;
+    };
+    for (int s = 0; s < S1_NST - 1 && s < S; ++s) issue(s);
+    __syncthreads();                                 // filter / tables visible
+
+    f32x4 acc[4];
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int xrow = w * 16 + fr;                    // this lane's B-fragment pixel row
+    for (int s = 0; s < S; ++s) {
+        wait_vm_rt(younger(s));
+        // the wave's own step s - 1 reads of the stage it re-fills are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (s + S1_NST - 1 < S) issue(s + S1_NST - 1);
+        const int kk = s % kt;
+        const char* Xs = ring + (s % S1_NST) * STG;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int chunk = ks * 4 + fg;
+            uint4 xb = *reinterpret_cast<const uint4*>(Xs + xrow * 128 + 16 * (chunk ^ ((xrow >> 1) & 7)));
+            if constexpr (PRO) {
+                float ss[16];
+                const float4* tp = reinterpret_cast<const float4*>(ptab + 2 * (kk * 64 + chunk * 8));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t4 = tp[q];
+                    ss[4 * q] = t4.x; ss[4 * q + 1] = t4.y; ss[4 * q + 2] = t4.z; ss[4 * q + 3] = t4.w;
+                }
+                xb = pro_affine8<T>(xb, ss, p.pro.relu);
+            }
+#pragma unroll
+            for (int nf = 0; nf < 4; ++nf) {
+                const int n = nf * 16 + fr;
+                const uint4 wa = *reinterpret_cast<const uint4*>(wsm + n * rowb + kk * 128 + 16 * (chunk ^ ((n >> 1) & 7)));
+                acc[nf] = mfma16x16x32<T>(wa, xb, acc[nf]);     // D^T[n][px]
+            }
+        }
+        if (kk == kt - 1) {
+            // lane: channels nf*16 + 4*fg .. +3 of pixel m
+            const int t = (int)blockIdx.x + (s / kt) * (int)gridDim.x;
+            const long m = (long)t * S1_TP + xrow;
+            const uint64_t gidx = (uint64_t)m * e.n_valid;
+#pragma unroll
+            for (int nf = 0; nf < 4; ++nf) {
+                const int col0 = nf * 16 + 4 * fg;
+                const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
+                const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
+                T o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float v = acc[nf][j] * sc4[j] + ad4[j];
+                    if (e.relu) v = fmaxf(v, 0.f);
+                    if (e.keep_prob < 1.f) v = seg_dropout(v, e.keep_prob, e.seed, gidx + col0 + j);
+                    o[j] = from_f32<T>(col0 + j < e.n_valid ? v : 0.f);
+                }
+                const bool ok = m < p.M && col0 < p.N;
+                uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + m * p.ldy + col0)
+                                : s1_trash + (tid & 4095);
+                *dst = *reinterpret_cast<const uint2*>(o);
+                acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+    wait_vmcnt<0>();
+}
+
+}  // namespace
+
+// y = epilogue(W . relu(BN(x))): single-tap 1x1 stride-1, N <= 64, C <= 256,
+// dense pixel rows (x_img / y_img are whole images of ldx / ldy rows),
+// no residual / mask epilogue
+bool s1x1_ok(const NTParams& p, int dtype, int nphases) {
+    return g_s1x1 && (dtype == SEG_BF16 || dtype == SEG_F16) && nphases == 1 && !p.phase && p.K == p.C &&
+           p.taps_w == 1 && p.ish == 1 && p.isw == 1 && p.ioh == 0 && p.iow == 0 && p.osh == 1 && p.osw == 1 &&
+           p.IH == p.Ha && p.IW == p.Wa && p.OH == p.Ha && p.OW == p.Wa && p.x_img == (long)p.IH * p.IW * p.ldx &&
+           p.y_img == (long)p.OH * p.OW * p.ldy && p.N <= 64 && p.K <= S1_MAXC && p.K % 8 == 0 && p.ldx % 8 == 0 &&
+           p.ldy % 4 == 0 && ((uintptr_t)p.x % 16) == 0 && ((uintptr_t)p.y % 8) == 0 && !p.epi.residual &&
+           !p.epi.mask && !p.epi.bn_x && p.M > 0;
+}
+
+void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {
+    const int ntiles = (p.M + S1_TP - 1) / S1_TP;
+    const int kt = (p.K + 63) / 64;
+    const int grid = std::min(ntiles, cus);
+    const bool pro = p.pro.gamma != nullptr;
+    if (dtype == SEG_F16) {
+        if (pro) hipLaunchKernelGGL((conv1x1_stream<f16, true>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+        else hipLaunchKernelGGL((conv1x1_stream<f16, false>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+    } else {
+        if (pro) hipLaunchKernelGGL((conv1x1_stream<bf16, true>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+        else hipLaunchKernelGGL((conv1x1_stream<bf16, false>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+    }
+}
+
+}  // namespace seg

@@ -193,6 +193,10 @@ __device__ __forceinline__ uint4 pro_affine8(uint4 v, const float* ss, int relu)
 }
 constexpr int NT2_PRO_MAXK = 1024;    // (scale, shift) table in LDS
 bool nt2_pro_ok(const NTParams& p, int dtype, int nphases);
+// persistent streaming 1x1 conv (dense1x1.hip): FC-DenseNet bottleneck convs
+extern int g_s1x1;
+bool s1x1_ok(const NTParams& p, int dtype, int nphases);
+void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s);
 void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s);
 void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype);
 

@@ -195,3 +195,57 @@ def test_conv3x3_bwd_data_through_bn_relu_dropout(dev, case, dtype, kp):
     assert_close(from_dev(dx, C), want, dtype, f"bn3-dgrad dx {case}")
     assert_close(dg.double().cpu(), gv.grad, torch.float32, f"bn3-dgrad dgamma {case}", 2e-3)
     assert_close(db.double().cpu(), bv.grad, torch.float32, f"bn3-dgrad dbeta {case}", 2e-3)
+
+
+# the streaming 1x1 kernel (conv1x1_stream: FC-DenseNet bottleneck convs,
+# C <= 256 -> N <= 64) vs float64, with the bottleneck's dropout epilogue,
+# the input as a channel slice of a wider concat buffer, pixel counts that
+# leave ragged last tiles and give most blocks several tiles
+S1_CASES = [(2, 130, 140, 48, 64), (1, 50, 61, 256, 64), (1, 40, 70, 112, 56), (2, 33, 35, 8, 16),
+            (3, 97, 131, 200, 64)]
+
+
+def _np_uniform_vec(seed, idx):
+    """tests.test_gpu_ops._np_uniform over a uint64 index array (same hash)."""
+    from tests.test_gpu_ops import _np_avalanche32
+    M = np.uint64(0xFFFFFFFF)
+    key = np.uint64(_np_avalanche32(((seed ^ (seed >> 32)) & 0xFFFFFFFF) ^ 0x632BE59B))
+    x = ((idx & M) ^ (((idx >> np.uint64(32)) * np.uint64(0x85EBCA6B)) & M)) & M
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & M
+    x ^= key
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & M
+    x ^= x >> np.uint64(16)
+    return ((x >> np.uint64(8)).astype(np.float64) / 16777216.0).astype(np.float32)
+
+
+@pytest.mark.parametrize("kp", [1.0, 0.2], ids=["no-dropout", "dropout"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", S1_CASES)
+def test_conv1x1_stream_bn_relu_dropout(dev, case, dtype, kp):
+    from tests.test_gpu_ops import _np_uniform
+    N, H, W, C, K = case
+    x, w, gamma, beta, xr, wr, a = _pro_case((N, H, W, C, K, 1), dtype, dev)
+    seed = 4242
+    ref = T.conv2d(a, wr)
+    if kp < 1.0:
+        u = _np_uniform_vec(seed, np.arange(N * H * W * K, dtype=np.uint64))
+        assert u[123] == np.float32(_np_uniform(seed, 123))
+        mask = torch.from_numpy(np.floor(np.float32(kp) + u).astype(np.float64)).view(N, H, W, K)
+        ref = ref / kp * mask
+    d = ops.conv_desc(N, H, W, C, K, 1, 1, 1, 1, "SAME", PRO_DT[dtype])
+    assert ops.conv_kernel_info(d, ops.OP_FWD_PRO)[0].startswith("conv1x1_stream")
+    wk = torch.empty(ops.packed_shape(1, 1, C, K, ops.PACK_KRSC), dtype=dtype, device=dev)
+    ops.pack_filter(w.float().to(dev).contiguous(), wk, ops.round8(C), ops.round8(K), ops.PACK_KRSC)
+    wide = torch.zeros(N, H, W, C + 24, dtype=dtype, device=dev)
+    wide[..., 16:16 + C] = to_dev(x, dtype, dev)
+    y = torch.full((N, H, W, d.K), float("nan"), dtype=dtype, device=dev)
+    epi = ops.epilogue(keep_prob=kp, seed=seed) if kp < 1.0 else None
+    ops.conv2d_fwd_pro(d, wide[..., 16:16 + C], ops.prologue(gamma.to(dev), beta.to(dev)), wk, y, epi)
+    torch.cuda.synchronize()
+    assert_close(from_dev(y, K), ref, dtype, f"conv1x1_stream {case}")
+    if kp < 1.0:   # the dropped positions are exactly the oracle's
+        got = from_dev(y, K)
+        assert bool((got[mask == 0] == 0).all())
+        assert bool((mask[(got == 0) & (ref.abs() > 1e-3)] == 0).all())
