@@ -235,6 +235,16 @@ int seg_maxpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int l
  * kept only where that max is > 0. */
 int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H,
                        int W, int C, int ldx, int ldy, int relu_mask, int dtype, void* stream);
+/* Training form (same ops, replaces the pair above inside a train step): the
+ * forward also records, per pooled element, one byte of idx (row stride C,
+ * 8-byte aligned): bits 0-1 the first-max window position (row-major), bit 2
+ * set where that max is > 0.  The gradient then reads dy and idx only (not x).
+ * Requires N*ceil(H/2)*ceil(W/2)*C/epc < 2^31 (SEG_EINVAL otherwise: use the
+ * x-reading pair). */
+int seg_maxpool2x2_fwd_argmax(const void* x, void* y, void* idx, int N, int H, int W, int C,
+                              int ldx, int ldy, int dtype, void* stream);
+int seg_maxpool2x2_bwd_argmax(const void* idx, const void* dy, void* dx, int N, int H, int W,
+                              int C, int ldx, int ldy, int relu_mask, int dtype, void* stream);
 int seg_avgpool2x2_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int ldy,
                        int dtype, void* stream);
 int seg_avgpool2x2_bwd(const void* dy, void* dx, int N, int H, int W, int C, int ldx, int ldy,

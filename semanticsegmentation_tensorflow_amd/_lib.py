@@ -153,6 +153,8 @@ SIGNATURES = {
     "seg_bias_grad_workspace": (_Z, [_L, _I]),
     "seg_maxpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_maxpool2x2_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_maxpool2x2_fwd_argmax": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "seg_maxpool2x2_bwd_argmax": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_avgpool2x2_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_avgpool2x2_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_add": (_I, [_P, _P, _P, _L, _I, _P]),

@@ -194,6 +194,87 @@ __global__ void maxpool_bwd_k(const T* __restrict__ x, const T* __restrict__ dy,
     }
 }
 
+// MaxPool with its switches recorded (training path): besides y, one byte per
+// pooled element -- bits 0-1 the first-max position q (0 = (0,0), 1 = (0,1),
+// 2 = (1,0), 3 = (1,1), TF's tie rule as maxpool_fwd_k), bit 2 set when the max
+// is > 0 (the ReluGrad of a post-ReLU input, !(m > 0) for NaN as well).  The
+// gradient then reads dy + 1 B/elem instead of the 4x-sized input x.  32-bit
+// index math (the host checks the element count).  idx row stride = C.
+template <typename T>
+__global__ void maxpool_fwd_idx_k(const T* __restrict__ x, T* __restrict__ y, unsigned char* __restrict__ idx, int H,
+                                  int W, int C, int ldx, int ldy, unsigned OW, unsigned CK, unsigned total) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned cc = i % CK, pix = i / CK;
+        const unsigned ow = pix % OW, t = pix / OW;
+        const unsigned oh = t % (unsigned)OH, n = t / (unsigned)OH;
+        const T* b = x + ((long)(n * (unsigned)H + 2 * oh) * W + 2 * ow) * ldx + cc * EPC;
+        float v0[EPC], v1[EPC], v2[EPC], v3[EPC];
+        Chunk<T>::unpack(ldc(b), v0);
+        Chunk<T>::unpack(ldc(b + ldx), v1);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx), v2);
+        Chunk<T>::unpack(ldc(b + (long)W * ldx + ldx), v3);
+        unsigned long long code = 0;
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            unsigned a = 0;
+            float m = v0[e];
+            if (v1[e] > m) { m = v1[e]; a = 1; }
+            if (v2[e] > m) { m = v2[e]; a = 2; }
+            if (v3[e] > m) { m = v3[e]; a = 3; }
+            v0[e] = m;
+            code |= (unsigned long long)(a | (m > 0.f ? 4u : 0u)) << (8 * e);
+        }
+        stc(y + (long)pix * ldy + cc * EPC, Chunk<T>::pack(v0));
+        unsigned char* q = idx + (long)pix * C + cc * EPC;
+        if constexpr (EPC == 8) *reinterpret_cast<unsigned long long*>(q) = code;
+        else *reinterpret_cast<unsigned*>(q) = (unsigned)code;
+    }
+}
+
+// MaxPoolGrad from the recorded switches: one thread per (2x2 input block,
+// chunk); blocks past the pooled region (odd H / W) receive zero gradient.
+template <typename T>
+__global__ void maxpool_bwd_idx_k(const unsigned char* __restrict__ idx, const T* __restrict__ dy, T* __restrict__ dx,
+                                  int H, int W, int C, int ldx, int ldy, int relu, unsigned BW, unsigned CK,
+                                  unsigned total) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int OH = H / 2, OW = W / 2, BH = (H + 1) / 2;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned cc = i % CK, blk = i / CK;
+        const unsigned bw = blk % BW, t = blk / BW;
+        const unsigned bh = t % (unsigned)BH, n = t / (unsigned)BH;
+        const long base = ((long)(n * (unsigned)H + 2 * bh) * W + 2 * bw) * ldx + cc * EPC;
+        float o[4][EPC];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) o[q][e] = 0.f;
+        if (bh < (unsigned)OH && bw < (unsigned)OW) {
+            const unsigned pix = (n * (unsigned)OH + bh) * (unsigned)OW + bw;
+            const unsigned char* q = idx + (long)pix * C + cc * EPC;
+            unsigned long long code;
+            if constexpr (EPC == 8) code = *reinterpret_cast<const unsigned long long*>(q);
+            else code = *reinterpret_cast<const unsigned*>(q);
+            float d[EPC];
+            Chunk<T>::unpack(ldc(dy + (long)pix * ldy + cc * EPC), d);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                const unsigned c8 = (unsigned)(code >> (8 * e)) & 7u;
+                const float g = (relu && !(c8 & 4u)) ? 0.f : d[e];
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) o[qq][e] = ((c8 & 3u) == (unsigned)qq) ? g : 0.f;
+            }
+        }
+        const bool h1 = 2 * bh + 1 < (unsigned)H, w1 = 2 * bw + 1 < (unsigned)W;
+        stc(dx + base, Chunk<T>::pack(o[0]));
+        if (w1) stc(dx + base + ldx, Chunk<T>::pack(o[1]));
+        if (h1) stc(dx + base + (long)W * ldx, Chunk<T>::pack(o[2]));
+        if (h1 && w1) stc(dx + base + (long)W * ldx + ldx, Chunk<T>::pack(o[3]));
+    }
+}
+
 template <typename T>
 __global__ void avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int ldx, int ldy) {
     constexpr int EPC = dt_traits<T>::EPC;
@@ -949,6 +1030,33 @@ extern "C" int seg_maxpool2x2_bwd(const void* x, const void* y, const void* dy, 
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
                                          (hipStream_t)stream, (const T*)x, (const T*)dy, (T*)dx, N, H, W, C, ldx, ldy,
                                          relu_mask));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_maxpool2x2_fwd_argmax(const void* x, void* y, void* idx, int N, int H, int W, int C, int ldx,
+                                         int ldy, int dtype, void* stream) {
+    if (!x || !y || !idx || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2 || N < 1 || (uintptr_t)idx % 8)
+        return SEG_EINVAL;
+    const long total = (long)N * (H / 2) * (W / 2) * (C / epc_of(dtype));
+    if ((long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / epc_of(dtype)) >= (1L << 31)) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_idx_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const T*)x, (T*)y, (unsigned char*)idx, H, W, C, ldx,
+                                         ldy, (unsigned)(W / 2), (unsigned)(C / epc_of(dtype)), (unsigned)total));
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
+extern "C" int seg_maxpool2x2_bwd_argmax(const void* idx, const void* dy, void* dx, int N, int H, int W, int C,
+                                         int ldx, int ldy, int relu_mask, int dtype, void* stream) {
+    if (!idx || !dy || !dx || (C & 7) || (ldx & 7) || (ldy & 7) || H < 2 || W < 2 || N < 1 || (uintptr_t)idx % 8)
+        return SEG_EINVAL;
+    const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / epc_of(dtype));
+    if (total >= (1L << 31)) return SEG_EINVAL;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_idx_k<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0,
+                                         (hipStream_t)stream, (const unsigned char*)idx, (const T*)dy, (T*)dx, H, W,
+                                         C, ldx, ldy, relu_mask, (unsigned)((W + 1) / 2),
+                                         (unsigned)(C / epc_of(dtype)), (unsigned)total));
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

@@ -368,6 +368,30 @@ def maxpool2x2_bwd(x, y, dy, dx, stream=None, relu_mask=False):
     return dx
 
 
+def maxpool_argmax_fits(x):
+    N, H, W, C = x.shape
+    return N * ((H + 1) // 2) * ((W + 1) // 2) * (C // (4 if x.dtype == torch.float32 else 8)) < 2 ** 31
+
+
+def maxpool2x2_fwd_argmax(x, y, idx, stream=None):
+    """MaxPool that also records its switches (1 byte per pooled element, row
+    stride C) for maxpool2x2_bwd_argmax."""
+    N, H, W, C = x.shape
+    check(_lib.lib().seg_maxpool2x2_fwd_argmax(ptr(x), ptr(y), ptr(idx), N, H, W, C, pixel_stride(x),
+                                               pixel_stride(y), seg_dtype(x), stream_ptr(stream)),
+          "max_pool")
+    return y
+
+
+def maxpool2x2_bwd_argmax(idx, dy, dx, stream=None, relu_mask=False):
+    """MaxPoolGrad from the forward's recorded switches (x not read)."""
+    N, H, W, C = dx.shape
+    check(_lib.lib().seg_maxpool2x2_bwd_argmax(ptr(idx), ptr(dy), ptr(dx), N, H, W, C, pixel_stride(dx),
+                                               pixel_stride(dy), 1 if relu_mask else 0, seg_dtype(dx),
+                                               stream_ptr(stream)), "max_pool_grad")
+    return dx
+
+
 def avgpool2x2_fwd(x, y, stream=None):
     N, H, W, C = x.shape
     check(_lib.lib().seg_avgpool2x2_fwd(ptr(x), ptr(y), N, H, W, C, pixel_stride(x),

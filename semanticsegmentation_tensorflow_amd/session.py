@@ -699,6 +699,7 @@ class Session:
         ws_need = 0
         p.packs = set()
         p.pack_apad = {}
+        p.pool_idx = {}     # MaxPool node id -> recorded switches (train plans)
         for n in p.nodes:
             y = n.output
             if n.kind == "input":
@@ -778,6 +779,12 @@ class Session:
                                   4 * 1024 * 2 * round8(Co))
             elif n.kind == "bn":
                 ws_need = max(ws_need, 4 * 1024 * 2 * round8(s[3]))
+            elif n.kind == "MaxPool" and p.train and id(n.inputs[0]) in p.needs_grad:
+                # the forward records its switches; MaxPoolGrad reads them, not x
+                xb = buf[id(n.inputs[0])]
+                if ops.maxpool_argmax_fits(xb):
+                    N, H, W, C = xb.shape
+                    p.pool_idx[id(n)] = torch.empty(N * (H // 2) * (W // 2) * C, dtype=torch.uint8, device=dev)
         ws_need = max(ws_need, 8192)
         self.ws.get(ws_need)
         # packed filter copies
@@ -986,7 +993,11 @@ class Session:
                 self._timed(n.desc, ops.OP_TFWD, ops.tconv2d_fwd, n.desc, x,
                             store.packed[(n.w.var_name, ops.PACK_TCONV_FWD)][0], y, epi, self.ws)
             elif k == "MaxPool":
-                ops.maxpool2x2_fwd(buf[id(n.inputs[0])], y)
+                idx = p.pool_idx.get(id(n))
+                if idx is not None:
+                    ops.maxpool2x2_fwd_argmax(buf[id(n.inputs[0])], y, idx)
+                else:
+                    ops.maxpool2x2_fwd(buf[id(n.inputs[0])], y)
             elif k == "AvgPool":
                 ops.avgpool2x2_fwd(buf[id(n.inputs[0])], y)
             elif k == "Add":
@@ -1388,8 +1399,12 @@ class Session:
                 if id(x) in ng:
                     dx, acc = dest(x)
                     prod = p.producer.get(id(x))
-                    ops.maxpool2x2_bwd(buf[id(x)], buf[id(n.output)], dy, dx,
-                                       relu_mask=prod is not None and id(prod) in p.mask_fuse)
+                    relu = prod is not None and id(prod) in p.mask_fuse
+                    idx = p.pool_idx.get(id(n))
+                    if idx is not None:
+                        ops.maxpool2x2_bwd_argmax(idx, dy, dx, relu_mask=relu)
+                    else:
+                        ops.maxpool2x2_bwd(buf[id(x)], buf[id(n.output)], dy, dx, relu_mask=relu)
                     done(dx, acc)
             elif k == "AvgPool":
                 x = n.inputs[0]

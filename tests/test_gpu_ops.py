@@ -326,6 +326,47 @@ def test_maxpool_fwd_bwd(dev, shape, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(2, 6, 8, 16), (1, 7, 9, 24), (1, 5, 5, 8), (4, 96, 312, 64)])
+def test_maxpool_argmax_fwd_bwd(dev, shape, dtype):
+    """Training form: the forward records its switches, MaxPoolGrad reads them
+    (not x); bit-exact with the x-reading pair and the oracle, ties to the
+    first max, odd H / W tails zero, fused ReluGrad incl. all-zero windows."""
+    N, H, W, C = shape
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    x[0, 0, 0, :] = x[0, 0, 1, :]          # exact ties -> first in scan order
+    x[0, 2:4, 2:4, :] = 0.0                # all-equal window (relu: max 0 -> no gradient)
+    x = rnd(x, dtype).requires_grad_(True)
+    y = tf.max_pool2x2(x)
+    dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
+    (y * dy).sum().backward()
+    xd = to_dev(x.detach(), dtype, dev)
+    Cp = ops.round8(C)
+    yd = torch.empty(N, H // 2, W // 2, Cp, dtype=dtype, device=dev)
+    idx = torch.full((N * (H // 2) * (W // 2) * Cp,), 255, dtype=torch.uint8, device=dev)
+    ops.maxpool2x2_fwd_argmax(xd, yd, idx)
+    dxd = torch.full_like(xd, float("nan"))
+    ops.maxpool2x2_bwd_argmax(idx, to_dev(dy, dtype, dev), dxd)
+    torch.cuda.synchronize()
+    assert torch.equal(from_dev(yd, C), y.detach())
+    assert torch.equal(from_dev(dxd, C), x.grad)
+    for relu_in in (False, True):
+        xr = (torch.relu(x.detach()) if relu_in else x.detach()).requires_grad_(True)
+        (tf.max_pool2x2(xr) * dy).sum().backward()
+        want = torch.where(xr.detach() > 0, xr.grad, torch.zeros_like(xr.grad))
+        xrd = to_dev(xr.detach(), dtype, dev)
+        ops.maxpool2x2_fwd_argmax(xrd, yd, idx)
+        dxd.fill_(float("nan"))
+        ops.maxpool2x2_bwd_argmax(idx, to_dev(dy, dtype, dev), dxd, relu_mask=True)
+        ref = torch.full_like(xrd, float("nan"))
+        ops.maxpool2x2_bwd(xrd, yd, to_dev(dy, dtype, dev), ref, relu_mask=True)
+        torch.cuda.synchronize()
+        assert torch.equal(dxd, ref)
+        if relu_in:
+            assert torch.equal(from_dev(dxd, C), want)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 def test_avgpool_fwd_bwd(dev, dtype):
     N, H, W, C = 2, 7, 6, 16
     g = torch.Generator().manual_seed(11)

@@ -62,7 +62,8 @@ def test_fcn_train_plan(dry):
     # forward: 17 fused conv launches, 3 tconv, 5 pools, 1 loss
     assert c.count("seg_conv2d_fwd") == 17
     assert c.count("seg_tconv2d_fwd") == 3
-    assert c.count("seg_maxpool2x2_fwd") == 5
+    # train plans record the pool switches; MaxPoolGrad reads them instead of x
+    assert c.count("seg_maxpool2x2_fwd_argmax") == 5
     assert c.count("seg_softmax_xent_fwd_bwd") == 1
     # backward: conv1_1 needs no input gradient (image is a placeholder)
     assert c.count("seg_conv2d_bwd_data") == 16
@@ -72,7 +73,7 @@ def test_fcn_train_plan(dry):
     assert c.count("seg_conv2d_bwd_filter_adam") == 2
     assert c.count("seg_tconv2d_bwd_data") == 3
     assert c.count("seg_tconv2d_bwd_filter") == 3
-    assert c.count("seg_maxpool2x2_bwd") == 5
+    assert c.count("seg_maxpool2x2_bwd_argmax") == 5
     assert c.count("seg_adam_tf1_pack") == 1          # one fused multi-tensor launch
     # skip fusion: pool3/pool4 gradients = sum of two consumers
     assert c.count("seg_add") == 2
