@@ -208,7 +208,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         }
     }
 
-    if (p.partial) {
+    if (p.partial && !p.tile_cnt) {
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -234,6 +234,36 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     const int cch = lane % CPR, rsub = lane / CPR;
     const int col0 = n0 + wn * WTN + cch * 8;
     const EpiParams& e = p.epi;
+    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
+    // store them to its slab (agent-coherent 16-byte stores), count in; the last
+    // split to arrive sums the slabs in the row loop below (splitk_arrive)
+    const bool fold = p.partial != nullptr;
+    if (fold) {
+        char* wb = smem + w * WTM * SROW;
+        const auto rs = splitk_rsrc(p.partial);
+        lds_barrier();
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    *reinterpret_cast<float*>(wb + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                        acc[mi][ni][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < NRR; ++k) {
+            const int rr = rsub + k * RPP;
+            const int ml = wm * WTM + rr;
+            const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
+            float v[8];
+            splitk_lds8(wb + rr * SROW + cch * 32, v);
+            splitk_put8(rs, ((blockIdx.z * (unsigned)p.M + (unsigned)((img * p.OH + oy) * p.OW + ox)) * (unsigned)p.N +
+                             col0) * 4u, v);
+        }
+        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
+    }
     // 16-bit ReluGrad mask rows of this lane, requested before the staging
     uint4 mkv[NRR];
     if constexpr (sizeof(T) == 2) {
@@ -251,13 +281,16 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     }
     lds_barrier();
     char* wbuf = smem + w * WTM * SROW;
+    if (!fold) {
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
-                *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) = acc[mi][ni][r];
+                for (int ni = 0; ni < TN; ++ni)
+                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                        acc[mi][ni][r];
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     float bias[8], scl[8], shf[8];
 #pragma unroll
@@ -275,9 +308,10 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
         if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
         const long pix = (long)oy * p.OW + ox;
-        const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
-        const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
-        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        float v[8];
+        if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)(img * p.OH * p.OW + pix) * (unsigned)p.N + col0) * 4u,
+                              (unsigned)p.M * p.N * 4u, (int)gridDim.z, v);
+        else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
         float res[8], mk[8];
         if (e.mask) {
             if constexpr (sizeof(T) == 2) {
@@ -543,7 +577,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
 
-    if (p.partial) {
+    if (p.partial && !p.tile_cnt) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -578,6 +612,38 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
     char* wbuf = smem + w * 64 * SROW;
+    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
+    // store them to its slab (agent-coherent 16-byte stores), count in; the last
+    // split to arrive sums the slabs in the row loop below (splitk_arrive)
+    const bool fold = p.partial != nullptr;
+    if (fold) {
+        const auto rs = splitk_rsrc(p.partial);
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+            lds_barrier();
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int ni = 0; ni < 2 * NFH; ++ni)
+                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                            acc[mh * 4 + mi][ni][r];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 64 / RPP; ++k) {
+                const int rr = rsub + k * RPP;
+                const int ml = wm * 128 + mh * 64 + rr;
+                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+                if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
+                float v[8];
+                splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+                splitk_put8(rs, ((blockIdx.z * (unsigned)p.M + (unsigned)((img * p.OH + oy) * p.OW + ox)) *
+                                 (unsigned)p.N + col0) * 4u, v);
+            }
+        }
+        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
+    }
     // ReluGrad mask rows: the first half's requested before its staging, the
     // second half's row by row as the first half's are consumed
     constexpr int NRR = 64 / RPP;
@@ -597,14 +663,16 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
         lds_barrier();
+        if (!fold) {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+            for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int ni = 0; ni < 2 * NFH; ++ni)
-                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                        acc[mh * 4 + mi][ni][r];
+                    for (int ni = 0; ni < 2 * NFH; ++ni)
+                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                            acc[mh * 4 + mi][ni][r];
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < NRR; ++k) {
@@ -618,9 +686,10 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             }
             if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
             const long pix = (long)oy * p.OW + ox;
-            const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
-            const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
-            float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            float v[8];
+            if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)(img * p.OH * p.OW + pix) * (unsigned)p.N + col0) * 4u,
+                                  (unsigned)p.M * p.N * 4u, (int)gridDim.z, v);
+            else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8];
             if (e.residual) {
                 const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;

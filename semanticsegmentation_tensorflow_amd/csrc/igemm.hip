@@ -17,6 +17,7 @@
 // K staged through double-buffered LDS with 16-byte register-staged loads.
 // bf16 operands use v_mfma_f32_16x16x32_bf16, fp32 operands the exact-f32
 // v_mfma_f32_16x16x4_f32 (parity path).  Accumulation is always fp32.
+#include <mutex>
 #include "common.h"
 #include "igemm.h"
 
@@ -645,6 +646,44 @@ static int num_cus() {
 
 int device_cus() { return num_cus(); }
 
+int* splitk_counters(long n) {
+    constexpr long CAP = 1L << 16;
+    static int* buf[64] = {};
+    static long ring[64] = {};
+    static std::mutex mu;
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64 || n > CAP) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!buf[dev]) {
+        int* b = nullptr;
+        if (hipMalloc(&b, CAP * sizeof(int)) != hipSuccess) return nullptr;
+        if (hipMemset(b, 0, CAP * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(b);
+            return nullptr;
+        }
+        buf[dev] = b;
+    }
+    if (ring[dev] + n > CAP) ring[dev] = 0;
+    int* r = buf[dev] + ring[dev];
+    ring[dev] += (n + 63) & ~63L;
+    return r;
+}
+
+// In-kernel split-K reduction (last arriving split, see splitk_arrive) when
+// the tail it adds is short: <= 4 slabs per tile and enough tiles to spread
+// the tails over the CUs; otherwise the full-chip splitk_reduce_nt pass.
+// Off by default: measured slower on C2 (conv5_x 6 launches 577 vs 334 + 90
+// us of reducer; conv6 / conv7 igemm_nt3 1068 vs 894 + 80 us) -- the last
+// split's tail runs on one CU per tile (80-128 CUs) and the agent-coherent
+// slab traffic is written through the L2s, where the separate pass spreads
+// the same reads over the whole chip from L2/MALL.  A device-scope fence in
+// place of the sc1 stores was slower still (conv5_x 141 vs 52 + 20 us).
+int g_splitk_fold = 0;
+bool splitk_fold_ok(long tiles, int splits, long slab_bytes) {
+    return g_splitk_fold && splits > 1 && splits <= 4 && tiles >= 32 && splits * slab_bytes < (1L << 31);
+}
+
 // Kernel generation for the NT GEMMs (1 = register-staged 128-row tiles,
 // 2 = LDS-DMA 3-stage ring, 256-row tiles).  Runtime-selectable for tests.
 int g_nt_variant = 2;
@@ -767,9 +806,14 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
             if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
         }
+        p.tile_cnt = p.partial && splitk_fold_ok(hp.tiles, hp.splits, (long)p.M * p.N * 4) ? splitk_counters(hp.tiles) : nullptr;
         launch_halo(p, hp, hp.splits, s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
-        if (p.partial) {
+        const bool folded = p.tile_cnt != nullptr;
+        p.tile_cnt = nullptr;
+        if (p.partial && folded) {
+            p.partial = nullptr;
+        } else if (p.partial) {
             const long total = (long)p.M * (p.N / 8);
             hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, hp.splits);
             SEG_CHECK_LAUNCH();
@@ -797,18 +841,24 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
+    if (nt3 && !nt4 && p.partial) {
+        const long tiles = (long)((max_m + 255) / 256) * ((p.N + 255) / 256);
+        p.tile_cnt = splitk_fold_ok(tiles, splits, (long)p.M * p.N * 4) ? splitk_counters(tiles) : nullptr;
+    }
+    const bool folded = p.tile_cnt != nullptr;
     if (nt4) launch_nt4(p, gridz, max_m, s);
     else if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
     else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
     SEG_CHECK_LAUNCH();
-    if (p.partial) {
+    p.tile_cnt = nullptr;
+    if (p.partial && !folded) {
         const long total = (long)p.M * (p.N / 8);
         hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
         SEG_CHECK_LAUNCH();
-        p.partial = nullptr;
     }
+    p.partial = nullptr;
     return SEG_OK;
 }
 

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
 
-    if (p.partial) {
+    if (p.partial && !p.tile_cnt) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -311,17 +311,48 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
     char* wbuf = smem + w * 64 * SROW;
+    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
+    // store them to its slab (agent-coherent 16-byte stores), count in; the last
+    // split to arrive sums the slabs in the row loop below (splitk_arrive)
+    const bool fold = p.partial != nullptr;
+    if (fold) {
+        const auto rs = splitk_rsrc(p.partial);
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+            lds_barrier();
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                            acc[mh * 4 + mi][ni][r];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 2
+            for (int rr = rsub; rr < 64; rr += RPP) {
+                const int row = m0 + wm * WTM + mh * 64 + rr;
+                if (row >= M || col0 >= p.N) continue;
+                float v[8];
+                splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+                splitk_put8(rs, ((blockIdx.z * (unsigned)M + (unsigned)row) * (unsigned)p.N + col0) * 4u, v);
+            }
+        }
+        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
+    }
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
         lds_barrier();
+        if (!fold) {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+            for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int ni = 0; ni < TN; ++ni)
-                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                        acc[mh * 4 + mi][ni][r];
+                    for (int ni = 0; ni < TN; ++ni)
+                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                            acc[mh * 4 + mi][ni][r];
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll 2
         for (int rr = rsub; rr < 64; rr += RPP) {
@@ -332,9 +363,10 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
             const int a = rem / Wa;
             const int b = rem - a * Wa;
             const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
-            const float4 lo = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32);
-            const float4 hi = *reinterpret_cast<const float4*>(wbuf + rr * SROW + cch * 32 + 16);
-            float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            float v[8];
+            if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)row * (unsigned)p.N + col0) * 4u,
+                                  (unsigned)M * p.N * 4u, (int)gridDim.z, v);
+            else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8], mk[8];
             if (e.mask) {
                 const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
