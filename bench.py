@@ -235,7 +235,7 @@ def kernel_symbol(name):
     bm, bn = a[1], a[2]
     # dtype-templated kernels appear mangled (`_ZN3seg10conv_halo2ILi16E...`)
     if fam == "conv_halo":
-        return r"conv_halo2[<I]" if bn == "256" else r"conv_halo[<I]"
+        return r"conv_halo2[<I]" if bn == "256" else r"conv_halo(_duo)?[<I]"
     if fam in ("igemm_nt3", "igemm_tn3"):
         return fam + "<"
     if fam == "igemm_nt2":

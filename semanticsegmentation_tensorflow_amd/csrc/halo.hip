@@ -42,6 +42,7 @@ int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
+int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -342,6 +343,225 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Two blocks per CU (N <= 128): conv_halo's tile and fragment layout with ONE
+// halo buffer and a 2-stage filter ring (BN = 128: 48 + 32 KiB; BN = 64: 48 +
+// 16 KiB) and the epilogue staged in two 32-row halves, so two blocks share a
+// CU (<= 128 VGPRs: 4 waves per SIMD).  One block's pipeline bubbles -- the
+// halo of each channel chunk is loaded after the previous chunk's last tap and
+// waited for before its first; the filter slice of iteration it+1 is in flight
+// during iteration it only -- are the other block's MFMA time.  On conv2_x of
+// FCN (C = 64 / 128: one or two chunks per tile, 1872 tiles) conv_halo left
+// each block ~80 % of its time waiting on a single in-order pipeline.
+// No split-K (the host uses it only for splits == 1).
+template <int BW, int HI, int BN, typename T = bf16>
+__global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) {
+    constexpr int NW = 8, WM = 4, WN = 2, BM = 256, BH = BM / BW;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int B_INS = BN / 8 / NW;
+    constexpr int HBUF = HI * NW * 1024;
+    constexpr int BSTAGE = BN * 128;
+    constexpr int SMEM = HBUF + 2 * BSTAGE;
+    static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
+    static_assert(SMEM <= 80 * 1024, "two blocks per CU");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
+    const int tsp = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
+    const int tpi = g.tiles_x * g.tiles_y;
+    const int img = tsp / tpi;
+    if (img >= g.nimg) return;
+    const int trem = tsp - img * tpi;
+    const int ty = trem / g.tiles_x, tx = trem - (trem / g.tiles_x) * g.tiles_x;
+    const int oy0 = ty * BH, ox0 = tx * BW, n0 = tn * BN;
+    const int ntaps = g.taps_h * p.taps_w;
+    const int iters = g.nchunks * ntaps;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w - (w / WN) * WN;
+    const int lr = lane >> 3;
+    const int c = (lane & 7) ^ (lr & 6);   // halo row (h*NW + w)*8 + lr: swizzle row & 6
+
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const void* zero = (const void*)halo_zero_page;
+
+    // 32-bit element offsets within the (block-uniform) image: fits 128 VGPRs
+    const T* __restrict__ Ximg = X + (long)img * p.x_img;
+    int h_off[HI];
+#pragma unroll
+    for (int h = 0; h < HI; ++h) {
+        const int hr = (h * NW + w) * 8 + lr;
+        const int hy = hr / g.hwd, hx = hr - (hr / g.hwd) * g.hwd;
+        const int ih = oy0 + p.ioh + g.hy0 + hy, iw = ox0 + p.iow + g.hx0 + hx;
+        const bool ok = hr < g.hrows && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        h_off[h] = ok ? (ih * p.IW + iw) * p.ldx + c * 8 : -1;
+    }
+    const int h_n = g.hrows > w * 8 ? min(HI, (g.hrows - w * 8 + NW * 8 - 1) / (NW * 8)) : 0;
+    int b_off[B_INS];
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+        const int n = n0 + (i * NW + w) * 8 + lr;
+        b_off[i] = n < p.N ? n * (int)p.w_col + c * 8 : -1;
+    }
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
+    const unsigned ldsB = lds0 + HBUF;
+    auto load_halo = [&](int kc) {
+        for (int h = 0; h < h_n; ++h) {
+            const void* src = h_off[h] >= 0 ? (const void*)(Ximg + h_off[h] + kc * 64) : zero;
+            glds16(src, lds0 + (h * NW + w) * 1024);
+        }
+    };
+    int b_kc = 0, b_j = 0, b_i = 0;
+    auto issue_b = [&](int stage) {
+        const long wtap = (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
+#pragma unroll
+        for (int i = 0; i < B_INS; ++i) {
+            const void* src = b_off[i] >= 0 ? (const void*)(Wt + b_off[i] + wtap) : zero;
+            glds16(src, ldsB + stage * BSTAGE + (i * NW + w) * 1024);
+        }
+        if (++b_i == p.taps_w) {
+            b_i = 0;
+            if (++b_j == g.taps_h) { b_j = 0; ++b_kc; }
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (iters > 0) {
+        load_halo(0);
+        issue_b(0);
+    }
+    const int fr = lane & 15, fg = lane >> 4;
+    int rowbase[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+        const int ml = wm * WTM + mi * 16;
+        rowbase[mi] = (ml / BW) * g.hwd + (ml % BW) + fr;
+    }
+    int t_j = 0, t_i = 0, kc = 0, stage = 0;
+    for (int it = 0; it < iters; ++it) {
+        wait_vmcnt<0>();            // slice it (and, at it = 0, the first halo) landed
+        lds_barrier();              // ... for every wave; slice it-1 / the old halo are dead
+        if (it > 0 && t_j == 0 && t_i == 0) {
+            // first tap of chunk kc: its halo replaces the previous chunk's
+            load_halo(kc);
+            if (it + 1 < iters) issue_b(stage ^ 1);
+            if (it + 1 < iters) wait_vmcnt<B_INS>();
+            else wait_vmcnt<0>();
+            lds_barrier();
+        } else if (it + 1 < iters) {
+            issue_b(stage ^ 1);
+        }
+        const char* Bs = smem + HBUF + stage * BSTAGE;
+        const int toff = (t_j * p.tsh - g.hy0) * g.hwd + t_i * p.tsw - g.hx0;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            uint4 af[TM], bfr[TN];
+            const int chunk = ks * 4 + fg;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                const int row = rowbase[mi] + toff;
+                af[mi] = *reinterpret_cast<const uint4*>(smem + row * 128 + 16 * (chunk ^ (row & 6)));
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const int row = wn * WTN + ni * 16 + fr;
+                bfr[ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * (chunk ^ (row & 6)));
+            }
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    acc[mi][ni] = mfma16x16x32<T>(af[mi], bfr[ni], acc[mi][ni]);
+        }
+        stage ^= 1;
+        if (++t_i == p.taps_w) {
+            t_i = 0;
+            if (++t_j == g.taps_h) {
+                t_j = 0;
+                ++kc;
+            }
+        }
+    }
+
+    // ---- epilogue in two 32-row halves per wave: wave tile -> LDS (fp32),
+    // then 8 columns x one row per lane (conv_halo's arithmetic)
+    constexpr int SROW = WTN * 4 + 16, HR = WTM / 2;
+    static_assert(NW * HR * SROW <= SMEM, "epilogue staging must fit");
+    constexpr int CPR = WTN / 8;
+    constexpr int RPP = 64 / CPR, NRH = HR / RPP;
+    const int cch = lane % CPR, rsub = lane / CPR;
+    const int col0 = n0 + wn * WTN + cch * 8;
+    const EpiParams& e = p.epi;
+    float bias[8];     // BN scale / shift (rare here) are read per row: 128 VGPRs
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bias[j] = (e.bias && col0 + j < e.n_valid) ? e.bias[col0 + j] : 0.f;
+    char* wbuf = smem + w * HR * SROW;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        uint4 mkv[NRH];          // ReluGrad mask rows of this half, requested before the staging
+        if (e.mask) {
+#pragma unroll
+            for (int k = 0; k < NRH; ++k) {
+                const int ml = wm * WTM + hh * HR + rsub + k * RPP;
+                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+                mkv[k] = uint4{0u, 0u, 0u, 0u};
+                if (oy < p.OH && ox < p.OW && col0 < p.N)
+                    mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
+                                                             ((long)oy * p.OW + ox) * e.ld_mask + col0);
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int mi = 0; mi < TM / 2; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni)
+                    *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
+                        acc[hh * (TM / 2) + mi][ni][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < NRH; ++k) {
+            const int rr = rsub + k * RPP;
+            const int ml = wm * WTM + hh * HR + rr;
+            const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
+            const long pix = (long)oy * p.OW + ox;
+            float v[8];
+            splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+            float res[8], mk[8];
+            if (e.mask) Chunk<T>::unpack(mkv[k], mk);
+            if (e.residual) {
+                const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
+            }
+            const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int col = col0 + j;
+                const bool cv = col < e.n_valid;
+                const float sc = (e.scale && cv) ? e.scale[col] : 1.f, sh = (e.shift && cv) ? e.shift[col] : 0.f;
+                float x = v[j] * sc + sh + bias[j];
+                if (e.relu) x = fmaxf(x, 0.f);
+                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.residual) x += res[j];
+                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                v[j] = col < e.n_valid ? x : 0.f;
+            }
+            T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
+            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        }
+    }
+}
 
 // ---------------------------------------------------------------------------
 // 256 x 256 variant (N > 128): 8 waves as 2 (M) x 4 (N), 128 x 64 per wave,
@@ -1298,8 +1518,24 @@ static void launch_halo_t(NTParams& p, const HaloGeom& g, long tiles, int gridz,
         hipLaunchKernelGGL((conv_halo<BW, HI, BN>), dim3((unsigned)tiles, 1, gridz), dim3(512), 0, s, p, g);
 }
 
+template <int BW, int HI, int BN>
+static void launch_halo_duo_t(NTParams& p, const HaloGeom& g, long tiles, hipStream_t s, int dtype) {
+    if (dtype == SEG_F16)
+        hipLaunchKernelGGL((conv_halo_duo<BW, HI, BN, f16>), dim3((unsigned)tiles), dim3(512), 0, s, p, g);
+    else
+        hipLaunchKernelGGL((conv_halo_duo<BW, HI, BN>), dim3((unsigned)tiles), dim3(512), 0, s, p, g);
+}
+
 template <int BW, int HI>
 static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s, int dtype) {
+    // two blocks per CU when there is no split-K (its 80 KiB LDS takes HI = 7 halos for BN = 64 only)
+    // (32-bit in-image offsets; the f16 BW = 32 / BN = 128 instance spills: conv_halo)
+    if (g_halo_duo && gridz == 1 && !p.partial && (bn == 64 || HI == 6) &&
+        (long)p.IH * p.IW * p.ldx < (1L << 31) && !(dtype == SEG_F16 && BW == 32 && bn == 128)) {
+        if (bn == 64) launch_halo_duo_t<BW, HI, 64>(p, g, tiles, s, dtype);
+        else launch_halo_duo_t<BW, 6, 128>(p, g, tiles, s, dtype);
+        return;
+    }
     if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s, dtype);
     else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s, dtype);
 }

@@ -202,7 +202,8 @@ void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
 extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
-extern int g_splitk_fold;   // 1: NT split-K reduced inside the producer (splitk_arrive)
+extern int g_splitk_fold;
+extern int g_halo_duo;      // halo.hip: two-blocks-per-CU conv_halo_duo for N <= 128   // 1: NT split-K reduced inside the producer (splitk_arrive)
 extern int g_tn_variant;
 extern int g_tn_fill;
 extern int g_tn_split_cap;

@@ -31,7 +31,8 @@ def ntv(request, dev):
     off so igemm_nt2 stays covered for wide N), 9 = 8 with the four-wave
     128x128-per-wave GEMM (igemm_nt4) in place of igemm_nt3.  Variant 8 also
     turns off the 2-stage short-K igemm_nt2 (K <= 128), so the 3-stage ring
-    stays covered for those problems."""
+    stays covered for those problems.  N <= 128 halo problems without split-K
+    run the two-blocks-per-CU conv_halo_duo except in variants 4 and 6."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
     ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
@@ -41,6 +42,7 @@ def ntv(request, dev):
     ops.set_option("nt3_stag", 0 if v == 5 else 1)
     ops.set_option("halo_phases", 4 if v == 6 else 2)
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
+    ops.set_option("halo_duo", 0 if v in (4, 6) else 1)   # 4 / 6 keep the one-block conv_halo covered
     ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
     ops.set_option("nt4", 1 if v == 9 else 0)
     ops.set_option("nt2_short", 0 if v == 8 else 8)
@@ -56,6 +58,7 @@ def ntv(request, dev):
     ops.set_option("nt3_stag", 1)
     ops.set_option("halo_phases", 2)
     ops.set_option("halo2_n128", 0)
+    ops.set_option("halo_duo", 1)
 
 
 DTYPES = [torch.float32, torch.bfloat16, torch.float16]
