@@ -292,17 +292,44 @@ __global__ __launch_bounds__(256) void igemm_nt(NTParams p) {
 
 // One thread per (row, 8 columns): sum the split-K slabs, apply the epilogue
 // once per row decomposition, store 16 B (bf16) / 32 B (fp32).
+// 32-bit index math (the host checks M * N / 8 < 2^31); the slabs of up to
+// four splits are requested before their (split-ordered) additions.
 template <typename T>
-__global__ void splitk_reduce_nt(NTParams p, int splits) {
-    const int c8 = p.N / 8;
-    const long total = (long)p.M * c8;
+__global__ __launch_bounds__(256) void splitk_reduce_nt(NTParams p, int splits) {
+    const unsigned c8 = (unsigned)p.N / 8;
+    const unsigned total = (unsigned)p.M * c8;
     const long slab = (long)p.M * p.N;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
         const int row = (int)(i / c8);
-        const int col0 = (int)(i - (long)row * c8) * 8;
+        const int col0 = (int)(i - (unsigned)row * c8) * 8;
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         const float* src = p.partial + (long)row * p.N + col0;
-        for (int z = 0; z < splits; ++z) {
+        int z = 0;
+        for (; z + 3 < splits; z += 4) {
+            float4 a[4], b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                a[q] = *reinterpret_cast<const float4*>(src + (z + q) * slab);
+                b[q] = *reinterpret_cast<const float4*>(src + (z + q) * slab + 4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[0] += a[q].x; v[1] += a[q].y; v[2] += a[q].z; v[3] += a[q].w;
+                v[4] += b[q].x; v[5] += b[q].y; v[6] += b[q].z; v[7] += b[q].w;
+            }
+        }
+        if (z + 1 < splits) {
+            const float4 a0 = *reinterpret_cast<const float4*>(src + z * slab);
+            const float4 b0 = *reinterpret_cast<const float4*>(src + z * slab + 4);
+            const float4 a1 = *reinterpret_cast<const float4*>(src + (z + 1) * slab);
+            const float4 b1 = *reinterpret_cast<const float4*>(src + (z + 1) * slab + 4);
+            v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
+            v[4] += b0.x; v[5] += b0.y; v[6] += b0.z; v[7] += b0.w;
+            v[0] += a1.x; v[1] += a1.y; v[2] += a1.z; v[3] += a1.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+            z += 2;
+        }
+        if (z < splits) {
             const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
             const float4 b = *reinterpret_cast<const float4*>(src + z * slab + 4);
             v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
@@ -680,6 +707,7 @@ int* splitk_counters(long n) {
 // the same reads over the whole chip from L2/MALL.  A device-scope fence in
 // place of the sc1 stores was slower still (conv5_x 141 vs 52 + 20 us).
 int g_splitk_fold = 0;
+int g_nt_nsplit = 1;    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
 bool splitk_fold_ok(long tiles, int splits, long slab_bytes) {
     return g_splitk_fold && splits > 1 && splits <= 4 && tiles >= 32 && splits * slab_bytes < (1L << 31);
 }
@@ -783,6 +811,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         SEG_CHECK_LAUNCH();
         if (p.partial) {
             const long total = (long)p.M * (p.N / 8);
+            if (total >= (1L << 31)) return SEG_EINVAL;
             hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
             SEG_CHECK_LAUNCH();
             p.partial = nullptr;
@@ -815,6 +844,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
             p.partial = nullptr;
         } else if (p.partial) {
             const long total = (long)p.M * (p.N / 8);
+            if (total >= (1L << 31)) return SEG_EINVAL;
             hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, hp.splits);
             SEG_CHECK_LAUNCH();
             p.partial = nullptr;
@@ -829,6 +859,32 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     } else if (nt3) {
         nt3_info(max_m, p.N, p.K, num_cus(), &splits);
         if (nphases > 1) splits = 1;
+    }
+    // N = 256 k + a tail of <= 128 columns (FC-DenseNet's 320 / 560 / 352 /
+    // 280-wide transposed-conv GEMMs): the 256-aligned head on igemm_nt3, the
+    // tail on igemm_nt2 (256 x 64 / 128 tiles) instead of a 256-wide tile that
+    // is 50-80 % padding.  Not with dropout (its counter uses the full row
+    // width) or the BN-backward epilogue (per-tile column sums).
+    if (nt3 && !nt4 && splits == 1 && g_nt_nsplit && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128 &&
+        p.epi.keep_prob >= 1.f && !p.epi.bn_x) {
+        const int nh = p.N / 256 * 256;
+        NTParams t = p;
+        p.N = nh;
+        launch_nt3(p, nphases, max_m, s, dt_traits<T>::id);
+        SEG_CHECK_LAUNCH();
+        p.N = t.N;
+        t.N -= nh;
+        t.w = reinterpret_cast<const T*>(t.w) + (long)nh * t.w_col;
+        t.y = reinterpret_cast<T*>(t.y) + nh;
+        if (t.epi.bias) t.epi.bias += nh;
+        if (t.epi.scale) t.epi.scale += nh;
+        if (t.epi.shift) t.epi.shift += nh;
+        if (t.epi.residual) t.epi.residual = reinterpret_cast<const T*>(t.epi.residual) + nh;
+        if (t.epi.mask) t.epi.mask = reinterpret_cast<const T*>(t.epi.mask) + nh;
+        t.epi.n_valid = std::max(0, t.epi.n_valid - nh);
+        launch_nt2(t, dt_traits<T>::id, t.N <= 64 ? 64 : 128, nphases, max_m, s);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
     }
     int gridz = nphases;
     if (splits > 1) {
@@ -855,7 +911,8 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     p.tile_cnt = nullptr;
     if (p.partial && !folded) {
         const long total = (long)p.M * (p.N / 8);
-        hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+        if (total >= (1L << 31)) return SEG_EINVAL;
+            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
         SEG_CHECK_LAUNCH();
     }
     p.partial = nullptr;

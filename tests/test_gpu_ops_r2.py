@@ -322,3 +322,54 @@ def test_splitk_fold_matches_reducer(dev, case, op):
         got = outs[1].double().cpu()
     err = (got - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1.2e-2, err
+
+
+# N = 256 k + a tail <= 128 on igemm_nt3 + igemm_nt2 (nt_nsplit): forward with
+# bias + ReLU, and the input gradient with the ReluGrad mask, vs the float64
+# oracle; the 256-aligned head is the same igemm_nt3 launch either way.
+@pytest.mark.parametrize("C,K,op", [(256, 320, "fwd"), (256, 352, "fwd"), (320, 256, "bwd_data"),
+                                    (560, 256, "bwd_data")])
+def test_nt_nsplit_head_tail(dev, C, K, op):
+    N, H, W = 2, 96, 96
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(31)
+    d = ops.conv_desc(N, H, W, C, K, 1, 1, 1, 1, "SAME", ops.BF16)
+    x64 = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
+    w64 = torch.randn(1, 1, C, K, generator=g, dtype=torch.float64) / C ** 0.5
+    dy64 = torch.randn(N, H, W, K, generator=g, dtype=torch.float64)
+    mask64 = torch.relu(torch.randn(N, H, W, C, generator=g, dtype=torch.float64))
+    b = (torch.randn(K, generator=g) * 0.1).to(dev)
+    ws = ops.Workspace(dev)
+    outs = {}
+    for ns in (0, 1):
+        ops.set_option("nt_nsplit", ns)
+        try:
+            if op == "fwd":
+                name = ops.conv_kernel_info(d, ops.OP_FWD)[0]
+                wk = torch.empty(ops.packed_shape(1, 1, C, K, ops.PACK_KRSC, C), dtype=dtype, device=dev)
+                ops.pack_filter(w64.float().to(dev), wk, C, K, ops.PACK_KRSC)
+                y = torch.full((N, H, W, K), float("nan"), dtype=dtype, device=dev)
+                ops.conv2d_fwd(d, x64.to(dev, dtype), wk, y, ops.epilogue(bias=b, relu=True), ws)
+            else:
+                name = ops.conv_kernel_info(d, ops.OP_BWD_DATA)[0]
+                wh = torch.empty(ops.packed_shape(1, 1, C, K, ops.PACK_HWIO, C), dtype=dtype, device=dev)
+                ops.pack_filter(w64.float().to(dev), wh, C, K, ops.PACK_HWIO)
+                y = torch.full((N, H, W, C), float("nan"), dtype=dtype, device=dev)
+                ops.conv2d_bwd_data(d, dy64.to(dev, dtype), wh, y, ws, epi=ops.epilogue(relu_mask=mask64.to(dev, dtype)))
+            torch.cuda.synchronize()
+        finally:
+            ops.set_option("nt_nsplit", 1)
+        assert name.startswith("igemm_nt3"), name
+        outs[ns] = y.clone()
+    assert torch.equal(outs[0][..., :256], outs[1][..., :256])
+    xr, wr = x64.to(dtype).double(), w64.to(dtype).double()
+    if op == "fwd":
+        ref = torch.relu(T.conv2d(xr, wr, 1, "SAME", 1) + b.double().cpu())
+    else:
+        xa = torch.zeros(N, H, W, C, dtype=torch.float64, requires_grad=True)
+        (T.conv2d(xa, wr, 1, "SAME", 1) * dy64.to(dtype).double()).sum().backward()
+        ref = torch.where(mask64.to(dtype).double() > 0, xa.grad, torch.zeros_like(xa.grad))
+    for ns in (0, 1):
+        got = outs[ns].double().cpu()
+        err = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 1.2e-2, (ns, err)
