@@ -180,7 +180,7 @@ __device__ __forceinline__ void wc_glds16(const void* gsrc, unsigned lds_dst) {
 
 __device__ uint4 wc_zero_page[4];
 
-// N = 64 (4 n fragments); 6 tap-pair fragments: (r, 0..1), (r, 2..3*) for r = 0..2
+// N <= 64 (4 n fragments; columns >= N staged as zeros); 6 tap-pair fragments: (r, 0..1), (r, 2..3*) for r = 0..2
 template <typename T>
 __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
     constexpr int DROWB = 128;                          // 64 dz channels
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
             const int r = (i * 4 + w) * 8 + lr;                 // dz tile row (pixel)
             const int ch = pc ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2));
             const int oy = oy0 + r / WC_BW, ox = ox0 + r % WC_BW;
-            const bool ok = oy < p.Ha && ox < p.Wa;
+            const bool ok = oy < p.Ha && ox < p.Wa && ch * 8 < p.N;     // N < 64: zero columns
             const void* src = ok ? (const void*)(Dz + (((long)img * p.Ha + oy) * p.Wa + ox) * p.ldb + ch * 8) : zero;
             wc_glds16(src, sb + HBUF + (i * 4 + w) * 1024);
         }
@@ -329,7 +329,8 @@ __global__ __launch_bounds__(256) void wgrad_c8(TNParams p, WCGeom g) {
 
 bool smallc_wgrad_ok(const TNParams& p, int dtype) {
     return g_smallc && (dtype == SEG_BF16 || dtype == SEG_F16) && p.Cg == 8 && p.M == 72 && p.taps_w == 3 && p.ish == 1 && p.isw == 1 &&
-           p.tsh == 1 && p.tsw == 1 && p.N == 64 && p.ldx == 8 && p.ldb == 64 && p.Ha > 0 && p.Wa > 0 &&
+           p.tsh == 1 && p.tsw == 1 && p.N % 16 == 0 && p.N >= 16 && p.N <= 64 && p.ldx == 8 && p.ldb % 8 == 0 &&
+           p.ldb >= p.N && p.Ha > 0 && p.Wa > 0 &&
            p.P % (p.Ha * p.Wa) == 0;
 }
 
