@@ -20,6 +20,8 @@ Compilation (per fetch set and fed shapes):
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -191,6 +193,8 @@ class Session:
         # BatchNorm(+ReLU) feeding a single 1x1 conv folded into its operand prologue
         self.fold_bn = True
         self.fold_dropout_grad = True   # Conv -> Dropout -> BN: the dropout gradient inside the BN backward
+        # a tensor's later input-gradient contributions accumulate in the epilogue
+        self.fuse_grad_sum = os.environ.get("SEG_FUSE_GRAD_SUM", "1") != "0"
         self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
@@ -1326,10 +1330,18 @@ class Session:
                     self._grad_ready([gn, bn_])
                 elif id(x) in ng:
                     dx, acc = dest(x)
-                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
-                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
-                                self._mask_epi(p, x))
-                    done(dx, acc)
+                    mepi = self._mask_epi(p, x)
+                    if acc is not None and mepi is None and self.fuse_grad_sum and self.capture is None:
+                        # a further consumer's contribution: accumulated in the
+                        # epilogue, in place (residual = the gradient so far)
+                        self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], acc, ws, None,
+                                    ops.epilogue(residual=acc))
+                        dx = acc
+                    else:
+                        self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None, mepi)
+                        done(dx, acc)
                 if self.capture is not None:
                     # tests: the buffers of this layer's three kernels (they persist
                     # after the step; dx before any accumulation of other consumers;
