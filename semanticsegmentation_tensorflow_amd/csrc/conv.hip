@@ -505,6 +505,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_nt_variant = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "tn_nsplit")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_tn_nsplit = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "nt_nsplit")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_nsplit = value;

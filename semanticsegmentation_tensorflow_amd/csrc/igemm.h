@@ -202,6 +202,7 @@ void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
 extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
+extern int g_tn_nsplit;
 extern int g_splitk_fold;
 extern int g_nt_nsplit;     // igemm_nt3 head + igemm_nt2 tail for N = 256 k + <= 128
 extern int g_halo_duo;      // halo.hip: two-blocks-per-CU conv_halo_duo for N <= 128   // 1: NT split-K reduced inside the producer (splitk_arrive)

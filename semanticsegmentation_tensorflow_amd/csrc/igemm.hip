@@ -707,7 +707,8 @@ int* splitk_counters(long n) {
 // the same reads over the whole chip from L2/MALL.  A device-scope fence in
 // place of the sc1 stores was slower still (conv5_x 141 vs 52 + 20 us).
 int g_splitk_fold = 0;
-int g_nt_nsplit = 1;    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
+int g_nt_nsplit = 1;
+int g_tn_nsplit = 1;    // TN: igemm_tn3 head + igemm_tn2 tail for N = 256 k + <= 128    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
 bool splitk_fold_ok(long tiles, int splits, long slab_bytes) {
     return g_splitk_fold && splits > 1 && splits <= 4 && tiles >= 32 && splits * slab_bytes < (1L << 31);
 }
@@ -1089,6 +1090,50 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     choose_tn(p.M, p.N, p.P, BKP, sizeof(T) == 2, bm, bn, splits);
     const bool tn3 = sizeof(T) == 2 && g_tn_variant == 2 && tn3_ok(p, dt_traits<T>::id);
     if (tn3) tn3_info(p.M, p.N, p.P, num_cus(), &splits);
+    // N = 256 k + a tail <= 128 (FC-DenseNet's transposed-conv filter
+    // gradients, N = 320 / 560 input channels): the 256-aligned head on
+    // igemm_tn3, the tail on igemm_tn2, each with its own split-K slabs in `ws`
+    // (reduced in stream order, so the tail reuses the head's slab space)
+    if (tn3 && g_tn_nsplit && !p.defer && !p.adam.p && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128) {
+        const int nh = p.N / 256 * 256;
+        const int kt = (p.P + BKP - 1) / BKP;
+        auto plan = [&](TNParams& q, int sp) {
+            const long cap = ws ? (long)(ws_bytes / ((size_t)q.M * q.N * sizeof(float))) : 1;
+            sp = (int)std::max(1L, std::min<long>(sp, cap));
+            q.partial = nullptr;
+            if (sp > 1) {
+                q.kt_per_split = (kt + sp - 1) / sp;
+                sp = (kt + q.kt_per_split - 1) / q.kt_per_split;
+                q.partial = reinterpret_cast<float*>(ws);
+            }
+            return sp;
+        };
+        TNParams h = p;
+        h.N = nh;
+        h.n_valid = std::min(p.n_valid, nh);
+        h.dbias = nullptr;
+        int sh;
+        tn3_info(h.M, h.N, h.P, num_cus(), &sh);
+        sh = plan(h, sh);
+        launch_tn3(h, sh, s, dt_traits<T>::id);
+        SEG_CHECK_LAUNCH();
+        tn_finish(h, sh, s);
+        SEG_CHECK_LAUNCH();
+        TNParams t = p;
+        t.N = p.N - nh;
+        t.n_valid = std::max(0, p.n_valid - nh);
+        t.b = reinterpret_cast<const T*>(p.b) + nh;
+        t.out = p.out + (long)nh * p.o_n;
+        t.dbias = nullptr;
+        int tbm, tbn, st;
+        choose_tn(t.M, t.N, t.P, BKP, 1, tbm, tbn, st);
+        st = plan(t, st);
+        launch_tn2(t, tbm, tbn, st, s, dt_traits<T>::id);
+        SEG_CHECK_LAUNCH();
+        tn_finish(t, st, s);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     int gridz = 1;
     if (splits > 1) {
         const int kt = (p.P + BKP - 1) / BKP;

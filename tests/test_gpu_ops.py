@@ -236,6 +236,7 @@ TCONV_CASES = [
     (2, 3, 2, 24, 24, 16, 4, 16, 8),     # tap-dense with 4 output channels
     (1, 4, 5, 16, 16, 20, 2, 8, 4),      # tap-dense k8 s4
     (2, 4, 4, 136, 8, 8, 72, 4, 2),      # tails in both channel dims
+    (1, 24, 32, 320, 48, 64, 128, 4, 2), # FC-DenseNet transition up 5 (320 -> 128): N = 256 + 64 split GEMMs
 ]
 
 
