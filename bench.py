@@ -65,6 +65,12 @@ def parse():
                     help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="seg_set_option kernel knob (A/B runs; repeatable)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="data-parallel Session over an RCCL ('nccl') process group even at world size 1 "
+                         "(e.g. torchrun --nproc-per-node 1): the C4 per-rank step, all-reduces included")
+    ap.add_argument("--no-dp-probe", action="store_true",
+                    help="N=1: skip the side line that re-times the step through a world-1 RCCL data-parallel Session")
+    ap.add_argument("--no-inference", action="store_true", help="skip the inference-latency line")
     ap.add_argument("--overlap-optimizer", action="store_true",
                     help="per-layer Adam on a side stream as gradients become final (measured slower: the "
                          "HBM-bound update steals CUs from the MFMA-bound backward)")
@@ -227,6 +233,52 @@ def pipeline_rate(H, W, device, threads=16, seconds=2.0):
             "note": f"375x1242 RGBA merge + RGB gt PNG pairs -> {H}x{W} samples + labels"}
 
 
+def inference_latency(device, dtype, H=375, W=1242, images=30):
+    """Per-image inference time the way the reference reports it
+    (Network/utils/utils.py:63-89, averaged over 30 images in
+    Network/main.py:200-206): one image per sess.run of tf.nn.softmax(logits)
+    with keep_prob 1.0.  Two figures: `device_ms_per_img` -- the image
+    resident in HBM, the softmax map left on the device (kernel time plus
+    launch overhead, synchronised per image); `gen_test_output_ms_per_img` --
+    evaluate.gen_test_output (numpy image in, numpy softmax out: host copies
+    included, the reference's loop body without PNG decode / resize)."""
+    import numpy as np
+    import torch
+    from semanticsegmentation_tensorflow_amd import evaluate as E
+    from semanticsegmentation_tensorflow_amd import graph as G
+    from semanticsegmentation_tensorflow_amd import tf
+    from semanticsegmentation_tensorflow_amd.fcn import FCN
+    HP, WP = pad32(H), pad32(W)
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
+    keep = tf.placeholder(tf.float32, name="keep_probability")
+    _, logits = FCN(image, keep, 2).create()
+    softmax = tf.nn.softmax(logits)
+    sess = tf.Session(compute_dtype=dtype, seed=0)
+    sess.run(tf.global_variables_initializer())
+    imgs, _ = synthetic(images, H, W, HP, WP, 4321, device)
+    for i in range(3):                                    # plan compile + warm-up
+        sess.run(softmax, feed_dict={image: imgs[i:i + 1], keep: 1.0}, as_numpy=False)
+    torch.cuda.synchronize()
+    t = []
+    for i in range(images):
+        t0 = time.perf_counter()
+        sess.run(softmax, feed_dict={image: imgs[i:i + 1], keep: 1.0}, as_numpy=False)
+        torch.cuda.synchronize()
+        t.append(time.perf_counter() - t0)
+    host = imgs.cpu().numpy()
+    t2 = [pt for _, _, _, pt in E.gen_test_output(sess, softmax, keep, image, host, (HP, WP))]
+    del sess
+    torch.cuda.empty_cache()
+    return {"batch": 1, "images": images, "image": f"{H}x{W} -> {HP}x{WP}", "dtype": dtype,
+            "fetch": "tf.nn.softmax(logits), keep_prob 1.0 (Network/utils/utils.py:81)",
+            "device_ms_per_img": round(1e3 * float(np.mean(t)), 3),
+            "device_ms_per_img_min": round(1e3 * float(np.min(t)), 3),
+            "gen_test_output_ms_per_img": round(1e3 * float(np.mean(t2)), 3),
+            "note": "device: image resident in HBM, softmax left on the device, synchronised per image; "
+                    "gen_test_output: numpy image in / numpy softmax out per image (host copies included)"}
+
+
 def kernel_symbol(name):
     """rocprof symbol pattern of a seg_conv_kernel_info family name (the main
     kernel; its split-K reducer launches are attributed to it separately)."""
@@ -316,21 +368,18 @@ WORKLOAD = {"fcn": "FCN (reference Network/model/FCN.py topology)",
                        "(semanticsegmentation_tensorflow_amd/deeplab.py; config C5)"}
 
 
-def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, fuse_adam=True,
-            overlap_optimizer=False, want_miou=False, fold_bn=True):
-    """Build `model`'s training graph, run `warmup` + `steps` timed train steps
-    on a synthetic batch resident in HBM, then one more step with HIP events
-    around every conv launch (on its launch stream) for the per-kernel
-    roofline.  Returns the measurement dict (no printing)."""
-    import torch
-    import torch.distributed as dist
+def build_train_graph(model, H, W, dtype, dp=None, fuse_adam=True, overlap_optimizer=False, fold_bn=True):
+    """The benchmarked training graph and Session: `model`'s builder on a
+    [None, HP, WP, 3] image placeholder (H x W zero-padded to multiples of
+    32), softmax-xent masked to H x W, tf.train.AdamOptimizer(1e-4).minimize
+    (Network/model/FCN.py:312-340).  The full-size parity tests
+    (tests/test_gpu_fullsize.py) build their step through this function, so
+    they run exactly the launch plan bench.py times."""
     from semanticsegmentation_tensorflow_amd import graph as G
-    from semanticsegmentation_tensorflow_amd import ops, tf
+    from semanticsegmentation_tensorflow_amd import tf
     from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
     from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
     from semanticsegmentation_tensorflow_amd.fcn import FCN
-
-    world = dp.world if dp is not None else 1
     HP, WP = pad32(H), pad32(W)
     G.reset_default_graph()
     image = tf.placeholder(tf.float32, [None, HP, WP, 3], name="input_image")
@@ -349,6 +398,25 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
                       fuse_adam=fuse_adam)
     sess.fold_bn = fold_bn
     sess.run(tf.global_variables_initializer())
+    return {"sess": sess, "image": image, "labels": labels, "keep": keep, "pred": pred, "logits": logits,
+            "loss": loss, "train_step": train_step, "HP": HP, "WP": WP}
+
+
+def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, fuse_adam=True,
+            overlap_optimizer=False, want_miou=False, fold_bn=True):
+    """Build `model`'s training graph, run `warmup` + `steps` timed train steps
+    on a synthetic batch resident in HBM, then one more step with HIP events
+    around every conv launch (on its launch stream) for the per-kernel
+    roofline.  Returns the measurement dict (no printing)."""
+    import torch
+    import torch.distributed as dist
+    from semanticsegmentation_tensorflow_amd import ops
+
+    world = dp.world if dp is not None else 1
+    g = build_train_graph(model, H, W, dtype, dp, fuse_adam, overlap_optimizer, fold_bn)
+    sess, image, labels, keep, pred, loss, train_step = (g[k] for k in ("sess", "image", "labels", "keep", "pred",
+                                                                        "loss", "train_step"))
+    HP, WP = g["HP"], g["WP"]
     img, lab = synthetic(B, H, W, HP, WP, 1234 + rank, device)
     feed = {image: img, labels: lab, keep: kp}
 
@@ -446,6 +514,36 @@ def extra_config(model, dtype, device, steps, warmup):
             **({"loss_scaling": m["loss_scaling"]} if "loss_scaling" in m else {})}
 
 
+def init_rccl(device):
+    """torch.distributed over RCCL ('nccl' on ROCm); a world-1 group when not
+    launched by torchrun."""
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29571")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    dist.init_process_group("nccl", device_id=device)
+
+
+def dp_probe(args, B, H, W, kp, device):
+    """The headline step re-timed through the data-parallel Session over a
+    world-1 RCCL process group (config C4's per-rank step: buckets all-reduced
+    over RCCL as backward produces them, Adam after the last bucket; the
+    wgrad+Adam epilogue fusion is off because the all-reduce sits between
+    gradient and update)."""
+    import torch.distributed as dist
+    from semanticsegmentation_tensorflow_amd.dp import DataParallel
+    init_rccl(device)
+    dp = DataParallel(bucket_mb=args.bucket_mb)
+    m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, 0)
+    return {"backend": dist.get_backend(), "world": dist.get_world_size(), "bucket_mb": args.bucket_mb,
+            "buckets": len(dp.buckets), "value": round(m["value"], 3), "unit": "images/s",
+            "ms_per_step": round(m["ms_per_step"], 3),
+            "note": "same workload as the headline, every gradient bucket all-reduced over RCCL"}
+
+
 def main():
     args = parse()
     import torch
@@ -457,8 +555,8 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dp = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    if world > 1 or args.force_dp:
+        init_rccl(device)
         from semanticsegmentation_tensorflow_amd.dp import DataParallel
         dp = DataParallel(bucket_mb=args.bucket_mb)
 
@@ -534,6 +632,11 @@ def main():
                 "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes; FETCH_SIZE doubled (gfx950)"}
         except Exception as exc:  # report, never crash the headline line
             result["roofline"]["traffic_error"] = repr(exc)
+    if rank == 0 and world == 1 and args.model == "fcn" and not args.no_inference and not args.pmc_child:
+        try:
+            result["inference"] = inference_latency(device, args.dtype, H, W)
+        except Exception as exc:  # report, never crash the headline line
+            result["inference"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and args.model == "fcn" and not args.no_extra:
         # C3 and C5 in the same run (side lines; the headline stays C2)
         for key, model in (("c3_fcdensenet", "fcdensenet"), ("c5_deeplab", "deeplab")):
@@ -549,9 +652,14 @@ def main():
                 result["cpu_baseline_160x576"] = cpu_baseline(160, 576, 160, 576, args.cpu_steps, "fcn")
         except Exception as exc:  # report, never crash the headline line
             result["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    if world == 1 and dp is None and args.model == "fcn" and not args.no_dp_probe:
+        try:
+            result["dp_mode"] = dp_probe(args, B, H, W, kp, device)
+        except Exception as exc:  # report, never crash the headline line
+            result["dp_mode"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if dp:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -155,10 +155,22 @@ def fcdensenet_param_shapes(in_channels=3, num_classes=2):
     return shapes
 
 
-def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
+def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2, quant=None, dropout_u=None):
     """`quant` as in fcn_forward: applied where the device stores an activation
-    (conv / BN+ReLU / avg-pool / transposed-conv outputs; concats copy)."""
+    (conv / BN+ReLU / avg-pool / transposed-conv outputs; concats copy).
+    `dropout_u`: {conv name: U[0,1) tensor} for the dropout after that conv
+    (FCDenseNet.py:30, :34); absent entries use keep_prob with a fresh draw."""
     q = quant or (lambda t: t)
+    du = dropout_u or {}
+
+    def conv_drop(h, name):
+        """Conv2D_Block + Dropout: the device applies the dropout in the conv
+        epilogue and rounds once."""
+        z = tf.conv2d(h, p[f"{name}/weights"])
+        u = du.get(name)
+        if u is None and keep_prob < 1.0:
+            u = torch.rand(z.shape, dtype=torch.float32)
+        return q(tf.dropout(z, keep_prob, u) if u is not None else z)
     bn = _BNCounter()
 
     def BN(h):
@@ -169,10 +181,8 @@ def fcdensenet_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
         return q(tf.conv2d(h, p[f"{name}/weights"]))
 
     def bottleneck(h, name):                       # FCDenseNet.py:23-35
-        h = conv(q(tf.relu(BN(h))), f"{name}_conv1")
-        h = tf.dropout(h, keep_prob)
-        h = conv(q(tf.relu(BN(h))), f"{name}_conv2")
-        return tf.dropout(h, keep_prob)
+        h = conv_drop(q(tf.relu(BN(h))), f"{name}_conv1")
+        return conv_drop(q(tf.relu(BN(h))), f"{name}_conv2")
 
     def dense_block(h, nl, name):                  # FCDenseNet.py:48-61
         feats = [h]
@@ -243,7 +253,8 @@ def deeplab_param_shapes(in_channels=3, num_classes=2, depth=256):
     return shapes
 
 
-def deeplab_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
+def deeplab_forward(p, x, keep_prob=1.0, num_classes=2, quant=None, dropout_u=None):
+    """`dropout_u`: U[0,1) tensor of the projection's Dropout (deeplab.py:82)."""
     q = quant or (lambda t: t)
     bn = _BNCounter()
 
@@ -271,7 +282,8 @@ def deeplab_forward(p, x, keep_prob=1.0, num_classes=2, quant=None):
         br.append(q(tf.relu(BN(q(tf.conv2d(feat, p[f"aspp{i + 1}/weights"], dilation=r))))))
     h = tf.concat(br)
     h = q(tf.relu(BN(q(tf.conv2d(h, p["concat_projection/weights"])))))
-    h = tf.dropout(h, keep_prob)
+    if dropout_u is not None or keep_prob < 1.0:
+        h = q(tf.dropout(h, keep_prob, dropout_u if dropout_u is not None else torch.rand(h.shape, dtype=h.dtype)))
     last = q(tf.conv2d(h, p["Last_layer/weights"]))
     logits = q(tf.resize_bilinear(last, (x.shape[1], x.shape[2])))
     pred = tf.argmax(logits).unsqueeze(-1)

@@ -18,13 +18,11 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "igemm4.hip", "dense1x1.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
 HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]   # host-only C++ (g++), linked into the same library
 HOST_LIBS = ["-lz"]
-# per-source extra flags: the 4-wave 128x128 GEMM keeps its accumulators in
-# VGPRs and the MFMA operands in AGPRs (the default form copies acc through
-# AGPRs every MFMA and spills)
-EXTRA_FLAGS = {"igemm4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# per-source extra compiler flags
+EXTRA_FLAGS = {}
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",

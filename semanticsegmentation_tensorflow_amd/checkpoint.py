@@ -11,8 +11,9 @@ Saver names:
   the BN `moving_mean` / `moving_variance`, non-trainable `tf.Variable`s such
   as the accumulate template's accumulators and `global_step`, int64);
 * the Adam slots as `<name>/Adam` and `<name>/Adam_1`;
-* the optimizer's `beta1_power` / `beta2_power` (beta^t, float32, as TF keeps
-  them) -- the Adam step t is restored from these, as TF does.
+* the optimizer's `beta1_power` / `beta2_power` (beta^(t+1) after t updates,
+  float32, as TF1's AdamOptimizer keeps them: created at beta, multiplied by
+  beta after every update) -- the Adam step t is restored from these.
 
 plus TF's `checkpoint` state file, so `get_checkpoint_state(dir)
 .model_checkpoint_path` works as in the reference.  `restore` reads bundles
@@ -37,14 +38,18 @@ def _npz(path):
 
 
 def _adam_step(d):
-    """Adam t from TF's beta powers (float32 beta^t; 0.9^t underflows past t ~ 980)."""
-    b1 = float(d.get("beta1_power", 0.0))
-    b2 = float(d.get("beta2_power", 0.0))
-    if 0.0 < b1 < 1.0:
-        return int(round(math.log(b1) / math.log(BETA1)))
-    if 0.0 < b2 < 1.0:
-        return int(round(math.log(b2) / math.log(BETA2)))
-    return 0 if b1 >= 1.0 else 10 ** 6
+    """Adam t from TF's beta powers.  TF1's AdamOptimizer creates beta1_power =
+    beta1 and multiplies it by beta1 after every update (_finish), so after t
+    updates it holds beta1^(t+1) (float32).  beta2_power = 0.999^(t+1) stays a
+    normal float32 up to t ~ 87k (0.9^(t+1) goes denormal past t ~ 830), so it
+    decides; beta1_power is the fallback.  No beta powers: step 0."""
+    b1 = float(d.get("beta1_power", BETA1))
+    b2 = float(d.get("beta2_power", BETA2))
+    if 1e-30 < b2 < 1.0:
+        return max(0, int(round(math.log(b2) / math.log(BETA2))) - 1)
+    if 1e-30 < b1 < 1.0:
+        return max(0, int(round(math.log(b1) / math.log(BETA1))) - 1)
+    raise ValueError(f"checkpoint beta powers ({b1!r}, {b2!r}) do not encode an Adam step")
 
 
 class Saver:
@@ -81,8 +86,8 @@ class Saver:
                 out[name + "/Adam"] = store.adam_m(name).cpu().numpy()
                 out[name + "/Adam_1"] = store.adam_v(name).cpu().numpy()
         t = store.step
-        out["beta1_power"] = np.float32(BETA1 ** t)
-        out["beta2_power"] = np.float32(BETA2 ** t)
+        out["beta1_power"] = np.float32(BETA1 ** (t + 1))
+        out["beta2_power"] = np.float32(BETA2 ** (t + 1))
         tf_bundle.write_bundle(path, out)
         d = os.path.dirname(os.path.abspath(path))
         self._kept.append(path)
@@ -118,7 +123,8 @@ class Saver:
             want = tuple(store.by_name[n].shape) if n in store.by_name else tuple(store.aux[n].shape)
             if tuple(np.shape(d[n])) != want:
                 raise ValueError(f"{n}: checkpoint shape {np.shape(d[n])} != variable shape {want}")
-        d = {k: (np.asarray(v, np.float32) if k != "beta_step" else v) for k, v in d.items()}
+        # int64 values (global_step) keep their integer width
+        d = {k: (v if np.asarray(v).dtype.kind in "iu" else np.asarray(v, np.float32)) for k, v in d.items()}
         d["beta_step"] = _adam_step(d) if ("beta1_power" in d or "beta2_power" in d) else store.step
         store.load_state_dict(d)
 

@@ -535,15 +535,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_abl = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "nt4_abl")) {
-        seg::g_nt4_abl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt4")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt4 = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "adam_tr_fused")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         g_adam_tr_fused = value;

@@ -279,11 +279,6 @@ extern int g_tn3_mfast;
 extern int g_tn3_adam_abl;
 extern int g_tn3_half;
 extern int g_nt3_fill;
-extern int g_nt4;
-extern int g_nt4_abl;
-bool nt4_ok(const NTParams& p, int dtype);
-void nt4_info(int M, int N, int K, int cus, int* splits);
-void launch_nt4(NTParams& p, int gridz, int max_m, hipStream_t s);
 extern int g_tn3_stagger_us;
 extern int g_tn3_stag;
 extern int g_nt3_stag;

@@ -747,10 +747,9 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     int bm, bn, splits;
     choose_nt(M, N, K, dtype == SEG_F32 ? 32 : 64, bm, bn, splits);
     if (g_nt_variant == 2 && nt3_applies(N, dtype)) {
-        int s3, s4;
+        int s3;
         nt3_info(M, N, K, num_cus(), &s3);
-        nt4_info(M, N, K, num_cus(), &s4);
-        splits = std::max(splits, std::max(s3, s4));
+        splits = std::max(splits, s3);
     }
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
@@ -853,11 +852,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         return SEG_OK;
     }
     const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, dt_traits<T>::id, nphases, max_m);
-    const bool nt4 = nt3 && is_bf16_v<T> && nt4_ok(p, SEG_BF16);
-    if (nt4) {
-        nt4_info(max_m, p.N, p.K, num_cus(), &splits);
-        if (nphases > 1) splits = 1;
-    } else if (nt3) {
+    if (nt3) {
         nt3_info(max_m, p.N, p.K, num_cus(), &splits);
         if (nphases > 1) splits = 1;
     }
@@ -866,7 +861,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     // tail on igemm_nt2 (256 x 64 / 128 tiles) instead of a 256-wide tile that
     // is 50-80 % padding.  Not with dropout (its counter uses the full row
     // width) or the BN-backward epilogue (per-tile column sums).
-    if (nt3 && !nt4 && splits == 1 && g_nt_nsplit && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128 &&
+    if (nt3 && splits == 1 && g_nt_nsplit && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128 &&
         p.epi.keep_prob >= 1.f && !p.epi.bn_x) {
         const int nh = p.N / 256 * 256;
         NTParams t = p;
@@ -889,8 +884,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     }
     int gridz = nphases;
     if (splits > 1) {
-        const int bk = nt4 ? 32 : BK;
-        const int kt = (p.K + bk - 1) / bk;
+        const int kt = (p.K + BK - 1) / BK;
         p.kt_per_split = (kt + splits - 1) / splits;
         splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
         const size_t need = (size_t)splits * p.M * p.N * sizeof(float);
@@ -898,13 +892,12 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (nt3 && !nt4 && p.partial) {
+    if (nt3 && p.partial) {
         const long tiles = (long)((max_m + 255) / 256) * ((p.N + 255) / 256);
         p.tile_cnt = splitk_fold_ok(tiles, splits, (long)p.M * p.N * 4) ? splitk_counters(tiles) : nullptr;
     }
     const bool folded = p.tile_cnt != nullptr;
-    if (nt4) launch_nt4(p, gridz, max_m, s);
-    else if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
+    if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
     else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
@@ -939,12 +932,10 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
         return "conv_halo";
     }
     if ((dtype == SEG_BF16 || dtype == SEG_F16) && g_nt_variant == 2 && nt3_pick(p, dtype, nphases, max_m)) {
-        const bool nt4 = dtype == SEG_BF16 && nt4_ok(p, SEG_BF16);
-        if (nt4) nt4_info(max_m, p.N, p.K, num_cus(), splits);
-        else nt3_info(max_m, p.N, p.K, num_cus(), splits);
+        nt3_info(max_m, p.N, p.K, num_cus(), splits);
         if (nphases > 1) *splits = 1;
         *bm = *bn = 256;
-        return nt4 ? "igemm_nt4" : "igemm_nt3";
+        return "igemm_nt3";
     }
     return *bm == 256 ? "igemm_nt2" : "igemm_nt";
 }

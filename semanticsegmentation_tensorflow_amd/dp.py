@@ -34,6 +34,13 @@ class DataParallel:
         # collectives covering them: the Session runs their Adam update on a
         # side stream once those complete
         self.on_launch = None
+        # (side, compute) streams while the Session defers split-K filter-
+        # gradient reductions to the side stream: a bucket's all-reduce is
+        # then issued from the side stream after it has caught up with the
+        # compute stream, so it waits for both the kernels enqueued on the
+        # compute stream and the deferred reductions -- without the compute
+        # stream ever waiting on the side stream
+        self.launch_streams = None
 
     def prepare(self, store):
         """Cut the flat gradient buffer into contiguous buckets of at most
@@ -85,8 +92,18 @@ class DataParallel:
         s, e, names = self.buckets[i]
         w = None
         if e > s:
-            w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                async_op=True)
+            if self.launch_streams is not None:
+                import torch
+                side, main = self.launch_streams
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                        async_op=True)
+            else:
+                w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                    async_op=True)
             self.works.append(w)
         self.bucket_work[i] = w
         self.launched[i] = True

@@ -182,8 +182,9 @@ class Session:
         self.store_fused_grads = False   # tests: also write the fused layers' gradients
         self._fused = None               # names updated inside backward this step
         # split-K reductions of filter gradients on a side stream, overlapping
-        # the next layer's input gradient (single process: DP all-reduces need
-        # the reduced gradient on the compute stream)
+        # the next layer's input gradient (with data parallelism each bucket's
+        # all-reduce is issued from that side stream, after it has caught up
+        # with the compute stream)
         self.defer_wgrad_reduce = True
         # Dropout right after a bias-free / ReLU-free conv (FC-DenseNet's
         # Conv2D_Block + dropout) applied in the conv epilogue
@@ -270,7 +271,11 @@ class Session:
         else:
             value = G.const_value(val)
         if var.var_name in store.aux:
-            ops.fill(store.aux[var.var_name], value)
+            t = store.aux[var.var_name]
+            if t.dtype == torch.int64:
+                t.fill_(int(round(value)))
+            else:
+                ops.fill(t, value)
             store.aux_version += 1
         else:
             ops.fill(store.param(var.var_name), value)
@@ -302,7 +307,7 @@ class Session:
             t = self.store.aux.get(gs.var_name)
             if t is None:
                 raise ValueError(f"global_step {gs.var_name} must be a non-trainable tf.Variable")
-            t.add_(1.0)
+            t.add_(1)
 
     def _train_spec(self, fetches):
         """The gradient-consuming fetches of one run call as one spec:
@@ -561,6 +566,11 @@ class Session:
                 continue
             us = users.get(id(out), [])
             if len(us) != 1 or us[0].kind != "bn" or us[0].inputs[0] is not out:
+                continue
+            if id(us[0]) in p.folded:
+                # that BN runs inside a 1x1 conv's operand prologue and its
+                # backward inside that conv's input-gradient epilogue, which has
+                # no dropout stage: the conv keeps its own mask re-draw
                 continue
             p.drop_fold[id(us[0])] = c
             p.drop_folded.add(id(c))
@@ -1067,12 +1077,14 @@ class Session:
                     and not scaled and p.adam_fusable:
                 self._fused = (opt, gs, set())
             self._red = None
-            if self.defer_wgrad_reduce and self.dp is None and self.device.type == "cuda":
+            if self.defer_wgrad_reduce and self.device.type == "cuda":
                 # (with the overlapped optimizer the reductions and each layer's
                 # Adam share the side stream: a layer's reduction precedes its update)
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self.device)
                 self._red = (self._side, torch.cuda.current_stream(self.device))
+                if self.dp is not None:
+                    self.dp.launch_streams = self._red
             if opt is not None and self.overlap_optimizer and self.device.type == "cuda":
                 # per-layer Adam on a side stream as soon as the layer's gradient is final
                 self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set)
@@ -1091,6 +1103,7 @@ class Session:
             if self.dp is not None:
                 self.dp.finish()
                 self.dp.on_launch = None
+                self.dp.launch_streams = None
             if scaled and not self._grads_finite():
                 # overflow in the scaled fp16 gradients: no update this step
                 # (TF LossScaleOptimizer), halve the scale
@@ -1212,6 +1225,19 @@ class Session:
             if acc is not None:
                 ops.add(acc, dst, acc)
 
+        def gdst(name):
+            """Where a variable's gradient is written: its slice of the flat
+            buffer when it is in var_list; otherwise a scratch sink, so the
+            slices the data-parallel buckets release up front (never_ready) are
+            not written while their all-reduce may be reading them."""
+            if name in p.var_set:
+                return store.grad(name)
+            t = p.tmp.get(("gscratch", name))
+            if t is None:
+                t = torch.zeros_like(store.grad(name))
+                p.tmp[("gscratch", name)] = t
+            return t
+
         ginit = set()      # aliased-concat roots whose gradient buffer holds data this step
 
         def adest(t):
@@ -1275,22 +1301,23 @@ class Session:
                         p.tmp[("dz", id(n.output))] = dz
                     ops.dropout_bwd_ch(dy, dz, n.desc.k_valid, n.kp_val, n.seed_val)
                     if n.bias is not None:
-                        fused_db = store.grad(n.bias.var_name)
+                        fused_db = gdst(n.bias.var_name)
                 elif id(n) in p.mask_fuse or (n.bias is not None and not n.relu):
                     # gradient arrives masked (or there is no ReLU): BiasAddGrad is
                     # summed by the filter-gradient launch below
                     if n.bias is not None:
-                        fused_db = store.grad(n.bias.var_name)
+                        fused_db = gdst(n.bias.var_name)
                 elif n.relu or n.bias is not None:
                     scale = 1.0 / n.kp_val if (n.kp_val is not None and n.kp_val < 1.0) else 1.0
                     dz = p.tmp.get(("dz", id(n.output)))
                     if dz is None:
                         dz = torch.zeros_like(yb)
                         p.tmp[("dz", id(n.output))] = dz
-                    db = store.grad(n.bias.var_name) if n.bias is not None else None
+                    db = gdst(n.bias.var_name) if n.bias is not None else None
                     K = n.desc.k_valid
                     self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
                 dx = None
+                dx_base = None
                 pro = getattr(n, "pro", None)
                 if (id(x) in ng and pro is not None and self.fuse_bn_bwd and id(pro.inputs[0]) in ng
                         and ops.conv_bwd_data_bn_workspace(n.desc) > 0):
@@ -1306,7 +1333,7 @@ class Session:
                     gn, bn_ = pro.gamma.var_name, pro.beta.var_name
                     self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
-                                store.param(bn_), dxb, store.grad(gn), store.grad(bn_), pro.eps, pro.relu, accf, ws)
+                                store.param(bn_), dxb, gdst(gn), gdst(bn_), pro.eps, pro.relu, accf, ws)
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
                 elif (id(x) in ng and id(n) in p.bn_before and self.fuse_bn_bwd
@@ -1324,16 +1351,20 @@ class Session:
                     gn, bn_ = b.gamma.var_name, b.beta.var_name
                     self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
-                                store.param(bn_), dxb, store.grad(gn), store.grad(bn_), b.eps, b.relu, False, ws,
+                                store.param(bn_), dxb, gdst(gn), gdst(bn_), b.eps, b.relu, False, ws,
                                 None, drop)
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
                 elif id(x) in ng:
                     dx, acc = dest(x)
                     mepi = self._mask_epi(p, x)
-                    if acc is not None and mepi is None and self.fuse_grad_sum and self.capture is None:
+                    if acc is not None and mepi is None and self.fuse_grad_sum:
                         # a further consumer's contribution: accumulated in the
                         # epilogue, in place (residual = the gradient so far)
+                        if self.capture is not None:
+                            # tests: the sum before this launch (an extra copy on
+                            # the stream; the launch plan is unchanged)
+                            dx_base = acc.clone()
                         self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
                                     store.packed[(n.w.var_name, ops.PACK_HWIO)][0], acc, ws, None,
                                     ops.epilogue(residual=acc))
@@ -1344,15 +1375,22 @@ class Session:
                         done(dx, acc)
                 if self.capture is not None:
                     # tests: the buffers of this layer's three kernels (they persist
-                    # after the step; dx before any accumulation of other consumers;
-                    # None when it went straight through a folded BN backward)
+                    # after the step; dx before any accumulation of later consumers,
+                    # or -- accumulated in the epilogue -- with dx_base, the sum it
+                    # was added to; None when it went straight through a folded BN
+                    # backward)
                     mask = self._mask_epi(p, x) if dx is not None else None
                     self.capture.append({"kind": "conv", "name": n.w.var_name, "bias": getattr(n.bias, "var_name", None),
                                          "x": buf[id(x)] if pro is None else buf[id(pro.inputs[0])],
                                          "pro": None if pro is None else (pro.gamma.var_name, pro.beta.var_name,
                                                                           pro.eps, pro.relu),
-                                         "y": buf[id(n.output)], "dz": dz, "dx": dx,
-                                         "dx_masked": mask is not None, "relu": n.relu, "desc": n.desc,
+                                         "y": buf[id(n.output)], "dz": dz,
+                                         # a copy: later consumers may accumulate into the buffer
+                                         "dx": None if dx is None else dx.clone(), "dx_base": dx_base,
+                                         "dx_masked": mask is not None,
+                                         "mask_scale": (mask.mask_scale if mask is not None else 1.0),
+                                         "relu": n.relu, "keep_prob": n.kp_val, "seed": n.seed_val,
+                                         "fused_adam": False, "desc": n.desc,
                                          "stride": n.stride, "dilation": n.dilation, "padding": n.padding})
                 want_w = n.w.var_name in p.var_set
                 want_b = n.bias is not None and n.bias.var_name in p.var_set
@@ -1374,6 +1412,8 @@ class Session:
                                 store.packed.get((wn, ops.PACK_KRSC)),
                                 store.grad(wn) if self.store_fused_grads else None, fused_db, ws)
                     fdone.add(wn)
+                    if self.capture is not None:
+                        self.capture[-1]["fused_adam"] = True
                 elif self._red is not None:
                     # kernel now, its split-K reduction on the side stream
                     side, main = self._red
@@ -1404,7 +1444,7 @@ class Session:
                 if want_w or want_b:
                     self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
                                 store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w), ws, None,
-                                store.grad(n.bias.var_name) if n.bias is not None else None)
+                                gdst(n.bias.var_name) if n.bias is not None else None)
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
@@ -1467,7 +1507,7 @@ class Session:
                         raise RuntimeError(f"{n.ops[0].name}: folded dropout gradient needs a sole reader")
                     drop = (c.kp_val, c.seed_val, c.desc.k_valid)
                 ops.bn_relu_bwd(buf[id(x)], buf[id(n.output)], dy, dx, store.param(n.gamma.var_name),
-                                store.grad(n.gamma.var_name), store.grad(n.beta.var_name), C, n.relu,
+                                gdst(n.gamma.var_name), gdst(n.beta.var_name), C, n.relu,
                                 n.eps, ws, accumulate=accf, beta=store.param(n.beta.var_name), dropout=drop)
                 done(dx, acc)
                 self._grad_ready([n.gamma.var_name, n.beta.var_name])

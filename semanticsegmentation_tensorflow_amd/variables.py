@@ -39,6 +39,10 @@ def init_value(var: G.Variable, seed: int = 0) -> np.ndarray:
     raise TypeError(f"unsupported initializer {ini!r}")
 
 
+def _aux_dtype(var):
+    return torch.int64 if getattr(var, "dtype", None) == G.int64 else torch.float32
+
+
 class VariableStore:
     """Trainable variables in the flat buffers (`vars`, backward order);
     non-trainable ones (the accumulate template's gradient accumulators,
@@ -65,7 +69,9 @@ class VariableStore:
         self.v = torch.zeros(off, dtype=torch.float32, device=device)
         self.by_name = {v.var_name: v for v in self.vars}
         self.aux_by_name = {v.var_name: v for v in self.aux_vars}
-        self.aux = {v.var_name: torch.zeros(tuple(v.shape), dtype=torch.float32, device=device)
+        # int64 non-trainables (global_step) stay int64, as TF keeps them: an
+        # fp32 counter stops advancing at 2^24
+        self.aux = {v.var_name: torch.zeros(tuple(v.shape), dtype=_aux_dtype(v), device=device)
                     for v in self.aux_vars}
         self.aux_version = 0    # bumped when a non-trainable value is written from the host
         self.order = order
@@ -105,7 +111,14 @@ class VariableStore:
             host[o:o + n] = init_value(v, self.seed).reshape(-1)
         self.params.copy_(torch.from_numpy(host).to(self.device))
         for v in self.aux_vars:
-            self.aux[v.var_name].copy_(torch.from_numpy(init_value(v, self.seed)).to(self.device))
+            t = self.aux[v.var_name]
+            if t.dtype == torch.int64:
+                ini = v.initializer
+                val = np.full(tuple(v.shape), int(ini.value), np.int64) if isinstance(ini, G.constant_initializer) \
+                    else np.rint(np.asarray(ini(tuple(v.shape)), np.float64)).astype(np.int64)
+                t.copy_(torch.from_numpy(np.asarray(val, np.int64).reshape(tuple(v.shape))).to(self.device))
+            else:
+                t.copy_(torch.from_numpy(init_value(v, self.seed)).to(self.device))
         self.aux_version += 1
         self.m.zero_()
         self.v.zero_()
@@ -113,6 +126,12 @@ class VariableStore:
         self.version += 1
 
     def assign(self, name, value):
+        if name in self.aux and self.aux[name].dtype == torch.int64:
+            a = np.asarray(value)
+            a = a.astype(np.int64) if a.dtype.kind in "iu" else np.rint(a).astype(np.int64)
+            self.aux[name].copy_(torch.from_numpy(a).to(self.device).view(self.aux[name].shape))
+            self.aux_version += 1
+            return
         t = torch.as_tensor(np.asarray(value, dtype=np.float32)).to(self.device)
         if name in self.aux:
             self.aux[name].copy_(t.view(self.aux[name].shape))

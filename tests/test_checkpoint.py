@@ -38,7 +38,9 @@ def test_saver_round_trip_tf_names(dry, tmp_path):  # noqa: F811
     assert index["conv6/weights"]["dtype"] == 1                            # DT_FLOAT
     assert index["conv_t3/weights"]["shape"] == (16, 16, 2, 256)           # [kh, kw, out, in]
     z = tf_bundle.read_bundle(path, ["beta1_power", "conv_t3/bias/Adam_1"])
-    assert abs(float(z["beta1_power"]) - 0.9 ** 7) < 1e-7
+    # TF1 Adam: beta1_power starts at beta1 and is multiplied after every
+    # update, so after 7 steps it holds 0.9^8
+    assert abs(float(z["beta1_power"]) - 0.9 ** 8) < 1e-7
     assert float(z["conv_t3/bias/Adam_1"][0]) == 0.5
     ref = {v.var_name: st.read(v.var_name) for v in st.vars}
     # clobber and restore
@@ -85,3 +87,37 @@ def test_saver_global_step_variable_and_bn_stats(dry, tmp_path):  # noqa: F811
     sess.assign("global_step", 0)
     saver.restore(sess, path)
     assert float(sess.variable_value("global_step")) == 12.0
+
+
+def test_saver_beta_powers_at_step0_and_large_steps(dry, tmp_path):  # noqa: F811
+    """a save before the first update writes TF's initial
+    beta1_power = 0.9 (not 1.0, which makes TF's lr_t 0/0); the step is
+    recovered from beta2_power where 0.9^(t+1) has gone denormal; global_step
+    round-trips as an int64 beyond float32's 2^24."""
+    from semanticsegmentation_tensorflow_amd import checkpoint as C
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, 32, 32, 3])
+    FCN(image, 1.0, 2).create()
+    gstep = tf.Variable(0, trainable=False, name="global_step")
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="f32")
+    sess.run(tf.global_variables_initializer())
+    saver = tf.train.Saver(tf.global_variables())
+    p0 = saver.save(sess, str(tmp_path / "a" / "m"))
+    z = tf_bundle.read_bundle(p0, ["beta1_power", "beta2_power"])
+    assert float(z["beta1_power"]) == np.float32(0.9) and float(z["beta2_power"]) == np.float32(0.999)
+    sess.store.step = 5
+    saver.restore(sess, p0)
+    assert sess.store.step == 0
+    big = 2 ** 24 + 3
+    sess.assign("global_step", big)
+    sess.store.step = 2000
+    p1 = saver.save(sess, str(tmp_path / "b" / "m"), global_step=gstep)
+    assert p1.endswith(f"m-{big}")
+    sess.assign("global_step", 0)
+    sess.store.step = 0
+    saver.restore(sess, p1)
+    assert sess.store.step == 2000
+    assert int(sess.variable_value("global_step")) == big
+    # TF-written powers: 0.9^(t+1) denormal / zero, 0.999^(t+1) still normal
+    assert C._adam_step({"beta1_power": np.float32(0.0), "beta2_power": np.float32(0.999 ** 5001)}) == 5000
+    assert C._adam_step({}) == 0

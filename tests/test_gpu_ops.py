@@ -17,8 +17,8 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9],
-                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3", "nt4"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8],
+                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3"])
 def ntv(request, dev):
     """Run NT tests on every kernel generation: 1 = register-staged GEMM,
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
@@ -28,8 +28,7 @@ def ntv(request, dev):
     end), 6 = 3 with four phases per iteration, 7 = 3 with the two-phase kernel also for N <= 128 (off by default),
     8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
     (by default only where its grid fills half the CUs; variant 2 keeps it
-    off so igemm_nt2 stays covered for wide N), 9 = 8 with the four-wave
-    128x128-per-wave GEMM (igemm_nt4) in place of igemm_nt3.  Variant 8 also
+    off so igemm_nt2 stays covered for wide N).  Variant 8 also
     turns off the 2-stage short-K igemm_nt2 (K <= 128), so the 3-stage ring
     stays covered for those problems.  N <= 128 halo problems without split-K
     run the two-blocks-per-CU conv_halo_duo except in variants 4 and 6."""
@@ -43,12 +42,10 @@ def ntv(request, dev):
     ops.set_option("halo_phases", 4 if v == 6 else 2)
     ops.set_option("halo2_n128", 1 if v == 7 else 0)
     ops.set_option("halo_duo", 0 if v in (4, 6) else 1)   # 4 / 6 keep the one-block conv_halo covered
-    ops.set_option("nt3_fill", 0 if v in (8, 9) else 1)   # small test problems: force the 256x256 tiles
-    ops.set_option("nt4", 1 if v == 9 else 0)
+    ops.set_option("nt3_fill", 0 if v == 8 else 1)   # small test problems: force the 256x256 tiles
     ops.set_option("nt2_short", 0 if v == 8 else 8)
     yield v
     ops.set_option("nt2_short", 8)
-    ops.set_option("nt4", 0)
     ops.set_option("nt3_fill", 1)
     ops.set_option("igemm_nt_variant", 2)
     ops.set_option("nt_halo", 1)
@@ -266,9 +263,7 @@ def test_tconv2d_fwd_bias_residual(dev, ntv, case, dtype):
     assert_close(from_dev(y, Co), ref, dtype, f"tconv fwd {case}")
 
 
-@pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("case", TCONV_CASES)
-def test_tconv2d_grads(dev, ntv, tnv, case, dtype):
+def _tconv_grad_case(case, dtype, dev):
     N, IH, IW, Ci, OH, OW, Co, k, s = case
     x, w, _ = _tconv_case(case, 6)
     xr = rnd(x, dtype).requires_grad_(True)
@@ -278,15 +273,32 @@ def test_tconv2d_grads(dev, ntv, tnv, case, dtype):
     dy = rnd(torch.randn(y.shape, generator=g, dtype=torch.float64), dtype)
     (y * dy).sum().backward()
     d = ops.tconv_desc(N, IH, IW, Ci, OH, OW, Co, k, k, s, "SAME", DT[dtype])
-    dyd = to_dev(dy, dtype, dev)
+    return x, w, xr, wr, dy, d
+
+
+# the input gradient runs the NT kernels, the filter gradient the TN ones:
+# each is swept over its own kernel generations (not their cross product)
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", TCONV_CASES)
+def test_tconv2d_bwd_data(dev, ntv, case, dtype):
+    N, IH, IW, Ci, OH, OW, Co, k, s = case
+    x, w, xr, wr, dy, d = _tconv_grad_case(case, dtype, dev)
     wb = _pack(w, ops.PACK_TCONV_BWD, dtype, dev, ops.tconv_filter_apad(d))
     dx = torch.full((N, IH, IW, d.C), float("nan"), dtype=dtype, device=dev)
-    ops.tconv2d_bwd_data(d, dyd, wb, dx)
-    dw = torch.full((k, k, Co, Ci), float("nan"), dtype=torch.float32, device=dev)
-    db = torch.full((Co,), float("nan"), dtype=torch.float32, device=dev)
-    ops.tconv2d_bwd_filter(d, to_dev(x, dtype, dev), dyd, dw, dbias=db)
+    ops.tconv2d_bwd_data(d, to_dev(dy, dtype, dev), wb, dx)
     torch.cuda.synchronize()
     assert_close(from_dev(dx, Ci), xr.grad, dtype, f"tconv bwd_data {case}")
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("case", TCONV_CASES)
+def test_tconv2d_bwd_filter(dev, tnv, case, dtype):
+    N, IH, IW, Ci, OH, OW, Co, k, s = case
+    x, w, xr, wr, dy, d = _tconv_grad_case(case, dtype, dev)
+    dw = torch.full((k, k, Co, Ci), float("nan"), dtype=torch.float32, device=dev)
+    db = torch.full((Co,), float("nan"), dtype=torch.float32, device=dev)
+    ops.tconv2d_bwd_filter(d, to_dev(x, dtype, dev), to_dev(dy, dtype, dev), dw, dbias=db)
+    torch.cuda.synchronize()
     tol = 2e-5 if dtype == torch.float32 else 2e-3
     assert_close(dw.double().cpu(), wr.grad, dtype, f"tconv bwd_filter {case}", tol)
     assert_close(db.double().cpu(), dy.sum(dim=(0, 1, 2)), dtype, f"tconv bias grad {case}", 2e-5)
