@@ -692,7 +692,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 4) return SEG_EINVAL;
+        if (value < 0 || value > 6) return SEG_EINVAL;
         seg::g_nt2_ablate = value;
         return SEG_OK;
     }

@@ -583,7 +583,8 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 // SIMD).  Every DMA wait precedes a barrier that the other group passes before
 // its reads of that data; the extra barrier is paid back after the loop.
 // ABL (diagnostic builds, garbage results): 1 = no DMA in the loop, 2 = no
-// MFMA, 3 = no LDS fragment reads.
+// MFMA, 3 = no LDS fragment reads, 4 = no halo DMA in the loop, 5 = no filter
+// DMA in the loop, 6 = DMA issued but never waited for.
 // PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
 // both B halves read in the first).
 template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16>
@@ -758,7 +759,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             read_a(0);
             read_b(0);
             read_b(1);
-            if (ABL != 1 && it + 1 < iters) issue_b(bbuf ^ 1);
+            if (ABL != 1 && ABL != 5 && it + 1 < iters) issue_b(bbuf ^ 1);
             __builtin_amdgcn_s_barrier();
             mma(0, 0);
             mma(0, 1);
@@ -768,9 +769,9 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             // after the leading group's next barrier): half an iteration for
             // the slice to land; unstaggered, the wait closes the iteration.
             read_a(1);
-            const bool hp = ABL != 1 && tap < h_n && kc + 1 < kc_end;
+            const bool hp = ABL != 1 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
             if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
-            if constexpr (STAG) {
+            if constexpr (STAG && ABL != 6) {
                 if (hp) wait_vmcnt<1>();
                 else wait_vmcnt<0>();
             }
@@ -1643,6 +1644,9 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
             if (g_nt2_ablate == 1) hipLaunchKernelGGL((conv_halo2<16, true, 1, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 2) hipLaunchKernelGGL((conv_halo2<16, true, 2, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 3) hipLaunchKernelGGL((conv_halo2<16, true, 3, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 4) hipLaunchKernelGGL((conv_halo2<16, true, 4, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 5) hipLaunchKernelGGL((conv_halo2<16, true, 5, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 6) hipLaunchKernelGGL((conv_halo2<16, true, 6, 2>), grid, dim3(512), 0, s, p, g);
             return;
         }
         if (g_halo_phases == 2) {
