@@ -412,8 +412,6 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             seg::WgradPlan wp;
             if (seg::smallc_wgrad_ok(p, d->dtype)) {
                 fam = "wgrad_c8"; bm = 72; bn = p.N; sp = seg::smallc_wgrad_splits(p, seg::device_cus());
-            } else if (seg::g_tn_variant == 2 && seg::wgrad_img_ok(p, d->dtype)) {
-                fam = "wgrad_img"; bm = p.M / p.Cg * 16; bn = 32; sp = 1;
             } else if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
             } else if (seg::g_tn_variant == 2 && seg::tn3_ok(p, d->dtype)) {
@@ -693,13 +691,8 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_halo_wide = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "wgrad_img")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_wgrad_img = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 6) return SEG_EINVAL;
+        if (value < 0 || value > 8) return SEG_EINVAL;
         seg::g_nt2_ablate = value;
         return SEG_OK;
     }
@@ -919,7 +912,7 @@ static bool wgrad_adam_params(const seg_conv_desc* d, TNParams* out) {
     if (seg::smallc_wgrad_ok(p, d->dtype)) return false;
     seg::WgradPlan wp;
     if (seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) return false;
-    if (!seg::wgrad_img_ok(p, d->dtype) && !seg::tn3_adam_ok(p, d->dtype)) return false;
+    if (!seg::tn3_adam_ok(p, d->dtype)) return false;
     *out = p;
     return true;
 }
@@ -983,8 +976,7 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.abl = seg::g_tn3_adam_abl;
     p.Mp = p.M;
     p.partial = nullptr;
-    if (seg::wgrad_img_ok(p, SEG_BF16)) seg::launch_wgrad_img(p, (hipStream_t)stream);
-    else seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
+    seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
     SEG_CHECK_LAUNCH();
     if (tr_after) {
         const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;

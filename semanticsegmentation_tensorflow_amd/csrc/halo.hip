@@ -584,7 +584,8 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 // its reads of that data; the extra barrier is paid back after the loop.
 // ABL (diagnostic builds, garbage results): 1 = no DMA in the loop, 2 = no
 // MFMA, 3 = no LDS fragment reads, 4 = no halo DMA in the loop, 5 = no filter
-// DMA in the loop, 6 = DMA issued but never waited for.
+// DMA in the loop, 6 = DMA issued but never waited for, 7 = every DMA piece
+// reads the zero page (same instructions, no L2 traffic), 8 = 1 + 3.
 // PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
 // both B halves read in the first).
 template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16>
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     const unsigned ldsB = lds0 + 2 * HBUF;
 
     auto load_halo = [&](int h, int kc, int buf) {
-        const void* src = h_off[h] >= 0 ? (const void*)(X + h_off[h] + kc * 64) : zero;
+        const void* src = (ABL != 7 && h_off[h] >= 0) ? (const void*)(X + h_off[h] + kc * 64) : zero;
         glds16(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
     };
     int b_kc = kc_begin, b_j = 0, b_i = 0;
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         const long wtap = (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {
-            const void* src = b_off[i] >= 0 ? (const void*)(Wt + b_off[i] + wtap) : zero;
+            const void* src = (ABL != 7 && b_off[i] >= 0) ? (const void*)(Wt + b_off[i] + wtap) : zero;
             glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
         }
         if (++b_i == p.taps_w) {
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi) {
                     const int row = rowbase[mh * 4 + mi] + toff;
-                    if constexpr (ABL == 3) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
+                    if constexpr (ABL == 3 || ABL == 8) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
                     else af[ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
@@ -706,7 +707,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
                 for (int ni = 0; ni < NFH; ++ni) {
                     const int row = wn * WTN + nh * (WTN / 2) + ni * 16 + fr;
-                    if constexpr (ABL == 3) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
+                    if constexpr (ABL == 3 || ABL == 8) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
                     else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
@@ -759,7 +760,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             read_a(0);
             read_b(0);
             read_b(1);
-            if (ABL != 1 && ABL != 5 && it + 1 < iters) issue_b(bbuf ^ 1);
+            if (ABL != 1 && ABL != 8 && ABL != 5 && it + 1 < iters) issue_b(bbuf ^ 1);
             __builtin_amdgcn_s_barrier();
             mma(0, 0);
             mma(0, 1);
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             // after the leading group's next barrier): half an iteration for
             // the slice to land; unstaggered, the wait closes the iteration.
             read_a(1);
-            const bool hp = ABL != 1 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
+            const bool hp = ABL != 1 && ABL != 8 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
             if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
             if constexpr (STAG && ABL != 6) {
                 if (hp) wait_vmcnt<1>();
@@ -1647,6 +1648,8 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
             if (g_nt2_ablate == 4) hipLaunchKernelGGL((conv_halo2<16, true, 4, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 5) hipLaunchKernelGGL((conv_halo2<16, true, 5, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 6) hipLaunchKernelGGL((conv_halo2<16, true, 6, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 7) hipLaunchKernelGGL((conv_halo2<16, true, 7, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 8) hipLaunchKernelGGL((conv_halo2<16, true, 8, 2>), grid, dim3(512), 0, s, p, g);
             return;
         }
         if (g_halo_phases == 2) {

@@ -191,9 +191,6 @@ struct TNParams {
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
-bool wgrad_img_ok(const TNParams& p, int dtype);         // wgrad_img.hip: whole-image large-filter wgrad
-void launch_wgrad_img(TNParams& p, hipStream_t s);        // (+ TF1 Adam when p.adam.p)
-extern int g_wgrad_img;
 void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
 size_t tn_workspace(int M, int N, int P, int dtype);

@@ -1063,13 +1063,6 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
         p.dbias = nullptr;
         return SEG_OK;
     }
-    if (sizeof(T) == 2 && g_tn_variant == 2 && !p.adam.p && wgrad_img_ok(p, dt_traits<T>::id)) {
-        // whole-image filter gradient (7x7 conv6): no split-K, bias by the caller
-        launch_wgrad_img(p, s);
-        SEG_CHECK_LAUNCH();
-        if (p.defer) { p.defer[0] = 1; p.defer[1] = p.M; }
-        return SEG_OK;
-    }
     WgradPlan wp;
     if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, dt_traits<T>::id, num_cus(), &wp)) {
         if (p.dbias) p.Mp = p.M + wp.nbias;   // wgrad_halo sums dy columns too (nbias partial rows)

@@ -213,18 +213,3 @@ def test_dropout_before_folded_bn_keeps_its_own_gradient(dry):
     assert c.count("seg_conv2d_bwd_data_bn") == 1
     assert c.count("seg_dropout_bwd_ch") == 1
 
-
-def test_wgrad_img_applicability():
-    """(host) launch choice of csrc/wgrad_img.hip; numerics: tests/test_gpu_wgrad_img.py."""
-    # conv6 at the C2 shape and conv6-like 5x5 / 7x7 take wgrad_img; 3x3
-    # layers keep wgrad_halo; channel counts off the 16 / 32 grid keep igemm_tn3
-    take = [(4, 12, 39, 512, 4096, 7), (1, 5, 7, 32, 64, 7), (3, 12, 30, 32, 96, 5)]
-    # 3x3; C / K off the grid; 160 x 576 (conv6 at 5 x 18: 3 k-steps per image,
-    # too short for the image DMA schedule with several images)
-    keep = [(4, 12, 39, 512, 512, 3), (1, 5, 7, 40, 264, 7), (1, 5, 7, 32, 72, 7), (8, 5, 18, 512, 4096, 7)]
-    for N, H, W, C, K, R in take:
-        d = ops.conv_desc(N, H, W, C, K, R, R, dtype=ops.BF16)
-        assert ops.conv_kernel_info(d, ops.OP_BWD_FILTER)[0].startswith("wgrad_img"), (N, H, W, C, K, R)
-    for N, H, W, C, K, R in keep:
-        d = ops.conv_desc(N, H, W, C, K, R, R, dtype=ops.BF16)
-        assert not ops.conv_kernel_info(d, ops.OP_BWD_FILTER)[0].startswith("wgrad_img"), (N, H, W, C, K, R)
