@@ -100,6 +100,19 @@ int seg_tconv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int OH, in
 /* w_krsc: packed filter [K][R][S][C] in `dtype` (seg_pack_filter mode 0). */
 int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_krsc,
                    const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
+/* Conv2D + bias + ReLU + MaxPool(2x2, stride 2) in one launch: conv_layer
+ * followed by max_pool (Network/model/FCN.py:56-57, :63, :69, :75, :81 with
+ * :158-160).  The conv output is never written: y_pool gets the pooled map
+ * [N][OH/2][OW/2] (row stride ld_pool), idx (may be NULL) the MaxPool
+ * switches in seg_maxpool2x2_fwd_argmax's encoding (row stride ld_idx bytes),
+ * both equal bit for bit to seg_conv2d_fwd + seg_maxpool2x2_fwd_argmax.
+ * 16-bit dtypes, even OH / OW, epilogue bias + ReLU only (no scale / shift /
+ * residual / mask / dropout), and a launch whose kernel has the pooled
+ * epilogue: seg_conv2d_fwd_pool_ok(d) == 1, SEG_EINVAL otherwise. */
+int seg_conv2d_fwd_pool_ok(const seg_conv_desc* d);
+int seg_conv2d_fwd_pool(const seg_conv_desc* d, const void* x, const void* w_krsc,
+                        const seg_epilogue* epi, void* y_pool, int ld_pool, void* idx, int ld_idx,
+                        void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropInput.  w_hwio: packed filter [R][S][C][K] in `dtype`
  * (seg_pack_filter mode 1).  dx may be a channel-slice view (ldx). */
 /* A-operand prologue: the conv reads relu(x * gamma / sqrt(1 + eps) + beta)

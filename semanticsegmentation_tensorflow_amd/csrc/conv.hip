@@ -109,13 +109,17 @@ static seg::EpiParams make_epi(const seg_epilogue* e, int n_valid, long res_img,
 // ---------------------------------------------------------------------------
 // parameter builders (shared by the launchers and the workspace queries)
 // ---------------------------------------------------------------------------
+// diagnostics only: extra elements of row padding in the packed KRSC (fwd) /
+// HWIO (dgrad) filter copies the caller allocated (L2 channel-stride probe)
+static int g_wpad = 0;
+
 static NTParams conv_fwd_params(const seg_conv_desc* d) {
     NTParams p = {};
     p.M = d->N * d->OH * d->OW; p.N = d->K; p.K = d->R * d->S * d->C;
     p.x_img = (long)d->H * d->W * d->ldx; p.IH = d->H; p.IW = d->W; p.C = d->C; p.ldx = d->ldx;
     p.Ha = d->OH; p.Wa = d->OW; p.ish = d->stride_h; p.isw = d->stride_w;
     p.ioh = -d->pad_top; p.iow = -d->pad_left; p.tsh = d->dil_h; p.tsw = d->dil_w; p.taps_w = d->S;
-    p.w_col = (long)d->R * d->S * d->C; p.w_tap = d->C; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
+    p.w_col = (long)d->R * d->S * (d->C + g_wpad); p.w_tap = d->C + g_wpad; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
     p.y_img = (long)d->OH * d->OW * d->ldy; p.OH = d->OH; p.OW = d->OW; p.ldy = d->ldy; p.osh = 1; p.osw = 1;
     return p;
 }
@@ -126,7 +130,7 @@ static NTParams conv_bwd_data_params(const seg_conv_desc* d) {
     p.x_img = (long)d->OH * d->OW * d->ldy; p.IH = d->OH; p.IW = d->OW; p.C = d->K; p.ldx = d->ldy;
     p.Ha = d->H; p.Wa = d->W; p.ish = 1; p.isw = 1;
     p.ioh = d->pad_top; p.iow = d->pad_left; p.tsh = -d->dil_h; p.tsw = -d->dil_w; p.taps_w = d->S;
-    p.w_col = d->K; p.w_tap = (long)d->C * d->K; p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
+    p.w_col = d->K + g_wpad; p.w_tap = (long)d->C * (d->K + g_wpad); p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
     p.y_img = (long)d->H * d->W * d->ldx; p.OH = d->H; p.OW = d->W; p.ldy = d->ldx; p.osh = 1; p.osw = 1;
     p.epi.n_valid = d->C; p.epi.keep_prob = 1.f;
     return p;
@@ -681,6 +685,16 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_halo_phases = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "wpad")) {
+        if (value < 0 || value > 256 || value % 8) return SEG_EINVAL;
+        g_wpad = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "halo_deepb")) {
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_halo_deepb = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "halo_stagger")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_halo_stagger = value;
@@ -692,7 +706,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 8) return SEG_EINVAL;
+        if (value < 0 || value > 12) return SEG_EINVAL;
         seg::g_nt2_ablate = value;
         return SEG_OK;
     }
@@ -717,6 +731,46 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
         SEG_CHECK_LAUNCH();
         return SEG_OK;
     }
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// Conv2D + bias + ReLU + MaxPool 2x2 / 2 in one launch: the pooled epilogue of
+// conv_res64 / conv_halo_duo / conv_halo2 (seg_conv2d_fwd_pool_ok).
+static bool fwd_pool_params(const seg_conv_desc* d, const seg_epilogue* epi, NTParams* out) {
+    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return false;
+    if ((d->OH & 1) || (d->OW & 1) || d->OH < 2 || d->OW < 2) return false;
+    if (epi && (epi->scale || epi->shift || epi->residual || epi->relu_mask || (epi->keep_prob > 0.f && epi->keep_prob < 1.f)))
+        return false;
+    NTParams p = conv_fwd_params(d);
+    p.epi = make_epi(epi, d->k_valid, 0);
+    if (d->dil_w == d->dil_h && seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) return false;
+    if (!seg::nt_pool_ok(p, d->dtype)) return false;
+    *out = p;
+    return true;
+}
+
+extern "C" int seg_conv2d_fwd_pool_ok(const seg_conv_desc* d) {
+    if (!d) return 0;
+    NTParams p;
+    seg_epilogue e = {};
+    e.relu = 1;
+    e.keep_prob = 1.f;
+    return fwd_pool_params(d, &e, &p) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_fwd_pool(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
+                                   void* y_pool, int ld_pool, void* idx, int ld_idx, void* ws, size_t ws_bytes,
+                                   void* stream) {
+    if (!d || !x || !w || !y_pool || ld_pool < d->K || (ld_pool & 7) || (idx && (ld_idx < d->K || (ld_idx & 7))))
+        return SEG_EINVAL;
+    if (((uintptr_t)y_pool & 15) || ((uintptr_t)idx & 7)) return SEG_EALIGN;
+    NTParams p;
+    if (!fwd_pool_params(d, epi, &p)) return SEG_EINVAL;
+    p.x = x; p.w = w; p.y = nullptr;
+    p.epi.pool_y = y_pool;
+    p.epi.pool_idx = reinterpret_cast<unsigned char*>(idx);
+    p.epi.ld_pool = ld_pool;
+    p.epi.ld_idx = ld_idx;
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 

@@ -43,12 +43,68 @@ int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
+int g_halo_deepb = 1;   // conv_halo2: filter slice it+2 issued in phase h1 of iteration it (deep ring)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
     int hwd, hrows, hy0, hx0;   // halo width, rows, origin offset vs tap (0,0)
     int nchunks, kc_per_split;
 };
+
+// MaxPool 2x2 / stride 2 fused into the LDS-staged epilogue (TF's MaxPool after
+// conv_layer's bias + ReLU, Network/model/FCN.py:55-100 / :158-160): wbuf holds
+// this wave's HR staged fp32 rows [rr][SROW] (8 column chunks of 8), row rr =
+// tile pixel ml0 + rr = (oy0 + ml / BW, ox0 + ml % BW), ml0 on an even tile
+// row.  Each lane keeps its column chunk (col0); items = (pooled pixel, chunk).
+// Every value is rounded to T before the comparison, so the pooled map and the
+// switches equal seg_maxpool2x2_fwd_argmax of the unfused conv output bit for
+// bit (first max in (0,0) (0,1) (1,0) (1,1) order; bit 2 = max > 0).
+template <typename T, int BW, int HR>
+__device__ __forceinline__ void pool_epi_rows(const NTParams& p, const char* wbuf, int srow, int ml0, int oy0, int ox0,
+                                              int img, int col0, int lane, const float* bias, const float* scl,
+                                              const float* shf) {
+    static_assert(HR % (2 * BW) == 0 && (HR / 4 * 8) % 64 == 0, "whole pooled rows per half, 64-lane items");
+    constexpr int PPR = BW / 2, NPP = HR / 4;
+    const EpiParams& e = p.epi;
+    const int PH = p.OH >> 1, PW = p.OW >> 1;
+#pragma unroll
+    for (int k = 0; k < NPP * 8 / 64; ++k) {
+        const int pp = (lane >> 3) + 8 * k;
+        const int prow = pp / PPR, pcol = pp - (pp / PPR) * PPR;
+        const int r00 = 2 * prow * BW + 2 * pcol;
+        const int ml = ml0 + r00;
+        const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
+        if (oy + 1 >= p.OH || ox + 1 >= p.OW || col0 >= p.N) continue;
+        float v[4][8];
+        splitk_lds8(wbuf + r00 * srow, v[0]);
+        splitk_lds8(wbuf + (r00 + 1) * srow, v[1]);
+        splitk_lds8(wbuf + (r00 + BW) * srow, v[2]);
+        splitk_lds8(wbuf + (r00 + BW + 1) * srow, v[3]);
+        float m[8];
+        unsigned long long code = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool cv = col0 + j < e.n_valid;
+            float q[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                float x = v[t][j] * scl[j] + shf[j] + bias[j];
+                if (e.relu) x = fmaxf(x, 0.f);
+                q[t] = cv ? to_f32(from_f32<T>(x)) : 0.f;
+            }
+            unsigned a = 0;
+            float mx = q[0];
+            if (q[1] > mx) { mx = q[1]; a = 1; }
+            if (q[2] > mx) { mx = q[2]; a = 2; }
+            if (q[3] > mx) { mx = q[3]; a = 3; }
+            m[j] = mx;
+            code |= (unsigned long long)(a | (mx > 0.f ? 4u : 0u)) << (8 * j);
+        }
+        const long pix = ((long)img * PH + (oy >> 1)) * PW + (ox >> 1);
+        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(e.pool_y) + pix * e.ld_pool + col0) = Chunk<T>::pack(m);
+        if (e.pool_idx) *reinterpret_cast<unsigned long long*>(e.pool_idx + pix * e.ld_idx + col0) = code;
+    }
+}
 
 template <int BW, int HI, int BN, typename T = bf16>
 __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
@@ -529,6 +585,15 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                     *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
                         acc[hh * (TM / 2) + mi][ni][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (BW == 16 && HR == 32 && CPR == 8) {
+            if (e.pool_y) {              // MaxPool fused (bias + ReLU only: no scale / shift here)
+                const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+                const float nil[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                pool_epi_rows<T, BW, HR>(p, wbuf + cch * 32, SROW, wm * WTM + hh * HR, oy0, ox0, img, col0, lane,
+                                         bias, one, nil);
+                continue;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < NRH; ++k) {
             const int rr = rsub + k * RPP;
@@ -585,10 +650,12 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 // ABL (diagnostic builds, garbage results): 1 = no DMA in the loop, 2 = no
 // MFMA, 3 = no LDS fragment reads, 4 = no halo DMA in the loop, 5 = no filter
 // DMA in the loop, 6 = DMA issued but never waited for, 7 = every DMA piece
-// reads the zero page (same instructions, no L2 traffic), 8 = 1 + 3.
+// reads the zero page (same instructions, no L2 traffic), 8 = 1 + 3, 9 = every
+// filter slice from the first slice's address (L1/L2-hot).  10 / 11 / 12: every DMA with
+// cache policy sc1 / nt / sc0 sc1 (valid results).
 // PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
 // both B halves read in the first).
-template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16>
+template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16, bool DB = false>
 __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     constexpr int NW = 8, BM = 256, BN = BNT, BH = BM / BW, HI = 6;
     constexpr int WTN = BN / 4, NFH = WTN / 32;   // per-wave columns, n-fragments per B half
@@ -648,15 +715,15 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 
     auto load_halo = [&](int h, int kc, int buf) {
         const void* src = (ABL != 7 && h_off[h] >= 0) ? (const void*)(X + h_off[h] + kc * 64) : zero;
-        glds16(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
+        glds16p<(ABL >= 10 ? ABL - 9 : 0)>(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
     };
     int b_kc = kc_begin, b_j = 0, b_i = 0;
     auto issue_b = [&](int buf) {
-        const long wtap = (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
+        const long wtap = ABL == 9 ? 0L : (long)((p.rb + p.rstep * b_j) * p.Sfull + (p.sb + p.sstep * b_i)) * p.w_tap + b_kc * 64;
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {
             const void* src = (ABL != 7 && b_off[i] >= 0) ? (const void*)(Wt + b_off[i] + wtap) : zero;
-            glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
+            glds16p<(ABL >= 10 ? ABL - 9 : 0)>(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
         }
         if (++b_i == p.taps_w) {
             b_i = 0;
@@ -674,7 +741,12 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
         issue_b(0);
     }
-    wait_vmcnt<0>();
+    if (DB && iters > 1 && ABL != 1 && ABL != 5 && ABL != 8) {   // slice 1 stays in flight
+        issue_b(1);
+        wait_vmcnt<B_INS>();
+    } else {
+        wait_vmcnt<0>();
+    }
     lds_barrier();
     if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
 
@@ -754,6 +826,49 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             else wait_vmcnt<0>();
             __builtin_amdgcn_s_barrier();
             mma(1, 0);
+            __builtin_amdgcn_s_barrier();
+        } else if constexpr (DB) {
+            // Deep filter ring: h0 moves the WHOLE slice it into registers, so
+            // its buffer is free once both groups' h0 reads have retired (the
+            // lagging group's at the barrier after its h0 MFMAs), and slice
+            // it+2 is issued into it in h1 -- five barrier intervals before
+            // the leading group's h0(it+2) reads it, instead of two.
+            //   leading group (wm 0): halo piece, barrier, slice it+2, MFMAs,
+            //     wait(all but slice it+2), barrier;
+            //   lagging group (wm 1): slice it+2, halo piece, wait(all but
+            //     those), barrier, MFMAs, barrier.
+            // Both waits retire slice it+1 before the barrier after which the
+            // leading group reads it (the leading group's h1 end = the lagging
+            // group's h1 pre-MFMA barrier).
+            read_a(0);
+            read_b(0);
+            read_b(1);
+            __builtin_amdgcn_s_barrier();
+            mma(0, 0);
+            mma(0, 1);
+            __builtin_amdgcn_s_barrier();
+            read_a(1);
+            const bool hp = ABL != 1 && ABL != 8 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
+            const bool bp = ABL != 1 && ABL != 8 && ABL != 5 && it + 2 < iters;
+            if (wm == 1 && bp) issue_b(bbuf);
+            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
+            if (wm == 1 && ABL != 6) {
+                if (bp) {
+                    if (hp) wait_vmcnt<B_INS + 1>();
+                    else wait_vmcnt<B_INS>();
+                } else {
+                    if (hp) wait_vmcnt<1>();
+                    else wait_vmcnt<0>();
+                }
+            }
+            __builtin_amdgcn_s_barrier();
+            if (wm == 0 && bp) issue_b(bbuf);
+            mma(1, 1);
+            mma(1, 0);
+            if (wm == 0 && ABL != 6) {
+                if (bp) wait_vmcnt<B_INS>();
+                else wait_vmcnt<0>();
+            }
             __builtin_amdgcn_s_barrier();
         } else {
             // h0: A0 + whole B slice, 32 MFMAs
@@ -896,6 +1011,13 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                             acc[mh * 4 + mi][ni][r];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (CPR == 8) {
+            if (e.pool_y) {              // MaxPool fused: pooled map + switches only
+                pool_epi_rows<T, BW, 64>(p, wbuf + cch * 32, SROW, wm * 128 + mh * 64, oy0, ox0, img, col0, lane,
+                                         bias, scl, shf);
+                continue;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < NRR; ++k) {
             const int rr = rsub + k * RPP;
@@ -1109,6 +1231,61 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                         acc[mi][ni] = mfma16x16x32<T>(fb[cur][ni], fa[cur][mi], acc[mi][ni]);
                     }
                 }
+        }
+        // ---- MaxPool 2x2 / 2 fused (conv1_2 -> pool1, Network/model/FCN.py:56-57): a
+        // wave's 64 pixels are image rows 2 wm (mi 0, 1) and 2 wm + 1 (mi 2, 3), so a
+        // window's vertical pair sits in one lane (mi, mi + 2) and its horizontal
+        // pair in lanes fr, fr ^ 1; even-fr lanes store 4 pooled channels + switches
+        // (values rounded to T before comparing: bit-equal to the unfused pool).
+        if constexpr (NB == 64 && ABL == 0) {
+            if (e.pool_y) {
+                const int img = t / tpi;
+                const int rem = t - img * tpi;
+                const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+                const int oy = ty * R64_BH + 2 * wm;
+                const int PH = p.OH >> 1, PW = p.OW >> 1;
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi) {
+                    const int ox = tx * R64_BW + mi * 16 + fr;
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const int col0 = wn * WTN + ni * 16 + 4 * fg;
+                        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
+                        const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
+                        T o[4];
+                        unsigned code = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float raw[4] = {acc[mi][ni][j], __shfl_xor(acc[mi][ni][j], 1),
+                                                  acc[mi + 2][ni][j], __shfl_xor(acc[mi + 2][ni][j], 1)};
+                            const bool cv = col0 + j < e.n_valid;
+                            float q[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                float x = raw[u] * sc4[j] + ad4[j];
+                                if (e.relu) x = fmaxf(x, 0.f);
+                                q[u] = cv ? to_f32(from_f32<T>(x)) : 0.f;
+                            }
+                            unsigned a = 0;
+                            float mx = q[0];
+                            if (q[1] > mx) { mx = q[1]; a = 1; }
+                            if (q[2] > mx) { mx = q[2]; a = 2; }
+                            if (q[3] > mx) { mx = q[3]; a = 3; }
+                            o[j] = from_f32<T>(mx);
+                            code |= (a | (mx > 0.f ? 4u : 0u)) << (8 * j);
+                        }
+                        if ((fr & 1) || oy + 1 >= p.OH || ox + 1 >= p.OW || col0 >= p.N) continue;
+                        const long pix = ((long)img * PH + (oy >> 1)) * PW + (ox >> 1);
+                        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(e.pool_y) + pix * e.ld_pool + col0) =
+                            *reinterpret_cast<const uint2*>(o);
+                        if (e.pool_idx) *reinterpret_cast<unsigned*>(e.pool_idx + pix * e.ld_idx + col0) = code;
+                    }
+                }
+                __syncthreads();                     // all taps read the halo
+                commit();                            // next tile's halo (waits for its loads)
+                __syncthreads();
+                continue;
+            }
         }
         // ---- epilogue straight from registers: pixel (mi, fr), channels 4*fg..+3 of (ni)
         {
@@ -1614,7 +1791,10 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
     if (dtype == SEG_F16) {   // half: the production schedules only
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
         if (hp.bn == 256) {
-            if (g_halo_stagger) {
+            if (g_halo_stagger && g_halo_deepb) {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16, true>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16, true>), grid, dim3(512), 0, s, p, g);
+            } else if (g_halo_stagger) {
                 if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
                 else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
             } else {
@@ -1650,10 +1830,17 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
             if (g_nt2_ablate == 6) hipLaunchKernelGGL((conv_halo2<16, true, 6, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 7) hipLaunchKernelGGL((conv_halo2<16, true, 7, 2>), grid, dim3(512), 0, s, p, g);
             if (g_nt2_ablate == 8) hipLaunchKernelGGL((conv_halo2<16, true, 8, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 9) hipLaunchKernelGGL((conv_halo2<16, true, 9, 2>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 10) hipLaunchKernelGGL((conv_halo2<16, true, 10, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 11) hipLaunchKernelGGL((conv_halo2<16, true, 11, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
+            if (g_nt2_ablate == 12) hipLaunchKernelGGL((conv_halo2<16, true, 12, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
             return;
         }
         if (g_halo_phases == 2) {
-            if (g_halo_stagger) {
+            if (g_halo_stagger && g_halo_deepb) {
+                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
+                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
+            } else if (g_halo_stagger) {
                 if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2>), grid, dim3(512), 0, s, p, g);
                 else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2>), grid, dim3(512), 0, s, p, g);
             } else {

@@ -35,6 +35,14 @@ struct EpiParams {
     int bn_cv;
     float* bn_part;
     int bn_C;
+    // MaxPool 2x2 / stride 2 of this conv's output fused into the epilogue
+    // (conv_res64, conv_halo_duo, conv_halo2): the conv output is not written;
+    // pool_y [img][OH/2][OW/2][ld_pool] gets the pooled map, pool_idx (may be
+    // null) the switches in seg_maxpool2x2_fwd_argmax's encoding (row stride
+    // ld_idx bytes).  Whole windows only (OH, OW even; checked by the host).
+    void* pool_y;
+    unsigned char* pool_idx;
+    int ld_pool, ld_idx;
 };
 
 // dgamma / dbeta from per-tile partial rows [nrows][2C] (eltwise.hip);
@@ -190,6 +198,7 @@ struct TNParams {
 };
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
+bool nt_pool_ok(const NTParams& p, int dtype);   // launch_nt's kernel fuses EpiParams::pool_y
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
@@ -299,6 +308,7 @@ struct HaloPlan {
 extern int g_nt_halo;
 extern int g_halo_wide;
 extern int g_halo_stagger;
+extern int g_halo_deepb;
 extern int g_halo_phases;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);

@@ -913,6 +913,24 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     return SEG_OK;
 }
 
+// Whether launch_nt's kernel for p has the fused MaxPool epilogue (EpiParams
+// pool_y): conv_res64 with 64-wide output blocks, conv_halo_duo with 16-px tile
+// rows and 64-column wave tiles, conv_halo2's 256-wide tiles -- each without
+// split-K (host-only mirror of launch_nt_typed / launch_halo's choices).
+bool nt_pool_ok(const NTParams& p, int dtype) {
+    if ((dtype != SEG_BF16 && dtype != SEG_F16) || g_nt_variant != 2 || p.pro.gamma || p.phase) return false;
+    if (res16c_ok(p, dtype)) return false;
+    if (res64_ok(p, dtype)) return !(p.N <= 16 && g_res16);
+    int bm, bn, splits;
+    choose_nt(p.M, p.N, p.K, 64, bm, bn, splits);
+    HaloPlan hp;
+    if (!halo_plan(p, dtype, splits, num_cus(), &hp) || hp.splits != 1 || g_splitk_fold) return false;
+    if (hp.bn == 256) return true;
+    if (hp.bn == 128 && hp.hi == 6 && g_halo_wide && g_halo2_n128) return false;   // conv_halo2<..., 128>
+    // conv_halo_duo (launch_halo_bn's condition) with BW = 16 and BN = 128
+    return hp.bn == 128 && hp.bw == 16 && g_halo_duo && hp.hi == 6 && (long)p.IH * p.IW * p.ldx < (1L << 31);
+}
+
 // The kernel launch_nt would pick for p (host-only mirror of launch_nt_typed).
 const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits) {
     const int bk = dtype == SEG_F32 ? 32 : 64;

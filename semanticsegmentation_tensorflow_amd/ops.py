@@ -157,6 +157,27 @@ def conv2d_fwd(desc, x, w_krsc, y, epi=None, ws=None, stream=None):
     return y
 
 
+def conv2d_fwd_pool_ok(desc):
+    """Whether seg_conv2d_fwd_pool (Conv2D + bias + ReLU + MaxPool 2x2/2 in one
+    launch) takes this convolution."""
+    return bool(_lib.lib().seg_conv2d_fwd_pool_ok(ctypes.byref(desc)))
+
+
+def conv2d_fwd_pool(desc, x, w_krsc, y_pool, idx=None, epi=None, ws=None, stream=None):
+    """Conv2D + epilogue (bias, ReLU) + MaxPool 2x2 / 2: writes the pooled map
+    y_pool [N, OH/2, OW/2, K] and, when idx is given, the switches
+    (maxpool2x2_fwd_argmax's encoding, row stride = y_pool's channel count);
+    the conv output itself is never materialised."""
+    d = _with_ld(desc, x, None)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_FWD))
+    check(_lib.lib().seg_conv2d_fwd_pool(ctypes.byref(d), ptr(x), ptr(w_krsc),
+                                         None if epi is None else ctypes.byref(epi), ptr(y_pool),
+                                         pixel_stride(y_pool), None if idx is None else ptr(idx),
+                                         y_pool.shape[3] if idx is not None else 0, wsp, wss,
+                                         stream_ptr(stream)), "conv2d_pool")
+    return y_pool
+
+
 def prologue(gamma, beta, eps=1e-3, relu=True):
     """The conv input is relu(x * gamma / sqrt(1 + eps) + beta) (frozen BN + ReLU).
     The struct keeps gamma / beta alive (it holds raw device pointers)."""

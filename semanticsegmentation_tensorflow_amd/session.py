@@ -197,6 +197,8 @@ class Session:
         # a tensor's later input-gradient contributions accumulate in the epilogue
         self.fuse_grad_sum = os.environ.get("SEG_FUSE_GRAD_SUM", "1") != "0"
         self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
+        # conv (+bias +ReLU) -> 2x2 MaxPool as one launch (pooled epilogue)
+        self.fuse_pool = os.environ.get("SEG_FUSE_POOL", "1") != "0"
         self._red = None                 # (side stream, compute stream) during a step
         self._side = None
         self._adam_ctx = None
@@ -508,6 +510,7 @@ class Session:
             else:
                 raise NotImplementedError(f"op {t} is not on the hot path")
         p.nodes = nodes
+        p.fetched = fetched
         self._fold_bn_prologues(p, fetched)
         self._fold_dropout_grads(p, fetched)
         self._allocate(p, consumers, feeds)
@@ -799,6 +802,7 @@ class Session:
                 if ops.maxpool_argmax_fits(xb):
                     N, H, W, C = xb.shape
                     p.pool_idx[id(n)] = torch.empty(N * (H // 2) * (W // 2) * C, dtype=torch.uint8, device=dev)
+        self._plan_pool_fusion(p, consumers)
         ws_need = max(ws_need, 8192)
         self.ws.get(ws_need)
         # packed filter copies
@@ -814,6 +818,34 @@ class Session:
         # gradient buffers / plan for backward
         if p.train:
             self._plan_backward(p)
+
+    def _plan_pool_fusion(self, p, consumers):
+        """conv_layer -> max_pool (Network/model/FCN.py:56-57, :158-160): a
+        ReLU conv whose only consumer is a 2x2 / 2 MaxPool runs as one launch
+        (ops.conv2d_fwd_pool) that writes the pooled map and the switches; the
+        conv output itself is never materialised (its gradient comes from the
+        switches: MaxPoolGrad's fused ReluGrad)."""
+        p.pool_fuse = {}
+        p.pool_fused = set()
+        if not self.fuse_pool or self.cdt == ops.F32:
+            return
+        for n in p.nodes:
+            if n.kind != "conv" or getattr(n, "pro", None) is not None or n.kp is not None:
+                continue
+            y = n.output
+            cs = consumers.get(id(y), [])
+            if len(cs) != 1 or cs[0].type != "MaxPool" or id(y) in p.fetched or id(y) in p.alias:
+                continue
+            m = next((c for c in p.nodes if c.kind == "MaxPool" and c.ops[0] is cs[0]), None)
+            if m is None or m.inputs[0] is not y:
+                continue
+            if p.train and id(y) in p.needs_grad and id(m) not in p.pool_idx:
+                continue                       # MaxPoolGrad would read the conv output
+            if not ops.conv2d_fwd_pool_ok(n.desc):
+                continue
+            p.pool_fuse[id(n)] = m
+            p.buf[id(y)] = None                # never written
+        p.pool_fused = {id(m) for m in p.pool_fuse.values()}
 
     def _plan_backward(self, p):
         dev = self.device
@@ -996,6 +1028,11 @@ class Session:
                     b = n.pro
                     self._timed(n.desc, ops.OP_FWD_PRO, ops.conv2d_fwd_pro, n.desc, buf[id(b.inputs[0])],
                                 self._prologue(b), store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
+                elif id(n) in p.pool_fuse:
+                    m = p.pool_fuse[id(n)]
+                    self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd_pool, n.desc, x,
+                                store.packed[(n.w.var_name, ops.PACK_KRSC)][0], buf[id(m.output)],
+                                p.pool_idx.get(id(m)), epi, self.ws)
                 else:
                     self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
                                 store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
@@ -1008,7 +1045,9 @@ class Session:
                             store.packed[(n.w.var_name, ops.PACK_TCONV_FWD)][0], y, epi, self.ws)
             elif k == "MaxPool":
                 idx = p.pool_idx.get(id(n))
-                if idx is not None:
+                if id(n) in p.pool_fused:
+                    pass                       # written by the producing conv's pooled epilogue
+                elif idx is not None:
                     ops.maxpool2x2_fwd_argmax(buf[id(n.inputs[0])], y, idx)
                 else:
                     ops.maxpool2x2_fwd(buf[id(n.inputs[0])], y)
@@ -1206,18 +1245,22 @@ class Session:
         ws = self.ws
         ng = p.needs_grad
 
+        def zeros_for(t):
+            # (a pool-fused conv's output has no buffer: only its shape)
+            return torch.zeros_like(buf[id(t)]) if buf[id(t)] is not None else self._act(p.shapes[id(t)])
+
         def dest(t):
             """(buffer to write t's gradient into, accumulate-after flag)."""
             if id(t) not in grad:
                 gbuf = p.tmp.get(("g", id(t)))
                 if gbuf is None:
-                    gbuf = torch.zeros_like(buf[id(t)])
+                    gbuf = zeros_for(t)
                     p.tmp[("g", id(t))] = gbuf
                 grad[id(t)] = gbuf
                 return gbuf, None
             tmp = p.tmp.get(("acc", id(t)))
             if tmp is None:
-                tmp = torch.zeros_like(buf[id(t)])
+                tmp = zeros_for(t)
                 p.tmp[("acc", id(t))] = tmp
             return tmp, grad[id(t)]
 
@@ -1385,6 +1428,10 @@ class Session:
                                          "pro": None if pro is None else (pro.gamma.var_name, pro.beta.var_name,
                                                                           pro.eps, pro.relu),
                                          "y": buf[id(n.output)], "dz": dz,
+                                         # MaxPool fused into the forward: (pooled map, switches)
+                                         "pool": ((buf[id(p.pool_fuse[id(n)].output)],
+                                                   p.pool_idx.get(id(p.pool_fuse[id(n)])))
+                                                  if id(n) in p.pool_fuse else None),
                                          # a copy: later consumers may accumulate into the buffer
                                          "dx": None if dx is None else dx.clone(), "dx_base": dx_base,
                                          "dx_masked": mask is not None,

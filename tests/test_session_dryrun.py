@@ -23,7 +23,8 @@ class _Rec:
         host_only = name in ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace",
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
                              "seg_adam_segments_plan", "seg_tconv_filter_apad",
-                             "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace")
+                             "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace",
+                             "seg_conv2d_fwd_pool_ok")
 
         def fn(*a):
             if host_only:
@@ -59,11 +60,14 @@ def test_fcn_train_plan(dry):
     dry.calls.clear()
     sess.run([train, loss], feed_dict={image: img, labels: lab, keep: 0.8})
     c = dry.calls
-    # forward: 17 fused conv launches, 3 tconv, 5 pools, 1 loss
-    assert c.count("seg_conv2d_fwd") == 17
+    # forward: 17 fused conv launches, 3 tconv, 5 pools, 1 loss; a pool whose
+    # conv's kernel has the pooled epilogue runs inside that conv's launch
+    fused = c.count("seg_conv2d_fwd_pool")
+    assert c.count("seg_conv2d_fwd") + fused == 17
     assert c.count("seg_tconv2d_fwd") == 3
     # train plans record the pool switches; MaxPoolGrad reads them instead of x
-    assert c.count("seg_maxpool2x2_fwd_argmax") == 5
+    assert c.count("seg_maxpool2x2_fwd_argmax") + fused == 5
+    assert fused >= 1                                  # conv1_2 (conv_res64) at least
     assert c.count("seg_softmax_xent_fwd_bwd") == 1
     # backward: conv1_1 needs no input gradient (image is a placeholder)
     assert c.count("seg_conv2d_bwd_data") == 16
@@ -93,7 +97,7 @@ def test_fcn_train_plan(dry):
     (gk, plan), = sess._adam_groups.items()
     assert plan.nsegs == len(sess.store.vars) - 2
     assert "conv6/weights" not in gk[1] and "conv7/weights" not in gk[1]
-    assert dry.calls.count("seg_conv2d_fwd") == 17
+    assert dry.calls.count("seg_conv2d_fwd") + dry.calls.count("seg_conv2d_fwd_pool") == 17
 
 
 def test_adam_segment_plan_host():
@@ -213,3 +217,19 @@ def test_dropout_before_folded_bn_keeps_its_own_gradient(dry):
     assert c.count("seg_conv2d_bwd_data_bn") == 1
     assert c.count("seg_dropout_bwd_ch") == 1
 
+
+
+def test_pool_fusion_choice_at_c2_shapes():
+    """(host) conv -> MaxPool fusion at the benchmarked 4 x 384 x 1248 FCN:
+    conv1_2 (conv_res64), conv2_2 (conv_halo_duo), conv3_3 / conv4_3
+    (conv_halo2 256x256) carry the pooled epilogue; conv5_3 splits K (3 fp32
+    slabs + a reducer) and keeps the separate pool; fp32 never fuses."""
+    take = [(4, 384, 1248, 64, 64), (4, 192, 624, 128, 128), (4, 96, 312, 256, 256), (4, 48, 156, 512, 512)]
+    for N, H, W, C, K in take:
+        d = ops.conv_desc(N, H, W, C, K, 3, 3, dtype=ops.BF16)
+        assert ops.conv2d_fwd_pool_ok(d), (H, W, C, K)
+        assert ops.conv2d_fwd_pool_ok(ops.conv_desc(N, H, W, C, K, 3, 3, dtype=ops.F16)), (H, W, C, K)
+        assert not ops.conv2d_fwd_pool_ok(ops.conv_desc(N, H, W, C, K, 3, 3, dtype=ops.F32))
+    assert not ops.conv2d_fwd_pool_ok(ops.conv_desc(4, 24, 78, 512, 512, 3, 3, dtype=ops.BF16))
+    # odd output size (375 x 1242 unpadded is even; 375 x 1241 is not): no whole windows
+    assert not ops.conv2d_fwd_pool_ok(ops.conv_desc(1, 375, 1241, 64, 64, 3, 3, dtype=ops.BF16))

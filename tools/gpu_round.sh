@@ -13,7 +13,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 cat $OUT/smoke.log
 timeout -k 10 400 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-P="--steps 10 --warmup 3 --no-cpu-baseline --no-traffic --no-miou --no-pipeline --no-extra"
+P="--steps 10 --warmup 3 --no-cpu-baseline --no-traffic --no-miou --no-pipeline --no-extra --no-dp-probe --no-inference"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py $P "$@" > $OUT/prof_bench.json 2> $OUT/prof.err || { echo rocprof failed; tail -20 $OUT/prof.err; exit 1; }
 for m in fcdensenet deeplab; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$m -o run -- python bench.py $P --model $m > $OUT/prof_$m.json 2> $OUT/prof_$m.err || { echo rocprof $m failed; tail -20 $OUT/prof_$m.err; exit 1; }

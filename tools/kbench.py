@@ -26,7 +26,9 @@ LAYERS = {"conv1_1": (384, 1248, 3, 64, 3), "conv1_2": (384, 1248, 64, 64, 3),
           "conv3_1": (96, 312, 128, 256, 3), "conv3_2": (96, 312, 256, 256, 3),
           "conv4_1": (48, 156, 256, 512, 3), "conv4_2": (48, 156, 512, 512, 3),
           "conv5_1": (24, 78, 512, 512, 3), "conv6": (12, 39, 512, 4096, 7), "conv7": (12, 39, 4096, 4096, 1)}
-OPS = {"fwd": ops.OP_FWD, "dgrad": ops.OP_BWD_DATA, "wgrad": ops.OP_BWD_FILTER, "wgrad_adam": ops.OP_BWD_FILTER}
+OPS = {"fwd": ops.OP_FWD, "dgrad": ops.OP_BWD_DATA, "wgrad": ops.OP_BWD_FILTER, "wgrad_adam": ops.OP_BWD_FILTER,
+       "fwdp": ops.OP_FWD, "dgradp": ops.OP_BWD_DATA}
+WPAD = 64   # fwdp / dgradp: packed filter rows padded by WPAD elements (diagnostic option "wpad")
 
 
 def setup(spec, N, dev, ws):
@@ -37,18 +39,29 @@ def setup(spec, N, dev, ws):
     x = (torch.randn(N, H, W, d.C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     dy = (torch.randn(N, d.OH, d.OW, d.K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     w32 = torch.randn(R, R, C, K, device=dev, generator=g) / (R * R * C) ** 0.5
-    if op == "fwd":
-        wk = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, d.C), dtype=torch.bfloat16, device=dev)
-        ops.pack_filter(w32, wk, d.C, d.K, ops.PACK_KRSC)
+    pad = WPAD if op.endswith("p") else 0
+
+    def padded(fn):
+        if not pad:
+            return fn
+
+        def run():
+            ops.set_option("wpad", pad)
+            fn()
+            ops.set_option("wpad", 0)
+        return run
+    if op in ("fwd", "fwdp"):
+        wk = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, d.C + pad), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wk, d.C + pad, d.K, ops.PACK_KRSC)
         y = torch.empty(N, d.OH, d.OW, d.K, dtype=torch.bfloat16, device=dev)
         b = torch.zeros(K, device=dev)
-        return d, op, lambda: ops.conv2d_fwd(d, x, wk, y, ops.epilogue(bias=b, relu=True), ws)
-    if op == "dgrad":
-        wh = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
-        ops.pack_filter(w32, wh, d.C, d.K, ops.PACK_HWIO)
+        return d, op, padded(lambda: ops.conv2d_fwd(d, x, wk, y, ops.epilogue(bias=b, relu=True), ws))
+    if op in ("dgrad", "dgradp"):
+        wh = torch.zeros(ops.packed_shape(R, R, C, K + pad, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wh, d.C, d.K + pad, ops.PACK_HWIO)
         dx = torch.empty(N, H, W, d.C, dtype=torch.bfloat16, device=dev)
         mask = torch.relu(torch.randn(N, H, W, d.C, device=dev, generator=g)).to(torch.bfloat16)
-        return d, op, lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None, ops.epilogue(relu_mask=mask))
+        return d, op, padded(lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None, ops.epilogue(relu_mask=mask)))
     dw = torch.empty(R, R, C, K, device=dev)
     db = torch.empty(K, device=dev)
     if op == "wgrad":
