@@ -524,11 +524,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_halo_duo = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "splitk_fold")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_splitk_fold = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "nt_halo")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt_halo = value;
@@ -590,16 +585,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_s1x1 = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "nt3_stag")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt3_stag = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_stag")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_tn3_stag = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "tn3_half")) {
         if (value < 0 || value > 7) return SEG_EINVAL;
         seg::g_tn3_half = value;
@@ -623,11 +608,6 @@ extern "C" int seg_set_option(const char* name, int value) {
     if (!strcmp(name, "nt3")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_nt3 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "halo2_n128")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_halo2_n128 = value;
         return SEG_OK;
     }
     if (!strcmp(name, "wgrad_nt32")) {
@@ -670,34 +650,14 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_wgrad_nbias = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "wgrad_la")) {
-        if (value < 1 || value > 3) return SEG_EINVAL;
-        seg::g_wgrad_la = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "wgrad_nt")) {
         if (value != 64 && value != 128) return SEG_EINVAL;
         seg::g_wgrad_nt = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "halo_phases")) {
-        if (value != 2 && value != 4) return SEG_EINVAL;
-        seg::g_halo_phases = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "wpad")) {
         if (value < 0 || value > 256 || value % 8) return SEG_EINVAL;
         g_wpad = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "halo_deepb")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_halo_deepb = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "halo_stagger")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_halo_stagger = value;
         return SEG_OK;
     }
     if (!strcmp(name, "halo_wide")) {
@@ -706,7 +666,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 12) return SEG_EINVAL;
+        if (value < 0 || value > 9) return SEG_EINVAL;
         seg::g_nt2_ablate = value;
         return SEG_OK;
     }

@@ -36,14 +36,10 @@ static __device__ uint4 halo_zero_page[4];
 
 int g_nt_halo = 1;
 int g_halo_wide = 1;
-int g_halo_stagger = 1;
-int g_halo_phases = 2;
 int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
-int g_halo2_n128 = 0;   // 2-phase kernel for N <= 128 (measured slower than conv_halo on conv2_x)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
-int g_halo_deepb = 1;   // conv_halo2: filter slice it+2 issued in phase h1 of iteration it (deep ring)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -265,7 +261,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         }
     }
 
-    if (p.partial && !p.tile_cnt) {
+    if (p.partial) {
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -291,36 +287,6 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     const int cch = lane % CPR, rsub = lane / CPR;
     const int col0 = n0 + wn * WTN + cch * 8;
     const EpiParams& e = p.epi;
-    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
-    // store them to its slab (agent-coherent 16-byte stores), count in; the last
-    // split to arrive sums the slabs in the row loop below (splitk_arrive)
-    const bool fold = p.partial != nullptr;
-    if (fold) {
-        char* wb = smem + w * WTM * SROW;
-        const auto rs = splitk_rsrc(p.partial);
-        lds_barrier();
-#pragma unroll
-        for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int ni = 0; ni < TN; ++ni)
-                    *reinterpret_cast<float*>(wb + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                        acc[mi][ni][r];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int k = 0; k < NRR; ++k) {
-            const int rr = rsub + k * RPP;
-            const int ml = wm * WTM + rr;
-            const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
-            float v[8];
-            splitk_lds8(wb + rr * SROW + cch * 32, v);
-            splitk_put8(rs, ((blockIdx.z * (unsigned)p.M + (unsigned)((img * p.OH + oy) * p.OW + ox)) * (unsigned)p.N +
-                             col0) * 4u, v);
-        }
-        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
-    }
     // 16-bit ReluGrad mask rows of this lane, requested before the staging
     uint4 mkv[NRR];
     if constexpr (sizeof(T) == 2) {
@@ -338,7 +304,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
     }
     lds_barrier();
     char* wbuf = smem + w * WTM * SROW;
-    if (!fold) {
+    {
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -366,9 +332,7 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
         const long pix = (long)oy * p.OW + ox;
         float v[8];
-        if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)(img * p.OH * p.OW + pix) * (unsigned)p.N + col0) * 4u,
-                              (unsigned)p.M * p.N * 4u, (int)gridDim.z, v);
-        else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+        splitk_lds8(wbuf + rr * SROW + cch * 32, v);
         float res[8], mk[8];
         if (e.mask) {
             if constexpr (sizeof(T) == 2) {
@@ -629,40 +593,36 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 }
 
 // ---------------------------------------------------------------------------
-// 256 x 256 variant (N > 128): 8 waves as 2 (M) x 4 (N), 128 x 64 per wave,
-// each (chunk, tap) iteration split into 4 phases, one C quadrant
-// (64 px x 32 ch x K=64 = 16 MFMAs) per phase:
-//   reads for the phase -> DMA issue -> [wait] -> barrier -> lgkmcnt(0) ->
-//   setprio(1) MFMA x16 setprio(0) -> barrier
-// Quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0): A halves re-read twice,
-// B halves once per iteration.  LDS: 2 halo buffers + 2 filter slices.
-//   q0 issues filter slice it+1 (4 DMA / wave) into the other slice buffer;
-//   q1 issues one halo piece of chunk+1 (taps < h_n);
-//   q3 waits for slice it+1 (vmcnt(1) if a halo piece is still young), so
-//   the next iteration's q0 reads it after q3's barriers.
-// WAR: a slice / halo buffer is restaged >= 2 phases after its last reads,
-// which every wave retired with lgkmcnt(0) before a barrier.
-// ---------------------------------------------------------------------------
-// STAG: the upper M wave group runs one barrier behind, so on every SIMD one
-// wave's MFMA cluster overlaps the other's LDS reads (waves w and w+4 share a
-// SIMD).  Every DMA wait precedes a barrier that the other group passes before
-// its reads of that data; the extra barrier is paid back after the loop.
+// 256 x 256 variant (N > 128): 8 waves as 2 (M) x 4 (N), 128 x 64 per wave.
+// Each (chunk, tap) iteration is two phases of 32 MFMAs between barriers:
+//   h0: A rows of the wave's first M half + the WHOLE filter slice into
+//       registers, barrier, 32 MFMAs, barrier;
+//   h1: A rows of the second half, the next chunk's halo piece (taps < h_n),
+//       filter slice it+2 into the buffer slice it just left, barrier, 32
+//       MFMAs, barrier.
+// The upper M wave group runs one barrier behind (waves w and w+4 share a
+// SIMD, so one wave's MFMA cluster overlaps the other's LDS reads).  Slice
+// it+2's DMA is issued after both groups' h0 reads of slice it retired (the
+// lagging group's at the barrier after its h0 MFMAs): the leading group
+// issues it after its h1 pre-MFMA barrier, the lagging group before it, and
+// each waits for everything but those pieces before the barrier after which
+// the leading group reads slice it+1 -- five barrier intervals of DMA
+// latency per slice.  LDS: 2 halo buffers + 2 filter slices (160 KiB).
 // ABL (diagnostic builds, garbage results): 1 = no DMA in the loop, 2 = no
 // MFMA, 3 = no LDS fragment reads, 4 = no halo DMA in the loop, 5 = no filter
-// DMA in the loop, 6 = DMA issued but never waited for, 7 = every DMA piece
-// reads the zero page (same instructions, no L2 traffic), 8 = 1 + 3, 9 = every
-// filter slice from the first slice's address (L1/L2-hot).  10 / 11 / 12: every DMA with
-// cache policy sc1 / nt / sc0 sc1 (valid results).
-// PH: phases per iteration, 4 (quadrant per phase) or 2 (A half per phase,
-// both B halves read in the first).
-template <int BW, bool STAG, int ABL = 0, int PH = 4, int BNT = 256, typename T = bf16, bool DB = false>
+// DMA in the loop, 7 = every DMA piece reads the zero page (same
+// instructions, no L2 traffic), 9 = every filter slice from the first slice's
+// address (L1/L2-hot).  Measured (conv4_2 fwd, 4 x 48 x 156 x 512): 116 us;
+// no DMA 99, zero page 97, hot slice 108, no filter DMA 100 -- the filter
+// stream's L2 round trips, not the DMA instructions, cost the difference.
+template <int BW, int ABL = 0, typename T = bf16>
 __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
-    constexpr int NW = 8, BM = 256, BN = BNT, BH = BM / BW, HI = 6;
+    constexpr int NW = 8, BM = 256, BN = 256, BH = BM / BW, HI = 6;
     constexpr int WTN = BN / 4, NFH = WTN / 32;   // per-wave columns, n-fragments per B half
     constexpr int HBUF = HI * NW * 1024;
     constexpr int BBUF = BN * 128;
     constexpr int SMEM = 2 * HBUF + 2 * BBUF;
-    constexpr int B_INS = BN / 8 / NW;   // 4 (BN 256) or 2 (BN 128)
+    constexpr int B_INS = BN / 8 / NW;   // 4
     static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -715,7 +675,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 
     auto load_halo = [&](int h, int kc, int buf) {
         const void* src = (ABL != 7 && h_off[h] >= 0) ? (const void*)(X + h_off[h] + kc * 64) : zero;
-        glds16p<(ABL >= 10 ? ABL - 9 : 0)>(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
+        glds16(src, lds0 + buf * HBUF + (h * NW + w) * 1024);
     };
     int b_kc = kc_begin, b_j = 0, b_i = 0;
     auto issue_b = [&](int buf) {
@@ -723,7 +683,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {
             const void* src = (ABL != 7 && b_off[i] >= 0) ? (const void*)(Wt + b_off[i] + wtap) : zero;
-            glds16p<(ABL >= 10 ? ABL - 9 : 0)>(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
+            glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
         }
         if (++b_i == p.taps_w) {
             b_i = 0;
@@ -741,14 +701,14 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
         issue_b(0);
     }
-    if (DB && iters > 1 && ABL != 1 && ABL != 5 && ABL != 8) {   // slice 1 stays in flight
+    if (iters > 1 && ABL != 1 && ABL != 5) {   // slice 1 stays in flight
         issue_b(1);
         wait_vmcnt<B_INS>();
     } else {
         wait_vmcnt<0>();
     }
     lds_barrier();
-    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
 
     const int fr = lane & 15, fg = lane >> 4;
     int rowbase[8];
@@ -769,7 +729,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi) {
                     const int row = rowbase[mh * 4 + mi] + toff;
-                    if constexpr (ABL == 3 || ABL == 8) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
+                    if constexpr (ABL == 3) af[ks][mi] = uint4{(unsigned)row, (unsigned)ks, 0u, (unsigned)mi};
                     else af[ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
@@ -779,7 +739,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
                 for (int ni = 0; ni < NFH; ++ni) {
                     const int row = wn * WTN + nh * (WTN / 2) + ni * 16 + fr;
-                    if constexpr (ABL == 3 || ABL == 8) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
+                    if constexpr (ABL == 3) bq[nh][ks][ni] = uint4{(unsigned)row, (unsigned)it, 1u, (unsigned)ni};
                     else bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
                 }
         };
@@ -801,105 +761,36 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                     }
             __builtin_amdgcn_s_setprio(0);
         };
-        if constexpr (PH == 4) {
-            // q0
-            read_a(0);
-            read_b(0);
-            if (ABL != 1 && it + 1 < iters) issue_b(bbuf ^ 1);
-            __builtin_amdgcn_s_barrier();
-            mma(0, 0);
-            __builtin_amdgcn_s_barrier();
-            // q1
-            read_b(1);
-            const bool hp = ABL != 1 && tap < h_n && kc + 1 < kc_end;
-            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
-            __builtin_amdgcn_s_barrier();
-            mma(0, 1);
-            __builtin_amdgcn_s_barrier();
-            // q2
-            read_a(1);
-            __builtin_amdgcn_s_barrier();
-            mma(1, 1);
-            __builtin_amdgcn_s_barrier();
-            // q3: slice it+1 (and every older DMA) must land before the next q0
-            if (hp) wait_vmcnt<1>();
-            else wait_vmcnt<0>();
-            __builtin_amdgcn_s_barrier();
-            mma(1, 0);
-            __builtin_amdgcn_s_barrier();
-        } else if constexpr (DB) {
-            // Deep filter ring: h0 moves the WHOLE slice it into registers, so
-            // its buffer is free once both groups' h0 reads have retired (the
-            // lagging group's at the barrier after its h0 MFMAs), and slice
-            // it+2 is issued into it in h1 -- five barrier intervals before
-            // the leading group's h0(it+2) reads it, instead of two.
-            //   leading group (wm 0): halo piece, barrier, slice it+2, MFMAs,
-            //     wait(all but slice it+2), barrier;
-            //   lagging group (wm 1): slice it+2, halo piece, wait(all but
-            //     those), barrier, MFMAs, barrier.
-            // Both waits retire slice it+1 before the barrier after which the
-            // leading group reads it (the leading group's h1 end = the lagging
-            // group's h1 pre-MFMA barrier).
-            read_a(0);
-            read_b(0);
-            read_b(1);
-            __builtin_amdgcn_s_barrier();
-            mma(0, 0);
-            mma(0, 1);
-            __builtin_amdgcn_s_barrier();
-            read_a(1);
-            const bool hp = ABL != 1 && ABL != 8 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
-            const bool bp = ABL != 1 && ABL != 8 && ABL != 5 && it + 2 < iters;
-            if (wm == 1 && bp) issue_b(bbuf);
-            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
-            if (wm == 1 && ABL != 6) {
-                if (bp) {
-                    if (hp) wait_vmcnt<B_INS + 1>();
-                    else wait_vmcnt<B_INS>();
-                } else {
-                    if (hp) wait_vmcnt<1>();
-                    else wait_vmcnt<0>();
-                }
-            }
-            __builtin_amdgcn_s_barrier();
-            if (wm == 0 && bp) issue_b(bbuf);
-            mma(1, 1);
-            mma(1, 0);
-            if (wm == 0 && ABL != 6) {
-                if (bp) wait_vmcnt<B_INS>();
-                else wait_vmcnt<0>();
-            }
-            __builtin_amdgcn_s_barrier();
-        } else {
-            // h0: A0 + whole B slice, 32 MFMAs
-            read_a(0);
-            read_b(0);
-            read_b(1);
-            if (ABL != 1 && ABL != 8 && ABL != 5 && it + 1 < iters) issue_b(bbuf ^ 1);
-            __builtin_amdgcn_s_barrier();
-            mma(0, 0);
-            mma(0, 1);
-            __builtin_amdgcn_s_barrier();
-            // h1: A1, halo piece; slice it+1 must land before the next h0.
-            // Staggered groups wait one barrier early (the lagging group reads
-            // after the leading group's next barrier): half an iteration for
-            // the slice to land; unstaggered, the wait closes the iteration.
-            read_a(1);
-            const bool hp = ABL != 1 && ABL != 8 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
-            if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
-            if constexpr (STAG && ABL != 6) {
+        read_a(0);
+        read_b(0);
+        read_b(1);
+        __builtin_amdgcn_s_barrier();
+        mma(0, 0);
+        mma(0, 1);
+        __builtin_amdgcn_s_barrier();
+        read_a(1);
+        const bool hp = ABL != 1 && ABL != 4 && tap < h_n && kc + 1 < kc_end;
+        const bool bp = ABL != 1 && ABL != 5 && it + 2 < iters;
+        if (wm == 1 && bp) issue_b(bbuf);
+        if (hp) load_halo(tap, kc + 1, hbuf ^ 1);
+        if (wm == 1) {
+            if (bp) {
+                if (hp) wait_vmcnt<B_INS + 1>();
+                else wait_vmcnt<B_INS>();
+            } else {
                 if (hp) wait_vmcnt<1>();
                 else wait_vmcnt<0>();
             }
-            __builtin_amdgcn_s_barrier();
-            mma(1, 1);
-            mma(1, 0);
-            if constexpr (!STAG) {
-                if (hp) wait_vmcnt<1>();
-                else wait_vmcnt<0>();
-            }
-            __builtin_amdgcn_s_barrier();
         }
+        __builtin_amdgcn_s_barrier();
+        if (wm == 0 && bp) issue_b(bbuf);
+        mma(1, 1);
+        mma(1, 0);
+        if (wm == 0) {
+            if (bp) wait_vmcnt<B_INS>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
         bbuf ^= 1;
         ++tap;
         if (++t_i == p.taps_w) {
@@ -912,9 +803,9 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             }
         }
     }
-    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
+    if (wm == 0) __builtin_amdgcn_s_barrier();
 
-    if (p.partial && !p.tile_cnt) {
+    if (p.partial) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -949,38 +840,6 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
     char* wbuf = smem + w * 64 * SROW;
-    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
-    // store them to its slab (agent-coherent 16-byte stores), count in; the last
-    // split to arrive sums the slabs in the row loop below (splitk_arrive)
-    const bool fold = p.partial != nullptr;
-    if (fold) {
-        const auto rs = splitk_rsrc(p.partial);
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh) {
-            lds_barrier();
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int ni = 0; ni < 2 * NFH; ++ni)
-                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                            acc[mh * 4 + mi][ni][r];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < 64 / RPP; ++k) {
-                const int rr = rsub + k * RPP;
-                const int ml = wm * 128 + mh * 64 + rr;
-                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-                if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
-                float v[8];
-                splitk_lds8(wbuf + rr * SROW + cch * 32, v);
-                splitk_put8(rs, ((blockIdx.z * (unsigned)p.M + (unsigned)((img * p.OH + oy) * p.OW + ox)) *
-                                 (unsigned)p.N + col0) * 4u, v);
-            }
-        }
-        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
-    }
     // ReluGrad mask rows: the first half's requested before its staging, the
     // second half's row by row as the first half's are consumed
     constexpr int NRR = 64 / RPP;
@@ -1000,7 +859,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
         lds_barrier();
-        if (!fold) {
+        {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -1031,9 +890,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
             const long pix = (long)oy * p.OW + ox;
             float v[8];
-            if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)(img * p.OH * p.OW + pix) * (unsigned)p.N + col0) * 4u,
-                                  (unsigned)p.M * p.N * 4u, (int)gridDim.z, v);
-            else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+            splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8];
             if (e.residual) {
                 const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
@@ -1788,78 +1645,29 @@ void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int 
     g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
     g.hwd = hp.geom[4]; g.hrows = hp.geom[5]; g.hy0 = hp.geom[6]; g.hx0 = hp.geom[7];
     g.nchunks = hp.geom[8]; g.kc_per_split = hp.geom[9];
-    if (dtype == SEG_F16) {   // half: the production schedules only
-        const dim3 grid((unsigned)hp.tiles, 1, gridz);
-        if (hp.bn == 256) {
-            if (g_halo_stagger && g_halo_deepb) {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16, true>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16, true>), grid, dim3(512), 0, s, p, g);
-            } else if (g_halo_stagger) {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
-            } else {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, false, 0, 2, 256, f16>), grid, dim3(512), 0, s, p, g);
-            }
-            return;
-        }
-        switch (hp.bw * 10 + hp.hi) {
-            case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-            case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-            case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-            case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-            case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-            default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        }
-        return;
-    }
-    if (hp.bn == 128 && hp.hi == 6 && g_halo_wide && g_halo2_n128) {
-        const dim3 grid((unsigned)hp.tiles, 1, gridz);
-        if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 128>), grid, dim3(512), 0, s, p, g);
-        else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 128>), grid, dim3(512), 0, s, p, g);
-        return;
-    }
     if (hp.bn == 256) {
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
-        if (g_nt2_ablate && hp.bw == 16) {   // diagnostics on the default two-phase schedule
-            if (g_nt2_ablate == 1) hipLaunchKernelGGL((conv_halo2<16, true, 1, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 2) hipLaunchKernelGGL((conv_halo2<16, true, 2, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 3) hipLaunchKernelGGL((conv_halo2<16, true, 3, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 4) hipLaunchKernelGGL((conv_halo2<16, true, 4, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 5) hipLaunchKernelGGL((conv_halo2<16, true, 5, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 6) hipLaunchKernelGGL((conv_halo2<16, true, 6, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 7) hipLaunchKernelGGL((conv_halo2<16, true, 7, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 8) hipLaunchKernelGGL((conv_halo2<16, true, 8, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 9) hipLaunchKernelGGL((conv_halo2<16, true, 9, 2>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 10) hipLaunchKernelGGL((conv_halo2<16, true, 10, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 11) hipLaunchKernelGGL((conv_halo2<16, true, 11, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
-            if (g_nt2_ablate == 12) hipLaunchKernelGGL((conv_halo2<16, true, 12, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
+        if (dtype == SEG_F16) {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, 0, f16>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32, 0, f16>), grid, dim3(512), 0, s, p, g);
             return;
         }
-        if (g_halo_phases == 2) {
-            if (g_halo_stagger && g_halo_deepb) {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2, 256, bf16, true>), grid, dim3(512), 0, s, p, g);
-            } else if (g_halo_stagger) {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true, 0, 2>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, true, 0, 2>), grid, dim3(512), 0, s, p, g);
-            } else {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false, 0, 2>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2<32, false, 0, 2>), grid, dim3(512), 0, s, p, g);
+        if (g_nt2_ablate && hp.bw == 16) {   // diagnostics
+            switch (g_nt2_ablate) {
+                case 1: hipLaunchKernelGGL((conv_halo2<16, 1>), grid, dim3(512), 0, s, p, g); return;
+                case 2: hipLaunchKernelGGL((conv_halo2<16, 2>), grid, dim3(512), 0, s, p, g); return;
+                case 3: hipLaunchKernelGGL((conv_halo2<16, 3>), grid, dim3(512), 0, s, p, g); return;
+                case 4: hipLaunchKernelGGL((conv_halo2<16, 4>), grid, dim3(512), 0, s, p, g); return;
+                case 5: hipLaunchKernelGGL((conv_halo2<16, 5>), grid, dim3(512), 0, s, p, g); return;
+                case 7: hipLaunchKernelGGL((conv_halo2<16, 7>), grid, dim3(512), 0, s, p, g); return;
+                case 9: hipLaunchKernelGGL((conv_halo2<16, 9>), grid, dim3(512), 0, s, p, g); return;
             }
-            return;
         }
-        if (g_halo_stagger) {
-            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, true>), grid, dim3(512), 0, s, p, g);
-            else hipLaunchKernelGGL((conv_halo2<32, true>), grid, dim3(512), 0, s, p, g);
-        } else {
-            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, false>), grid, dim3(512), 0, s, p, g);
-            else hipLaunchKernelGGL((conv_halo2<32, false>), grid, dim3(512), 0, s, p, g);
-        }
+        if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16>), grid, dim3(512), 0, s, p, g);
+        else hipLaunchKernelGGL((conv_halo2<32>), grid, dim3(512), 0, s, p, g);
         return;
     }
-    const int key = hp.bw * 10 + hp.hi;
-    switch (key) {
+    switch (hp.bw * 10 + hp.hi) {
         case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
         case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
         case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;

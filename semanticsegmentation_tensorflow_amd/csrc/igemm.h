@@ -83,10 +83,6 @@ struct NTParams {
     EpiParams epi;
     float* partial;
     int kt_per_split;
-    // split-K folded into the producer (conv_halo / conv_halo2 / igemm_nt3):
-    // per-tile arrival counters (gridDim.x of them, zero on entry, left zero);
-    // null = the separate splitk_reduce_nt pass sums the slabs
-    int* tile_cnt;
     // conv2d_transpose phase split: blockIdx.z = ph*st_w + pw
     int phase, st_h, st_w, pad_t, pad_l, Nimg;
     ProParams pro;
@@ -97,54 +93,7 @@ struct NTParams {
 // A element: x[img, a*ish + j*tsh + ioh, b*isw + i*tsw + iow, c]
 // B element: b[p*ldb + n]
 // Output   : out[tap*o_tap + c*o_c + n*o_n] for c < c_valid, n < n_valid.
-// Split-K reduction inside the producing kernel ("last arriving split"):
-// every split stages its fp32 tile through LDS and stores its slab rows with
-// 16-byte agent-coherent (sc1, written through the XCD's L2) buffer stores --
-// the 8 XCDs' L2s are not coherent with each other, and a device-scope fence
-// would write back a whole L2 per block --, waits for them to complete and
-// counts itself in on its tile's counter; the split that arrives last returns
-// true, sums the slabs in split order with agent-coherent loads (splitk_sum8:
-// the additions splitk_reduce_nt makes, so folded and separate reductions agree
-// bit for bit) and runs the epilogue.  No block ever waits for another, so
-// residency of the whole grid is not assumed.  Slab byte offsets are 32-bit
-// (the host folds only when splits * M * N * 4 < 2^31).
-// lds_flag: 4 bytes of LDS no wave reads or writes any more.
-typedef unsigned int splitk_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t splitk_rsrc(const float* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
-}
-constexpr int kSplitkSc1 = 16;    // cache policy: sc1 (agent coherence)
-__device__ __forceinline__ void splitk_put8(__amdgpu_buffer_rsrc_t rs, unsigned off, const float v[8]) {
-    const splitk_u4 a = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-    const splitk_u4 b = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
-    __builtin_amdgcn_raw_buffer_store_b128(a, rs, (int)off, 0, kSplitkSc1);
-    __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)(off + 16), 0, kSplitkSc1);
-}
-__device__ __forceinline__ bool splitk_arrive(int* cnt, int splits, int* lds_flag) {
-    __builtin_amdgcn_s_waitcnt(0);       // this lane's slab stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == splits - 1;
-        if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
-        *lds_flag = last;
-    }
-    __syncthreads();
-    return *reinterpret_cast<volatile int*>(lds_flag) != 0;
-}
-// 8 consecutive fp32 columns of one output row summed over the split slabs,
-// in split order from 0
-__device__ __forceinline__ void splitk_sum8(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned slab, int splits,
-                                            float v[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    for (int z = 0; z < splits; ++z) {
-        const splitk_u4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + z * slab), 0, kSplitkSc1);
-        const splitk_u4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + z * slab + 16), 0, kSplitkSc1);
-        v[0] += __uint_as_float(a.x); v[1] += __uint_as_float(a.y); v[2] += __uint_as_float(a.z); v[3] += __uint_as_float(a.w);
-        v[4] += __uint_as_float(b.x); v[5] += __uint_as_float(b.y); v[6] += __uint_as_float(b.z); v[7] += __uint_as_float(b.w);
-    }
-}
+// 8 consecutive fp32 values staged in LDS (the epilogues' row reads)
 __device__ __forceinline__ void splitk_lds8(const char* src, float v[8]) {
     const float4 lo = *reinterpret_cast<const float4*>(src);
     const float4 hi = *reinterpret_cast<const float4*>(src + 16);
@@ -152,12 +101,6 @@ __device__ __forceinline__ void splitk_lds8(const char* src, float v[8]) {
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
 }
 
-// Library-owned arrival counters (zeroed once per device; each launch leaves its
-// slice zero): n consecutive ints from a ring, so launches in flight on
-// different streams do not share counters.
-int* splitk_counters(long n);
-// fold the NT split-K reduction into the producer when its tail is short
-bool splitk_fold_ok(long tiles, int splits, long slab_bytes);
 
 struct TNParams {
     int M, N, P;
@@ -212,9 +155,8 @@ extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;
 extern int g_tn_nsplit;
-extern int g_splitk_fold;
 extern int g_nt_nsplit;     // igemm_nt3 head + igemm_nt2 tail for N = 256 k + <= 128
-extern int g_halo_duo;      // halo.hip: two-blocks-per-CU conv_halo_duo for N <= 128   // 1: NT split-K reduced inside the producer (splitk_arrive)
+extern int g_halo_duo;      // halo.hip: two-blocks-per-CU conv_halo_duo for N <= 128
 extern int g_tn_variant;
 extern int g_tn_fill;
 extern int g_tn_split_cap;
@@ -289,8 +231,6 @@ extern int g_tn3_adam_abl;
 extern int g_tn3_half;
 extern int g_nt3_fill;
 extern int g_tn3_stagger_us;
-extern int g_tn3_stag;
-extern int g_nt3_stag;
 bool tn3_ok(const TNParams& p, int dtype);
 inline bool tn3_applies(int M, int N, int dtype) {
     return g_tn3 && (dtype == SEG_BF16 || dtype == SEG_F16) && M >= 256 && N > 128;
@@ -307,9 +247,6 @@ struct HaloPlan {
 };
 extern int g_nt_halo;
 extern int g_halo_wide;
-extern int g_halo_stagger;
-extern int g_halo_deepb;
-extern int g_halo_phases;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
 void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype = SEG_BF16);
@@ -320,7 +257,6 @@ bool res16c_ok(const NTParams& p, int dtype);
 void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
 int res16c_grid(const NTParams& p, int cus);
 void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype);
-extern int g_halo2_n128;
 bool res64_ok(const NTParams& p, int dtype);
 void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 
@@ -340,7 +276,6 @@ struct WgradPlan {
 };
 extern int g_wgrad_halo;
 extern int g_wgrad_nt;
-extern int g_wgrad_la;
 extern int g_wgrad_abl;
 extern int g_wgrad_nbias;
 extern int g_wgrad_nt32;

@@ -673,45 +673,9 @@ static int num_cus() {
 
 int device_cus() { return num_cus(); }
 
-int* splitk_counters(long n) {
-    constexpr long CAP = 1L << 16;
-    static int* buf[64] = {};
-    static long ring[64] = {};
-    static std::mutex mu;
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64 || n > CAP) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!buf[dev]) {
-        int* b = nullptr;
-        if (hipMalloc(&b, CAP * sizeof(int)) != hipSuccess) return nullptr;
-        if (hipMemset(b, 0, CAP * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            (void)hipFree(b);
-            return nullptr;
-        }
-        buf[dev] = b;
-    }
-    if (ring[dev] + n > CAP) ring[dev] = 0;
-    int* r = buf[dev] + ring[dev];
-    ring[dev] += (n + 63) & ~63L;
-    return r;
-}
+int g_nt_nsplit = 1;    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
+int g_tn_nsplit = 1;    // TN: igemm_tn3 head + igemm_tn2 tail for N = 256 k + <= 128
 
-// In-kernel split-K reduction (last arriving split, see splitk_arrive) when
-// the tail it adds is short: <= 4 slabs per tile and enough tiles to spread
-// the tails over the CUs; otherwise the full-chip splitk_reduce_nt pass.
-// Off by default: measured slower on C2 (conv5_x 6 launches 577 vs 334 + 90
-// us of reducer; conv6 / conv7 igemm_nt3 1068 vs 894 + 80 us) -- the last
-// split's tail runs on one CU per tile (80-128 CUs) and the agent-coherent
-// slab traffic is written through the L2s, where the separate pass spreads
-// the same reads over the whole chip from L2/MALL.  A device-scope fence in
-// place of the sc1 stores was slower still (conv5_x 141 vs 52 + 20 us).
-int g_splitk_fold = 0;
-int g_nt_nsplit = 1;
-int g_tn_nsplit = 1;    // TN: igemm_tn3 head + igemm_tn2 tail for N = 256 k + <= 128    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
-bool splitk_fold_ok(long tiles, int splits, long slab_bytes) {
-    return g_splitk_fold && splits > 1 && splits <= 4 && tiles >= 32 && splits * slab_bytes < (1L << 31);
-}
 
 // Kernel generation for the NT GEMMs (1 = register-staged 128-row tiles,
 // 2 = LDS-DMA 3-stage ring, 256-row tiles).  Runtime-selectable for tests.
@@ -835,14 +799,9 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
             if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
         }
-        p.tile_cnt = p.partial && splitk_fold_ok(hp.tiles, hp.splits, (long)p.M * p.N * 4) ? splitk_counters(hp.tiles) : nullptr;
         launch_halo(p, hp, hp.splits, s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
-        const bool folded = p.tile_cnt != nullptr;
-        p.tile_cnt = nullptr;
-        if (p.partial && folded) {
-            p.partial = nullptr;
-        } else if (p.partial) {
+        if (p.partial) {
             const long total = (long)p.M * (p.N / 8);
             if (total >= (1L << 31)) return SEG_EINVAL;
             hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, hp.splits);
@@ -892,18 +851,12 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (nt3 && p.partial) {
-        const long tiles = (long)((max_m + 255) / 256) * ((p.N + 255) / 256);
-        p.tile_cnt = splitk_fold_ok(tiles, splits, (long)p.M * p.N * 4) ? splitk_counters(tiles) : nullptr;
-    }
-    const bool folded = p.tile_cnt != nullptr;
     if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
     else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
     else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
     SEG_CHECK_LAUNCH();
-    p.tile_cnt = nullptr;
-    if (p.partial && !folded) {
+    if (p.partial) {
         const long total = (long)p.M * (p.N / 8);
         if (total >= (1L << 31)) return SEG_EINVAL;
             hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
@@ -924,9 +877,8 @@ bool nt_pool_ok(const NTParams& p, int dtype) {
     int bm, bn, splits;
     choose_nt(p.M, p.N, p.K, 64, bm, bn, splits);
     HaloPlan hp;
-    if (!halo_plan(p, dtype, splits, num_cus(), &hp) || hp.splits != 1 || g_splitk_fold) return false;
+    if (!halo_plan(p, dtype, splits, num_cus(), &hp) || hp.splits != 1) return false;
     if (hp.bn == 256) return true;
-    if (hp.bn == 128 && hp.hi == 6 && g_halo_wide && g_halo2_n128) return false;   // conv_halo2<..., 128>
     // conv_halo_duo (launch_halo_bn's condition) with BW = 16 and BN = 128
     return hp.bn == 128 && hp.bw == 16 && g_halo_duo && hp.hi == 6 && (long)p.IH * p.IW * p.ldx < (1L << 31);
 }

@@ -8,7 +8,7 @@
 //  * each 64-deep K tile is two phases: h0 reads A rows 0..127 of the wave's
 //    half + the whole B slice and issues the LDS-DMA of B(t+1); h1 reads A
 //    rows 128..255 and issues A(t+2); each phase = 32 MFMAs between barriers;
-//  * the upper M wave group runs one barrier behind (STAG), so on every SIMD
+//  * the upper M wave group runs one barrier behind, so on every SIMD
 //    one wave's MFMA cluster overlaps the other wave's LDS reads;
 //  * LDS: A in a 3-stage ring (3 x 32 KiB), B in a 2-stage ring (2 x 32 KiB)
 //    = 160 KiB, one block per CU.  Every buffer is restaged >= 2 phases after
@@ -26,10 +26,9 @@
 namespace seg {
 
 int g_nt3 = 1;
-int g_nt3_stag = 1;     // wave-group stagger (0: unstaggered, DMA wait a full iteration after issue)
 __device__ uint4 g_nt3_zero[4];
 
-template <bool STAG, typename T = bf16>
+template <typename T = bf16>
 __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
     constexpr int NW = 8, BM = 256, BN = 256, BK = 64;
     constexpr int WTM = 128, WTN = 64, TN = WTN / 16;   // TM = 8 (two halves of 4)
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         }
     }
     lds_barrier();
-    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
 
     const int fr = lane & 15, fg = lane >> 4;
     int abuf = 0, bbuf = 0;
@@ -204,43 +203,6 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                         acc[mh * 4 + mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[mh * 4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
         };
-        if constexpr (!STAG) {
-            // unstaggered: one barrier per iteration (every DMA target was last
-            // read in an earlier iteration; slice t+1 waited for at the end)
-            read_a(0);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int ni = 0; ni < TN; ++ni) {
-                    const int row = wn * WTN + ni * 16 + fr;
-                    bq[ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
-                }
-            if (it + 1 < nk) issue_b(bbuf ^ 1);
-            if (it + 2 < nk) issue_a(abuf == 0 ? 2 : abuf - 1);
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < TN; ++ni)
-                        acc[mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[mi][ni]);
-            read_a(1);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < TN; ++ni)
-                        acc[4 + mi][ni] = mfma16x16x32<T>(af[ks][mi], bq[ks][ni], acc[4 + mi][ni]);
-            __builtin_amdgcn_s_setprio(0);
-            if (it + 2 < nk) wait_vmcnt<A_INS>();
-            else wait_vmcnt<0>();
-            lds_barrier();
-            abuf = abuf == 2 ? 0 : abuf + 1;
-            bbuf ^= 1;
-            continue;
-        }
         // h0: A half 0 + B slice; B(t+1) into the other B buffer (last read at h0(t-1))
         read_a(0);
 #pragma unroll
@@ -259,26 +221,19 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         read_a(1);
         const int anext = abuf == 0 ? 2 : abuf - 1;   // (abuf + 2) % 3
         if (it + 2 < nk) issue_a(anext);
-        // staggered: the wait precedes the barrier the lagging group passes
-        // before its next reads (half an iteration for B(t+1) to land);
-        // unstaggered: right before the iteration's last barrier
-        if constexpr (STAG) {
-            if (it + 2 < nk) wait_vmcnt<A_INS>();
-            else wait_vmcnt<0>();
-        }
+        // the wait precedes the barrier the lagging group passes before its
+        // next reads (half an iteration for B(t+1) to land)
+        if (it + 2 < nk) wait_vmcnt<A_INS>();
+        else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         mma(1);
-        if constexpr (!STAG) {
-            if (it + 2 < nk) wait_vmcnt<A_INS>();
-            else wait_vmcnt<0>();
-        }
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
         bbuf ^= 1;
     }
-    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
+    if (wm == 0) __builtin_amdgcn_s_barrier();
 
-    if (p.partial && !p.tile_cnt) {
+    if (p.partial) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -311,39 +266,10 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
     }
     char* wbuf = smem + w * 64 * SROW;
-    // split-K folded into this kernel: stage this split's fp32 rows through LDS,
-    // store them to its slab (agent-coherent 16-byte stores), count in; the last
-    // split to arrive sums the slabs in the row loop below (splitk_arrive)
-    const bool fold = p.partial != nullptr;
-    if (fold) {
-        const auto rs = splitk_rsrc(p.partial);
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh) {
-            lds_barrier();
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int ni = 0; ni < TN; ++ni)
-                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                            acc[mh * 4 + mi][ni][r];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll 2
-            for (int rr = rsub; rr < 64; rr += RPP) {
-                const int row = m0 + wm * WTM + mh * 64 + rr;
-                if (row >= M || col0 >= p.N) continue;
-                float v[8];
-                splitk_lds8(wbuf + rr * SROW + cch * 32, v);
-                splitk_put8(rs, ((blockIdx.z * (unsigned)M + (unsigned)row) * (unsigned)p.N + col0) * 4u, v);
-            }
-        }
-        if (!splitk_arrive(p.tile_cnt + blockIdx.x, gridDim.z, reinterpret_cast<int*>(smem))) return;
-    }
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
         lds_barrier();
-        if (!fold) {
+        {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -364,9 +290,7 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
             const int b = rem - a * Wa;
             const long pix = (long)(a * p.osh + ooh) * p.OW + (b * p.osw + oow);
             float v[8];
-            if (fold) splitk_sum8(splitk_rsrc(p.partial), ((unsigned)row * (unsigned)p.N + col0) * 4u,
-                                  (unsigned)M * p.N * 4u, (int)gridDim.z, v);
-            else splitk_lds8(wbuf + rr * SROW + cch * 32, v);
+            splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8], mk[8];
             if (e.mask) {
                 const T* mp = reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0;
@@ -414,8 +338,7 @@ bool nt3_ok(const NTParams& p, int dtype) {
 template <typename T>
 static void launch_nt3_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + 255) / 256) * ((p.N + 255) / 256);
-    if (g_nt3_stag) hipLaunchKernelGGL((igemm_nt3<true, T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((igemm_nt3<false, T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((igemm_nt3<T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
 }
 
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype) {
@@ -440,13 +363,11 @@ int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2
 int g_tn3_mfast = 0;       // tile order: M fastest when the B (dy) panel is the larger operand
 int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split
 int g_tn3_stagger_us = 40;  // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
-// Wave-group stagger in the main loop.  Off: the DMA wait for slice t+1 moves
-// from before h1 to the end of the iteration, a full iteration after its
-// issue instead of half of one.  The dy / x slices of a filter gradient miss
-// L2 far more often than a forward conv's filter slices, so here the longer
-// window beats the MFMA / LDS-read overlap (conv6 main loop 445 -> 307 us),
-// while conv_halo2 and igemm_nt3 stay staggered (measured slower without).
-int g_tn3_stag = 0;
+// Main loop unstaggered: the DMA wait for slice t+1 sits at the end of the
+// iteration, a full iteration after its issue.  The dy / x slices of a filter
+// gradient miss L2 far more often than a forward conv's filter slices, so the
+// longer window beats conv_halo2's wave-group stagger here (conv6 main loop
+// 445 -> 307 us measured with the staggered form, since removed).
 __device__ int g_tn3_cu_slots[4096];
 int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue
 
@@ -457,7 +378,7 @@ int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4
 // 128 / 32 is the half tile (4 waves, 64 KiB rings + 68 KiB epilogue staging)
 // that runs two blocks per CU, so one block's HBM-bound epilogue (the fused
 // Adam) overlaps the other block's MFMA main loop.
-template <bool STAG, int ABL = 0, bool MFAST = false, bool ADAM = false, int BN = 256, int BKP = 64, typename T = bf16>
+template <int ABL = 0, bool MFAST = false, bool ADAM = false, int BN = 256, int BKP = 64, typename T = bf16>
 __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, int tiles_n, int splits) {
     static_assert(!ADAM || is_bf16_v<T>, "the fused Adam epilogue writes bf16 weight copies");
     constexpr int BM = 256, WTM = 128, WTN = 64, TN = WTN / 16;
@@ -467,9 +388,9 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
     constexpr int A_INS = BKP / RPI / NW, B_INS = BKP / RPIB / NW;
     constexpr int KS = BKP / 32;
     constexpr int ABUF = BKP * ROWB, BBUF = BKP * ROWBB;
-    // B (dy) ring depth: 3 stages for the unstaggered half tile (B(t+2) issued
-    // at t, two iterations to land; its 32-deep iterations are short), else 2
-    constexpr int BST = (BN == 128 && !STAG) ? 3 : 2;
+    // B (dy) ring depth: 3 stages for the half tile (B(t+2) issued at t, two
+    // iterations to land; its 32-deep iterations are short), else 2
+    constexpr int BST = BN == 128 ? 3 : 2;
     constexpr int RING = 3 * ABUF + BST * BBUF;
     constexpr int EPI = ADAM ? NW * (32 * (WTN * 4 + 16) + WTN * (32 * 2 + 16)) : NW * 64 * (WTN * 4 + 16);
     constexpr int SMEM = RING > EPI ? RING : EPI;
@@ -614,7 +535,6 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         }
     }
     lds_barrier();
-    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
 
     const int fg = lane >> 4;
     const int tq = (lane & 15) >> 2, tpp = lane & 3;
@@ -664,7 +584,7 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
                         acc[mh * 4 + mi][ni] = mfma_v8<T>(af[ks][mi], bq[ks][ni], acc[mh * 4 + mi][ni]);
             __builtin_amdgcn_s_setprio(0);
         };
-        if constexpr (!STAG && ABL == 0) {
+        if constexpr (ABL == 0) {
             // Unstaggered: ONE barrier per iteration.  Every buffer a DMA of
             // this iteration writes was last read in an earlier iteration (the
             // previous end barrier retired those reads), and slice t+1 is
@@ -734,27 +654,18 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         const int anext = abuf == 0 ? 2 : abuf - 1;
         const bool more = ABL != 1 && it + 2 < nk;
         if (more) issue_a(anext);
-        // Staggered groups: a wave's DMA wait must precede a barrier that the
-        // OTHER group passes before reading the data, i.e. one barrier early,
-        // leaving slice it+1 half an iteration to land.  Unstaggered: the wait
-        // sits right before the iteration's last barrier (a full iteration).
-        if constexpr (STAG) {
-            if (more) wait_vmcnt<A_INS>();
-            else wait_vmcnt<0>();
-        }
+        // the wait sits right before the iteration's last barrier (a full
+        // iteration after the slice's issue)
         __builtin_amdgcn_s_barrier();
         if (ABL != 2) mma(1);
         else asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(af[0][0]), "v"(af[KS - 1][3]) : "memory");
-        if constexpr (!STAG) {
-            // newest: B(t+2) (3-stage B ring) and A(t+2); A(t+1), B(t+1) landed
-            if (more) wait_vmcnt<BST == 3 ? A_INS + B_INS : A_INS>();
-            else wait_vmcnt<0>();
-        }
+        // newest: B(t+2) (3-stage B ring) and A(t+2); A(t+1), B(t+1) landed
+        if (more) wait_vmcnt<BST == 3 ? A_INS + B_INS : A_INS>();
+        else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         abuf = abuf == 2 ? 0 : abuf + 1;
         bbuf = bbuf == BST - 1 ? 0 : bbuf + 1;
     }
-    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
     if (ABL == 3) {   // every accumulator feeds the (never taken) store: no MFMA is dead code
         float sum = 0.f;
 #pragma unroll
@@ -951,14 +862,12 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {
     if (dtype == SEG_F16) {   // half storage: plain filter gradients only (loss scaling keeps Adam separate)
         if (splits == 1 && (g_tn3_half & 2)) {
             const int tn = (p.N + 127) / 128;
-            if (g_tn3_stag) hipLaunchKernelGGL((igemm_tn3<true, 0, false, false, 128, 32, f16>), dim3(tm * tn), dim3(256), 0, s, p, tm, tn, 1);
-            else hipLaunchKernelGGL((igemm_tn3<false, 0, false, false, 128, 32, f16>), dim3(tm * tn), dim3(256), 0, s, p, tm, tn, 1);
+            hipLaunchKernelGGL((igemm_tn3<0, false, false, 128, 32, f16>), dim3(tm * tn), dim3(256), 0, s, p, tm, tn, 1);
             return;
         }
         const int tn = (p.N + 255) / 256;
-        const dim3 g(tm * tn * splits);
-        if (g_tn3_stag) hipLaunchKernelGGL((igemm_tn3<true, 0, false, false, 256, 64, f16>), g, dim3(512), 0, s, p, tm, tn, splits);
-        else hipLaunchKernelGGL((igemm_tn3<false, 0, false, false, 256, 64, f16>), g, dim3(512), 0, s, p, tm, tn, splits);
+        hipLaunchKernelGGL((igemm_tn3<0, false, false, 256, 64, f16>), dim3(tm * tn * splits), dim3(512), 0, s, p, tm,
+                           tn, splits);
         return;
     }
     const bool multi_round = (long)tm * ((p.N + 255) / 256) > device_cus();
@@ -977,18 +886,7 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {
         } else {
             p.adam.stagger = 0;
         }
-#define TN3H(MF, AD) hipLaunchKernelGGL((igemm_tn3<true, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
-#define TN3HU(MF, AD) hipLaunchKernelGGL((igemm_tn3<false, 0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
-        if (!g_tn3_stag) {
-            if (p.adam.p) {
-                if (mfast) TN3HU(true, true);
-                else TN3HU(false, true);
-            } else {
-                if (mfast) TN3HU(true, false);
-                else TN3HU(false, false);
-            }
-            return;
-        }
+#define TN3H(MF, AD) hipLaunchKernelGGL((igemm_tn3<0, MF, AD, 128, 32>), g, b, 0, s, p, tm, tn, 1)
         if (p.adam.p) {
             if (mfast) TN3H(true, true);
             else TN3H(false, true);
@@ -996,43 +894,25 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {
             if (mfast) TN3H(true, false);
             else TN3H(false, false);
         }
-#undef TN3HU
 #undef TN3H
         return;
     }
     const int tn = (p.N + 255) / 256;
     const dim3 g(tm * tn * splits), b(512);
     const bool mfast = g_tn3_mfast && tm > tn;
-#define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<true, A, MF>), g, b, 0, s, p, tm, tn, splits)
-#define TN3U(A, MF) hipLaunchKernelGGL((igemm_tn3<false, A, MF>), g, b, 0, s, p, tm, tn, splits)
-    if (!g_tn3_stag) {
-        switch (g_tn3_abl) {
-            case 1: TN3U(1, false); return;
-            case 2: TN3U(2, false); return;
-            case 3: TN3U(3, false); return;
-        }
-        if (p.adam.p) {
-            if (mfast) hipLaunchKernelGGL((igemm_tn3<false, 0, true, true>), g, b, 0, s, p, tm, tn, splits);
-            else hipLaunchKernelGGL((igemm_tn3<false, 0, false, true>), g, b, 0, s, p, tm, tn, splits);
-            return;
-        }
-        if (mfast) TN3U(0, true);
-        else TN3U(0, false);
-        return;
-    }
+#define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<A, MF>), g, b, 0, s, p, tm, tn, splits)
     switch (g_tn3_abl) {
         case 1: TN3(1, false); return;
         case 2: TN3(2, false); return;
         case 3: TN3(3, false); return;
     }
     if (p.adam.p) {
-        if (mfast) hipLaunchKernelGGL((igemm_tn3<true, 0, true, true>), g, b, 0, s, p, tm, tn, splits);
-        else hipLaunchKernelGGL((igemm_tn3<true, 0, false, true>), g, b, 0, s, p, tm, tn, splits);
+        if (mfast) hipLaunchKernelGGL((igemm_tn3<0, true, true>), g, b, 0, s, p, tm, tn, splits);
+        else hipLaunchKernelGGL((igemm_tn3<0, false, true>), g, b, 0, s, p, tm, tn, splits);
         return;
     }
     if (mfast) TN3(0, true);
     else TN3(0, false);
-#undef TN3U
 #undef TN3
 }
 

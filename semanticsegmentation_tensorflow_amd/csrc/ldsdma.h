@@ -15,24 +15,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                  : "memory");
 }
 
-// cache-policy variants of glds16: 1 = sc1 (agent scope: bypasses the CU's L1),
-// 2 = nt (non-temporal), 3 = sc0 sc1
-template <int POL>
-__device__ __forceinline__ void glds16p(const void* gsrc, unsigned lds_dst) {
-    unsigned keep;
-    if constexpr (POL == 1)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-    else if constexpr (POL == 2)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-    else if constexpr (POL == 3)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-    else
-        glds16(gsrc, lds_dst);
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

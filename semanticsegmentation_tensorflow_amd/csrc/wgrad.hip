@@ -32,7 +32,6 @@ static __device__ uint4 wg_zero_page[4];
 
 int g_wgrad_halo = 1;
 int g_wgrad_nt = 128;
-int g_wgrad_la = 3;   // 1: per-read index arithmetic, 2: flat 36-step pipeline (spills), 3: packed per-lane offsets
 int g_wgrad_abl = 0;
 int g_wgrad_nt32 = 1;     // 32-wide dy tiles for N <= 32
 int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
@@ -52,11 +51,11 @@ __device__ __forceinline__ int wg_swz(int row) {
 
 // NST LDS stages (tile t+NST-1 in flight while t is consumed); HI halo DMA
 // pieces per wave (8 rows each): 4 covers dilation 1, 5 dilation 2.
-// LA: A-fragment read-ahead distance in (substep, tap) steps (1 or 2).
 // ABL (diagnostic builds, garbage results): 1 no DMA in the loop, 2 no MFMA,
 // 3 no LDS fragment reads.
-template <int BW, int NT, int NST, int HI, int LA = 1, int ABL = 0, typename T = bf16>
+template <int NT, int NST, int HI, int ABL = 0, typename T = bf16>
 __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
+    constexpr int BW = 16;
     using V8 = vec8_t<T>;
     constexpr int NW = 8, BH = 128 / BW;
     constexpr int NF = NT / 32;               // n fragments per wave
@@ -157,34 +156,12 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) tapoff[r * 3 + s] = r * p.tsh * g.hwd + s * p.tsw;
 
-    // LA == 2: per-lane LDS byte offsets of every tap's A fragment (rows kk and
-    // kk + 4 of substep 0) and of every B fragment
-    unsigned a_lo[9], a_hi[9], b_lo[NF], b_hi[NF];
-    if constexpr (LA == 2) {
-        const int kk = 8 * fg + tq;
-        const int py = kk / BW, px = kk - (kk / BW) * BW;
-        const int achk = cf * 2 + (tpp >> 1);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            const int r1 = py * g.hwd + px + tapoff[t];
-            a_lo[t] = r1 * 128 + 16 * (achk ^ wg_swz<128>(r1)) + 8 * (tpp & 1);
-            a_hi[t] = (r1 + 4) * 128 + 16 * (achk ^ wg_swz<128>(r1 + 4)) + 8 * (tpp & 1);
-        }
-        const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
-#pragma unroll
-        for (int ni = 0; ni < NF; ++ni) {
-            const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
-            b_lo[ni] = kk * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d1)) + 8 * (tpp & 1);
-            b_hi[ni] = (kk + 4) * DROWB + 16 * ((chk & ~15) | ((chk & 15) ^ d2)) + 8 * (tpp & 1);
-        }
-    }
-    // LA == 3: the same per-lane offsets packed two per register (rows kk and
-    // kk + 4 as lo | hi << 16; BW = 16, hwd % 8 == 0 so substeps only add a
-    // wave-uniform base): one VALU op per fragment read instead of the
-    // index / swizzle arithmetic, at 13 VGPRs
+    // per-lane LDS byte offsets of every tap's A fragment and of every B
+    // fragment, packed two per register (rows kk and kk + 4 as lo | hi << 16;
+    // BW = 16, hwd % 8 == 0 so substeps only add a wave-uniform base): one
+    // VALU op per fragment read instead of the index / swizzle arithmetic
     unsigned a_pk[9], b_pk[NF];
-    if constexpr (LA == 3) {
-        static_assert(BW == 16, "packed offsets need 16-pixel tile rows");
+    {
         const int kk = 8 * fg + tq;
         const int py = kk / BW, px = kk - (kk / BW) * BW;
         const int achk = cf * 2 + (tpp >> 1);
@@ -227,8 +204,6 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
         else wait_vmcnt<12>();
         lds_barrier();
         if (ABL != 1 && t + NST - 1 < t_end) stage_tile(t + NST - 1, buf == 0 ? NST - 1 : buf - 1);
-        const char* Hs = smem + buf * STAGE;
-        const char* Ds = Hs + HBUF;
         // flat software pipeline over the 36 (substep, tap) steps of the tile:
         // the A fragment of step s+1 (and the B fragments of the next substep)
         // are read while the MFMAs of step s issue
@@ -241,21 +216,11 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 }
                 return;
             }
-            const int kk = ss * 32 + 8 * fg + tq;
-            const int d1 = wg_swz<DROWB>(kk), d2 = wg_swz<DROWB>(kk + 4);
 #pragma unroll
             for (int ni = 0; ni < NF; ++ni) {
-                s16x4 lo, hi;
-                if constexpr (LA == 3) {
-                    SEG_LDS char* dbs = (SEG_LDS char*)smem + buf * STAGE + HBUF + ss * 32 * DROWB;
-                    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] & 0xffffu)));
-                    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] >> 16)));
-                } else {
-                    const int chk = ((nh * (NT / 2) + ni * 16) >> 3) + (tpp >> 1);
-                    const int q1 = (chk & ~15) | ((chk & 15) ^ d1), q2 = (chk & ~15) | ((chk & 15) ^ d2);
-                    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + kk * DROWB + 16 * q1 + 8 * (tpp & 1)));
-                    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + (kk + 4) * DROWB + 16 * q2 + 8 * (tpp & 1)));
-                }
+                SEG_LDS char* dbs = (SEG_LDS char*)smem + buf * STAGE + HBUF + ss * 32 * DROWB;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] & 0xffffu)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(dbs + (b_pk[ni] >> 16)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 bo[ni] = __builtin_bit_cast(V8, v);
                 if (do_bias && ni == cf && ss % g.nbias == ct) {
@@ -266,76 +231,17 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             }
         };
         auto read_a = [&](int ss, int tap) {
-            if constexpr (LA == 3) {
-                SEG_LDS char* hb = (SEG_LDS char*)smem + buf * STAGE + ss * (32 / BW) * g.hwd * 128;
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] & 0xffffu)));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] >> 16)));
-                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                return __builtin_bit_cast(V8, v);
-            }
             if constexpr (ABL == 3) {
                 s16x8 v = {(short)ss, (short)tap, 1, 2, 3, 4, 5, (short)lane};
                 return __builtin_bit_cast(V8, v);
             }
-            const int kk = ss * 32 + 8 * fg + tq;
-            const int py = kk / BW, px = kk - (kk / BW) * BW;
-            const int r1 = py * g.hwd + px + tapoff[tap];
-            const int achk = cf * 2 + (tpp >> 1);
-            const int a1 = achk ^ wg_swz<128>(r1), a2 = achk ^ wg_swz<128>(r1 + 4);
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + r1 * 128 + 16 * a1 + 8 * (tpp & 1)));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + (r1 + 4) * 128 + 16 * a2 + 8 * (tpp & 1)));
+            SEG_LDS char* hb = (SEG_LDS char*)smem + buf * STAGE + ss * (32 / BW) * g.hwd * 128;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] & 0xffffu)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(hb + (a_pk[tap] >> 16)));
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             return __builtin_bit_cast(V8, v);
         };
         V8 b0[NF], b1[NF];
-        if constexpr (LA == 2) {
-            // flat 36-step pipeline (requires BW = 16 and hwd % 8 == 0, so a
-            // substep = +2 halo rows x hwd keeps every XOR swizzle): all LDS
-            // addresses are per-lane constants + immediates -- no VALU address
-            // math in the loop; A two steps ahead, next B at tap 4.
-            auto rd = [&](unsigned off) {
-                return __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Hs + off));
-            };
-            auto rdd = [&](unsigned off) {
-                return __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(Ds + off));
-            };
-            auto fa = [&](int k) {
-                const int ss = k / 9, tap = k - (k / 9) * 9;
-                const unsigned so = (unsigned)ss * (32 / BW) * g.hwd * 128;
-                const s16x4 lo = rd(a_lo[tap] + so), hi = rd(a_hi[tap] + so);
-                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                return __builtin_bit_cast(V8, v);
-            };
-            auto fb = [&](int ss, V8* bo) {
-#pragma unroll
-                for (int ni = 0; ni < NF; ++ni) {
-                    const s16x4 lo = rdd(b_lo[ni] + ss * 32 * DROWB), hi = rdd(b_hi[ni] + ss * 32 * DROWB);
-                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    bo[ni] = __builtin_bit_cast(V8, v);
-                    if (do_bias && ni == cf && ss % g.nbias == ct) {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e)
-                            dsum[ni] += bits16_to_f32<T>((unsigned short)v[e]);
-                    }
-                }
-            };
-            fb(0, b0);
-            V8 ar[3];
-            ar[0] = fa(0);
-            ar[1] = fa(1);
-#pragma unroll
-            for (int k = 0; k < 36; ++k) {
-                const int ss = k / 9, tap = k - (k / 9) * 9;
-                if (k + 2 < 36) ar[(k + 2) % 3] = fa(k + 2);
-                if (tap == 4 && ss + 1 < 4) fb(ss + 1, (ss & 1) ? b0 : b1);
-                V8* bc = (ss & 1) ? b1 : b0;
-#pragma unroll
-                for (int ni = 0; ni < NF; ++ni)
-                    acc[tap][ni] = mfma_v8<T>(ar[k % 3], bc[ni], acc[tap][ni]);
-            }
-            buf = buf == NST - 1 ? 0 : buf + 1;
-            continue;
-        }
         read_b(0, b0);
         V8 a_cur = read_a(0, 0);
         // one substep: 9 taps, A(tap+1) read ahead, next substep's B at tap 4
@@ -411,33 +317,23 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
 // ---------------------------------------------------------------------------
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     if (!g_wgrad_halo || (dtype != SEG_BF16 && dtype != SEG_F16)) return false;
-    if (dtype == SEG_F16 && g_wgrad_la != 3) return false;   // half: the production schedule only
     if (p.ish != 1 || p.isw != 1 || p.taps_w != 3 || p.Cg % 64 != 0 || p.M != 9 * p.Cg) return false;
     if (p.tsh <= 0 || p.tsw <= 0 || p.N % 8 != 0 || p.ldb % 8 != 0 || p.ldx % 8 != 0) return false;
     if (p.Ha <= 0 || p.Wa <= 0 || p.P % (p.Ha * p.Wa) != 0) return false;
     const int nimg = p.P / (p.Ha * p.Wa);
-    long best = -1;
-    for (int bw : {32, 16}) {
-        if (g_wgrad_la >= 2 && bw != 16) continue;
-        const int bh = 128 / bw;
-        int hwd = bw + 2 * p.tsw;
-        if (g_wgrad_la >= 2) hwd = (hwd + 7) & ~7;          // substep row shifts keep the swizzle
-        const int hrows = hwd * (bh + 2 * p.tsh);
-        if (hrows > 5 * 64) continue;
-        const int tx = (p.Wa + bw - 1) / bw, ty = (p.Ha + bh - 1) / bh;
-        const long cost = (long)tx * ty * (128 * 8 + hrows);
-        if (best < 0 || cost < best) {
-            best = cost;
-            wp->bw = bw;
-            wp->g[0] = tx; wp->g[1] = ty; wp->g[3] = hwd; wp->g[4] = hrows;
-        }
-    }
-    if (best < 0) return false;
+    // 16 x 8-pixel tiles (the packed per-lane fragment offsets need 16-pixel
+    // rows); halo rows padded to a multiple of 8 so substep shifts keep the swizzle
+    const int bw = 16, bh = 128 / bw;
+    const int hwd = (bw + 2 * p.tsw + 7) & ~7;
+    const int hrows = hwd * (bh + 2 * p.tsh);
+    if (hrows > 5 * 64) return false;
+    wp->bw = bw;
+    wp->g[0] = (p.Wa + bw - 1) / bw; wp->g[1] = (p.Ha + bh - 1) / bh; wp->g[3] = hwd; wp->g[4] = hrows;
     // 128-wide dy tiles (2 LDS stages, 4 halo pieces) when N allows and the halo fits
     wp->nt = (g_wgrad_nt == 128 && p.N > 64 && wp->g[4] <= 4 * 64) ? 128 : 64;
     // <= 32 output channels (FC-DenseNet growth convs, 64 -> 16): 32-wide dy
     // tiles instead of padding to 64 (half the MFMAs, a quarter of the dy LDS)
-    if (g_wgrad_nt32 && p.N <= 32 && g_wgrad_la == 3 && wp->bw == 16) wp->nt = 32;
+    if (g_wgrad_nt32 && p.N <= 32) wp->nt = 32;
     wp->g[2] = nimg;
     const int nct = p.Cg / 64, nnt = (p.N + wp->nt - 1) / wp->nt;
     const int nout = nct * nnt;
@@ -464,53 +360,25 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
     g.nbias = wp.nbias;
     const dim3 grid((unsigned)wp.blocks), block(512);
     const bool small = g.hrows <= 4 * 64;     // 4 halo pieces -> 3 stages fit
-    if (g_wgrad_abl && wp.nt == 128) {
-        if (wp.bw == 32) {
-            if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 1>), grid, block, 0, s, p, g);
-            if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 2>), grid, block, 0, s, p, g);
-            if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4, 1, 3>), grid, block, 0, s, p, g);
-        } else {
-            if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 1>), grid, block, 0, s, p, g);
-            if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 2>), grid, block, 0, s, p, g);
-            if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 1, 3>), grid, block, 0, s, p, g);
-        }
+    if (g_wgrad_abl && wp.nt == 128 && dtype == SEG_BF16) {   // diagnostics
+        if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 1>), grid, block, 0, s, p, g);
+        if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 2>), grid, block, 0, s, p, g);
+        if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 3>), grid, block, 0, s, p, g);
         return;
     }
-    if (g_wgrad_la == 2 && wp.nt == 128 && wp.bw == 16) {
-        hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 2>), grid, block, 0, s, p, g);
+    if (dtype == SEG_F16) {
+        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 0, f16>), grid, block, 0, s, p, g);
+        else if (wp.nt == 32 && small) hipLaunchKernelGGL((wgrad_halo<32, 3, 4, 0, f16>), grid, block, 0, s, p, g);
+        else if (wp.nt == 32) hipLaunchKernelGGL((wgrad_halo<32, 2, 5, 0, f16>), grid, block, 0, s, p, g);
+        else if (small) hipLaunchKernelGGL((wgrad_halo<64, 3, 4, 0, f16>), grid, block, 0, s, p, g);
+        else hipLaunchKernelGGL((wgrad_halo<64, 2, 5, 0, f16>), grid, block, 0, s, p, g);
         return;
     }
-    if (wp.nt == 32) {                        // wgrad_plan: la == 3, bw == 16
-        if (dtype == SEG_F16) {
-            if (small) hipLaunchKernelGGL((wgrad_halo<16, 32, 3, 4, 3, 0, f16>), grid, block, 0, s, p, g);
-            else hipLaunchKernelGGL((wgrad_halo<16, 32, 2, 5, 3, 0, f16>), grid, block, 0, s, p, g);
-        } else {
-            if (small) hipLaunchKernelGGL((wgrad_halo<16, 32, 3, 4, 3>), grid, block, 0, s, p, g);
-            else hipLaunchKernelGGL((wgrad_halo<16, 32, 2, 5, 3>), grid, block, 0, s, p, g);
-        }
-        return;
-    }
-    if (dtype == SEG_F16) {                   // wgrad_plan: la == 3, bw == 16
-        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 3, 0, f16>), grid, block, 0, s, p, g);
-        else if (small) hipLaunchKernelGGL((wgrad_halo<16, 64, 3, 4, 3, 0, f16>), grid, block, 0, s, p, g);
-        else hipLaunchKernelGGL((wgrad_halo<16, 64, 2, 5, 3, 0, f16>), grid, block, 0, s, p, g);
-        return;
-    }
-    if (g_wgrad_la == 3 && wp.bw == 16) {
-        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4, 3>), grid, block, 0, s, p, g);
-        else if (small) hipLaunchKernelGGL((wgrad_halo<16, 64, 3, 4, 3>), grid, block, 0, s, p, g);
-        else hipLaunchKernelGGL((wgrad_halo<16, 64, 2, 5, 3>), grid, block, 0, s, p, g);
-        return;
-    }
-    if (wp.bw == 32) {
-        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<32, 128, 2, 4>), grid, block, 0, s, p, g);
-        else if (small) hipLaunchKernelGGL((wgrad_halo<32, 64, 3, 4>), grid, block, 0, s, p, g);
-        else hipLaunchKernelGGL((wgrad_halo<32, 64, 2, 5>), grid, block, 0, s, p, g);
-    } else {
-        if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<16, 128, 2, 4>), grid, block, 0, s, p, g);
-        else if (small) hipLaunchKernelGGL((wgrad_halo<16, 64, 3, 4>), grid, block, 0, s, p, g);
-        else hipLaunchKernelGGL((wgrad_halo<16, 64, 2, 5>), grid, block, 0, s, p, g);
-    }
+    if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<128, 2, 4>), grid, block, 0, s, p, g);
+    else if (wp.nt == 32 && small) hipLaunchKernelGGL((wgrad_halo<32, 3, 4>), grid, block, 0, s, p, g);
+    else if (wp.nt == 32) hipLaunchKernelGGL((wgrad_halo<32, 2, 5>), grid, block, 0, s, p, g);
+    else if (small) hipLaunchKernelGGL((wgrad_halo<64, 3, 4>), grid, block, 0, s, p, g);
+    else hipLaunchKernelGGL((wgrad_halo<64, 2, 5>), grid, block, 0, s, p, g);
 }
 
 }  // namespace seg

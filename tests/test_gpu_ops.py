@@ -17,31 +17,24 @@ from tests.gpu_utils import assert_close, from_dev, rnd, to_dev
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8],
-                ids=["nt1", "nt2", "halo", "halo128", "halo-nostag", "halo-4ph", "halo2-n128", "nt3"])
+@pytest.fixture(params=[1, 2, 3, 4, 8], ids=["nt1", "nt2", "halo", "halo128", "nt3"])
 def ntv(request, dev):
     """Run NT tests on every kernel generation: 1 = register-staged GEMM,
     2 = LDS-DMA GEMM, 3 = 2 + the halo-tiled direct conv where it applies
-    (bf16, stride 1, C % 64 == 0; 256x256 four-phase tiles for N > 128),
-    4 = 3 restricted to the 256x128 halo tiles, 5 = 3 without the wave-group
-    stagger (two-phase schedule; igemm_nt3 too: DMA waits at the iteration
-    end), 6 = 3 with four phases per iteration, 7 = 3 with the two-phase kernel also for N <= 128 (off by default),
-    8 = 2 with the 256x256-tile GEMM (igemm_nt3) for every N > 128 problem
-    (by default only where its grid fills half the CUs; variant 2 keeps it
-    off so igemm_nt2 stays covered for wide N).  Variant 8 also
-    turns off the 2-stage short-K igemm_nt2 (K <= 128), so the 3-stage ring
-    stays covered for those problems.  N <= 128 halo problems without split-K
-    run the two-blocks-per-CU conv_halo_duo except in variants 4 and 6."""
+    (16-bit, stride 1, C % 64 == 0; 256x256 deep-ring tiles for N > 128),
+    4 = 3 restricted to the 256x128 halo tiles, 8 = 2 with the 256x256-tile
+    GEMM (igemm_nt3) for every N > 128 problem (by default only where its grid
+    fills half the CUs; variant 2 keeps it off so igemm_nt2 stays covered for
+    wide N).  Variant 8 also turns off the 2-stage short-K igemm_nt2 (K <= 128),
+    so the 3-stage ring stays covered for those problems.  N <= 128 halo
+    problems without split-K run the two-blocks-per-CU conv_halo_duo except in
+    variant 4 (the one-block conv_halo stays covered)."""
     v = request.param
     ops.set_option("igemm_nt_variant", 1 if v == 1 else 2)
-    ops.set_option("nt_halo", 1 if 3 <= v <= 7 else 0)
+    ops.set_option("nt_halo", 1 if v in (3, 4) else 0)
     ops.set_option("nt3", 0 if v == 2 else 1)
     ops.set_option("halo_wide", 0 if v == 4 else 1)
-    ops.set_option("halo_stagger", 0 if v == 5 else 1)
-    ops.set_option("nt3_stag", 0 if v == 5 else 1)
-    ops.set_option("halo_phases", 4 if v == 6 else 2)
-    ops.set_option("halo2_n128", 1 if v == 7 else 0)
-    ops.set_option("halo_duo", 0 if v in (4, 6) else 1)   # 4 / 6 keep the one-block conv_halo covered
+    ops.set_option("halo_duo", 0 if v == 4 else 1)
     ops.set_option("nt3_fill", 0 if v == 8 else 1)   # small test problems: force the 256x256 tiles
     ops.set_option("nt2_short", 0 if v == 8 else 8)
     yield v
@@ -51,10 +44,6 @@ def ntv(request, dev):
     ops.set_option("nt_halo", 1)
     ops.set_option("nt3", 1)
     ops.set_option("halo_wide", 1)
-    ops.set_option("halo_stagger", 1)
-    ops.set_option("nt3_stag", 1)
-    ops.set_option("halo_phases", 2)
-    ops.set_option("halo2_n128", 0)
     ops.set_option("halo_duo", 1)
 
 
@@ -167,31 +156,25 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
-                                                         "wgrad-nbias4", "tn3-half", "wgrad-la1", "tn3-stag"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                   "wgrad-nbias4", "tn3-half"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
-    where it applies (bf16, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy tiles,
-    5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off in 2 so
-    igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
-    BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5 with
-    the 256x128 two-blocks-per-CU tiles also for plain single-split launches,
-    8 = 4 with the per-fragment index arithmetic instead of packed per-lane
-    LDS offsets (wgrad_la 1 vs the default 3), 9 = 5 with the wave-group
-    staggered main loop (DMA wait one barrier early; off by default)."""
+    where it applies (16-bit, stride 1, C % 64 == 0), 4 = 3 with 128-wide dy
+    tiles, 5 = 2 with the 256x256-tile TN GEMM (igemm_tn3; on by default, off
+    in 2 so igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
+    BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5
+    with the 256x128 two-blocks-per-CU tiles also for plain single-split
+    launches."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
-    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6, 8) else 0)
-    ops.set_option("wgrad_la", 1 if v == 8 else 3)
-    ops.set_option("wgrad_nt", 128 if v in (4, 6, 8) else 64)
+    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6) else 0)
+    ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
     ops.set_option("tn3_half", 7 if v == 7 else 1)
-    ops.set_option("tn3_stag", 1 if v == 9 else 0)
     yield v
-    ops.set_option("tn3_stag", 0)
-    ops.set_option("wgrad_la", 3)
     ops.set_option("tn3_half", 1)
     ops.set_option("tn3", 1)
     ops.set_option("wgrad_nbias", 1)

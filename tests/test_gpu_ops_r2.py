@@ -251,79 +251,6 @@ def test_conv1x1_stream_bn_relu_dropout(dev, case, dtype, kp):
         assert bool((mask[(got == 0) & (ref.abs() > 1e-3)] == 0).all())
 
 
-# Split-K folded into the producer (last arriving split sums the slabs and runs
-# the epilogue) vs the separate splitk_reduce_nt pass: same additions in the
-# same order, so bit-identical; and both vs the float64 oracle.
-# (N, H, W, C, K, R, dropout keep) -- conv5_x of C2 on conv_halo2 (3 channel-chunk
-# splits, 80 tiles), a 1x1 conv7-like GEMM on igemm_nt3, conv_halo 128-wide.
-FOLD_CASES = [
-    (4, 24, 78, 512, 512, 3, 1.0),
-    (4, 24, 78, 512, 512, 3, 0.8),
-    (4, 12, 39, 1024, 1024, 1, 1.0),
-    (2, 24, 70, 512, 128, 3, 1.0),
-]
-
-
-@pytest.mark.parametrize("case", FOLD_CASES)
-@pytest.mark.parametrize("op", ["fwd", "bwd_data"])
-def test_splitk_fold_matches_reducer(dev, case, op):
-    N, H, W, C, K, R, kp = case
-    dtype = torch.bfloat16
-    g = torch.Generator().manual_seed(21)
-    if op == "bwd_data":
-        C, K = K, C          # dgrad: the conv maps K -> C; the GEMM's N is C
-    d = ops.conv_desc(N, H, W, C, K, R, R, 1, 1, "SAME", ops.BF16)
-    x64 = torch.randn(N, H, W, C, generator=g, dtype=torch.float64)
-    w64 = torch.randn(R, R, C, K, generator=g, dtype=torch.float64) / (R * R * C) ** 0.5
-    dy64 = torch.randn(N, H, W, K, generator=g, dtype=torch.float64)
-    mask64 = torch.relu(torch.randn(N, H, W, C, generator=g, dtype=torch.float64))
-    b = (torch.randn(K, generator=g) * 0.1).to(dev)
-    ws = ops.Workspace(dev)
-    outs = {}
-    for fold in (0, 1):
-        ops.set_option("splitk_fold", fold)
-        try:
-            if op == "fwd":
-                name, sp, _ = ops.conv_kernel_info(d, ops.OP_FWD)
-                wk = torch.empty(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, C), dtype=dtype, device=dev)
-                ops.pack_filter(w64.float().to(dev), wk, C, K, ops.PACK_KRSC)
-                y = torch.full((N, H, W, K), float("nan"), dtype=dtype, device=dev)
-                ops.conv2d_fwd(d, x64.to(dev, dtype), wk, y,
-                               ops.epilogue(bias=b, relu=True, keep_prob=kp, seed=7), ws)
-            else:
-                name, sp, _ = ops.conv_kernel_info(d, ops.OP_BWD_DATA)
-                wh = torch.empty(ops.packed_shape(R, R, C, K, ops.PACK_HWIO, C), dtype=dtype, device=dev)
-                ops.pack_filter(w64.float().to(dev), wh, C, K, ops.PACK_HWIO)
-                y = torch.full((N, H, W, C), float("nan"), dtype=dtype, device=dev)
-                mk = mask64.to(dev, dtype)
-                ops.conv2d_bwd_data(d, dy64.to(dev, dtype), wh, y, ws, epi=ops.epilogue(relu_mask=mk))
-            torch.cuda.synchronize()
-        finally:
-            ops.set_option("splitk_fold", 0)      # the library default (measured slower on C2)
-        assert sp > 1, (name, sp)
-        outs[fold] = y.clone()
-    assert torch.equal(outs[0], outs[1])
-    # oracle
-    xr = x64.to(dtype).double()
-    wr = w64.to(dtype).double()
-    if op == "fwd":
-        ref = T.conv2d(xr, wr, 1, "SAME", 1) + b.double().cpu()
-        ref = torch.relu(ref)
-        got = outs[1].double().cpu()
-        if kp < 1.0:      # dropout: compare where both kept
-            keep = got != 0
-            ref = torch.where(keep, ref / kp, torch.zeros_like(ref))
-    else:
-        dyr = dy64.to(dtype).double()
-        xa = torch.zeros(N, H, W, C, dtype=torch.float64, requires_grad=True)
-        (T.conv2d(xa, wr, 1, "SAME", 1) * dyr).sum().backward()
-        ref = xa.grad
-        ref = torch.where(mask64.to(dtype).double() > 0, ref, torch.zeros_like(ref))
-        got = outs[1].double().cpu()
-    err = (got - ref).abs().max().item() / ref.abs().max().item()
-    assert err < 1.2e-2, err
-
-
 # N = 256 k + a tail <= 128 on igemm_nt3 + igemm_nt2 (nt_nsplit): forward with
 # bias + ReLU, and the input gradient with the ReluGrad mask, vs the float64
 # oracle; the 256-aligned head is the same igemm_nt3 launch either way.

@@ -221,7 +221,7 @@ def test_dropout_before_folded_bn_keeps_its_own_gradient(dry):
 
 def test_pool_fusion_choice_at_c2_shapes():
     """(host) conv -> MaxPool fusion at the benchmarked 4 x 384 x 1248 FCN:
-    conv1_2 (conv_res64), conv2_2 (conv_halo_duo), conv3_3 / conv4_3
+    conv1_2 (conv_res64), conv2_2 (conv_halo_duo), conv3_3 / conv4_4
     (conv_halo2 256x256) carry the pooled epilogue; conv5_3 splits K (3 fp32
     slabs + a reducer) and keeps the separate pool; fp32 never fuses."""
     take = [(4, 384, 1248, 64, 64), (4, 192, 624, 128, 128), (4, 96, 312, 256, 256), (4, 48, 156, 512, 512)]
