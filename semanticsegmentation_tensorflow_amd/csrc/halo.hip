@@ -47,6 +47,11 @@ struct HaloGeom {
     int nchunks, kc_per_split;
 };
 
+// value of lane ^ 1 (DPP quad_perm [1, 0, 3, 2]: no LDS crossbar traffic)
+__device__ __forceinline__ float dpp_swap1(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
 // MaxPool 2x2 / stride 2 fused into the LDS-staged epilogue (TF's MaxPool after
 // conv_layer's bias + ReLU, Network/model/FCN.py:55-100 / :158-160): wbuf holds
 // this wave's HR staged fp32 rows [rr][SROW] (8 column chunks of 8), row rr =
@@ -1113,8 +1118,8 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                         unsigned code = 0;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            const float raw[4] = {acc[mi][ni][j], __shfl_xor(acc[mi][ni][j], 1),
-                                                  acc[mi + 2][ni][j], __shfl_xor(acc[mi + 2][ni][j], 1)};
+                            const float raw[4] = {acc[mi][ni][j], dpp_swap1(acc[mi][ni][j]),
+                                                  acc[mi + 2][ni][j], dpp_swap1(acc[mi + 2][ni][j])};
                             const bool cv = col0 + j < e.n_valid;
                             float q[4];
 #pragma unroll

@@ -27,7 +27,7 @@ LAYERS = {"conv1_1": (384, 1248, 3, 64, 3), "conv1_2": (384, 1248, 64, 64, 3),
           "conv4_1": (48, 156, 256, 512, 3), "conv4_2": (48, 156, 512, 512, 3),
           "conv5_1": (24, 78, 512, 512, 3), "conv6": (12, 39, 512, 4096, 7), "conv7": (12, 39, 4096, 4096, 1)}
 OPS = {"fwd": ops.OP_FWD, "dgrad": ops.OP_BWD_DATA, "wgrad": ops.OP_BWD_FILTER, "wgrad_adam": ops.OP_BWD_FILTER,
-       "fwdp": ops.OP_FWD, "dgradp": ops.OP_BWD_DATA}
+       "fwdp": ops.OP_FWD, "dgradp": ops.OP_BWD_DATA, "fwdpool": ops.OP_FWD, "fwd+pool": ops.OP_FWD}
 WPAD = 64   # fwdp / dgradp: packed filter rows padded by WPAD elements (diagnostic option "wpad")
 
 
@@ -56,6 +56,21 @@ def setup(spec, N, dev, ws):
         y = torch.empty(N, d.OH, d.OW, d.K, dtype=torch.bfloat16, device=dev)
         b = torch.zeros(K, device=dev)
         return d, op, padded(lambda: ops.conv2d_fwd(d, x, wk, y, ops.epilogue(bias=b, relu=True), ws))
+    if op in ("fwdpool", "fwd+pool"):        # Conv2D + bias + ReLU + MaxPool 2x2: fused vs the pair
+        wk = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, d.C), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wk, d.C, d.K, ops.PACK_KRSC)
+        y = torch.empty(N, d.OH, d.OW, d.K, dtype=torch.bfloat16, device=dev)
+        yp = torch.empty(N, d.OH // 2, d.OW // 2, d.K, dtype=torch.bfloat16, device=dev)
+        idx = torch.empty(N * (d.OH // 2) * (d.OW // 2) * d.K, dtype=torch.uint8, device=dev)
+        b = torch.zeros(K, device=dev)
+        epi = ops.epilogue(bias=b, relu=True)
+        if op == "fwdpool":
+            return d, op, lambda: ops.conv2d_fwd_pool(d, x, wk, yp, idx, epi, ws)
+
+        def pair():
+            ops.conv2d_fwd(d, x, wk, y, epi, ws)
+            ops.maxpool2x2_fwd_argmax(y, yp, idx)
+        return d, op, pair
     if op in ("dgrad", "dgradp"):
         wh = torch.zeros(ops.packed_shape(R, R, C, K + pad, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
         ops.pack_filter(w32, wh, d.C, d.K + pad, ops.PACK_HWIO)
