@@ -447,6 +447,12 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
 
     # ---- per-kernel timing (HIP events on the launch stream) for the roofline
     sess.timer = []
+    # a spin kernel first, so the host has queued the whole step before the GPU
+    # reaches it: the event pairs then bracket device time only (the timed
+    # step's per-launch event records slow the host; on a step of many small
+    # launches -- C3 -- the GPU would otherwise catch up and the host's gaps
+    # would land inside the spans)
+    torch.cuda._sleep(int(4e8))
     sess.run(train_step, feed_dict=feed)
     torch.cuda.synchronize()
     per = {}

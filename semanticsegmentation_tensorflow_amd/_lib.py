@@ -18,7 +18,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip", "wadam.hip"]
 HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]   # host-only C++ (g++), linked into the same library
 HOST_LIBS = ["-lz"]
 # per-source extra compiler flags

@@ -600,6 +600,26 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_tn3_mfast = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "wadam")) {      // warp-specialized fused filter gradient + Adam (conv6 / conv7)
+        if (value != 0 && value != 1) return SEG_EINVAL;
+        seg::g_wadam = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wadam_abl")) {   // diagnostic builds only: results are garbage
+        if (value < 0 || value > 4) return SEG_EINVAL;
+        seg::g_wadam_abl = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wadam_nst")) {
+        if (value != 4 && value != 6) return SEG_EINVAL;
+        seg::g_wadam_nst = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wadam_nt")) {
+        if (value < 0 || value > 2) return SEG_EINVAL;
+        seg::g_wadam_nt = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "tn3")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_tn3 = value;
@@ -990,7 +1010,8 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.abl = seg::g_tn3_adam_abl;
     p.Mp = p.M;
     p.partial = nullptr;
-    seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
+    if (seg::wadam_ok(p, SEG_BF16)) seg::launch_wadam(p, (hipStream_t)stream);
+    else seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
     SEG_CHECK_LAUNCH();
     if (tr_after) {
         const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;

@@ -136,6 +136,8 @@ struct TNParams {
         int stagger;           // half tiles: second block per CU starts this many 10 ns ticks late
         int first_round;       // blocks of the first dispatch round (2 per CU)
         int* cu_slots;         // per-CU arrival counters (zeroed per launch)
+        unsigned state_bytes;  // wadam.hip: extent of the p / m / v (and gradient) slices
+        unsigned rows_bytes;   // wadam.hip: extent of the bf16 rows copy
     } adam;
     ProParams pro;             // A = x operand prologue (igemm_tn only)
 };
@@ -238,6 +240,13 @@ inline bool tn3_applies(int M, int N, int dtype) {
 void tn3_info(int M, int N, int P, int cus, int* splits);
 void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype);
 bool tn3_adam_ok(const TNParams& p, int dtype);
+// warp-specialized filter gradient + TF1 Adam (wadam.hip) for the fused conv6 / conv7 launches
+extern int g_wadam;
+extern int g_wadam_nt;
+extern int g_wadam_abl;
+extern int g_wadam_nst;
+bool wadam_ok(const TNParams& p, int dtype);
+void launch_wadam(TNParams& p, hipStream_t s);
 
 // halo-tiled direct conv (halo.hip) for stride-1 NT problems
 struct HaloPlan {
