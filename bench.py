@@ -290,6 +290,8 @@ def kernel_symbol(name):
         return r"conv_halo2[<I]" if bn == "256" else r"conv_halo(_duo)?[<I]"
     if fam in ("igemm_nt3", "igemm_tn3"):
         return fam + "<"
+    if fam == "igemm_nt2_bn":   # the BatchNorm-backward instantiation (last template flag)
+        return rf"igemm_nt2I\w*Li{bm}ELi{bn}E\w*Lb0ELb1EEEv"
     if fam == "igemm_nt2":
         return rf"igemm_nt2I\w*Li{bm}ELi{bn}E"
     if fam == "igemm_tn2":
@@ -629,7 +631,7 @@ def main():
         try:
             argv = [a for a in sys.argv[1:] if a not in ("--kernel-table",)]
             argv = argv + ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-miou",
-                           "--no-pipeline", "--no-extra"]
+                           "--no-pipeline", "--no-extra", "--no-dp-probe", "--no-inference"]
             t = pmc_traffic(argv, kernel_symbol(dname), os.path.join(ROOT, "gpurun_out", "bench_pmc"))
             result["roofline"]["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
             result["roofline"]["traffic_detail"] = {
@@ -650,6 +652,22 @@ def main():
                 result[key] = extra_config(model, None, device, args.extra_steps, 3)
             except Exception as exc:  # report, never crash the headline line
                 result[key] = {"error": repr(exc)}
+                continue
+            if args.no_traffic:
+                continue
+            try:   # HBM traffic of that config's dominant kernel, same two PMC passes
+                roof = result[key]["roofline"]
+                sym = kernel_symbol(roof["kernel"])
+                argv = ["--model", model, "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
+                        "--no-miou", "--no-pipeline", "--no-extra", "--no-dp-probe", "--no-inference"]
+                t = pmc_traffic(argv, sym, os.path.join(ROOT, "gpurun_out", "bench_pmc_" + model))
+                roof["traffic"] = round(t["FETCH_SIZE"] + t["WRITE_SIZE"])
+                roof["traffic_detail"] = {
+                    "unit": "bytes per launch", "fetch_x2": round(t["FETCH_SIZE"]), "write": round(t["WRITE_SIZE"]),
+                    "symbol": sym, "launches": t["launches"],
+                    "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes; FETCH_SIZE doubled (gfx950)"}
+            except Exception as exc:
+                result[key]["roofline"]["traffic_error"] = repr(exc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(H, W, HP, WP, args.cpu_steps, args.model)

@@ -606,13 +606,18 @@ extern "C" int seg_set_option(const char* name, int value) {
         return SEG_OK;
     }
     if (!strcmp(name, "wadam_abl")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 4) return SEG_EINVAL;
+        if (value < 0 || value > 15) return SEG_EINVAL;
         seg::g_wadam_abl = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "wadam_nst")) {
-        if (value != 4 && value != 6) return SEG_EINVAL;
-        seg::g_wadam_nst = value;
+    if (!strcmp(name, "wadam_bk")) {
+        if (value != 32 && value != 64) return SEG_EINVAL;
+        seg::g_wadam_bk = value;
+        return SEG_OK;
+    }
+    if (!strcmp(name, "wadam_mw")) {
+        if (value != 4 && value != 8) return SEG_EINVAL;
+        seg::g_wadam_mw = value;
         return SEG_OK;
     }
     if (!strcmp(name, "wadam_nt")) {

@@ -244,7 +244,8 @@ bool tn3_adam_ok(const TNParams& p, int dtype);
 extern int g_wadam;
 extern int g_wadam_nt;
 extern int g_wadam_abl;
-extern int g_wadam_nst;
+extern int g_wadam_mw;
+extern int g_wadam_bk;
 bool wadam_ok(const TNParams& p, int dtype);
 void launch_wadam(TNParams& p, hipStream_t s);
 

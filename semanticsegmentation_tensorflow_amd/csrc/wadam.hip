@@ -29,13 +29,16 @@
 #include "igemm.h"
 #include "ldsdma.h"
 
+#include <type_traits>
+
 namespace seg {
 
 int g_wadam = 0;   // off until it beats igemm_tn3's fused form
 int g_wadam_nt = 0;   // p / m / v cache policy: 0 plain, 1 nt loads + stores, 2 sc1 stores (dropped from L2)
-int g_wadam_nst = 6;  // LDS ring stages (3..6)
-int g_wadam_abl = 0;  // diagnostics (garbage results): 1 update waves idle, 2 MFMA waves idle, 3 no operand DMA,
-                      // 4 update waves idle + every tile's operands from tile 0 (L2-hot)
+int g_wadam_mw = 4;   // MFMA waves per block: 4 (one per SIMD) or 8 (two)
+int g_wadam_bk = 32;  // pixel rows per stage: 32 (6-stage ring) or 64 (3 stages, 8 MFMA waves)
+int g_wadam_abl = 0;  // diagnostics (garbage results), bits: 1 update waves idle, 2 MFMA waves idle,
+                      // 4 no operand DMA, 8 every tile's operands from tile 0 (L2-hot)
 __device__ uint4 g_wadam_zero[4];
 
 __device__ __forceinline__ int wadam_swz(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
@@ -54,13 +57,19 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, 
 
 __device__ __forceinline__ void wa_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int NST, bool SG, int NTL, int ABL = 0>
-__global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, int tiles_n) {
+template <int NST, bool SG, int NTL, int ABL = 0, int MW = 4, int BKP = 32>
+__global__ __launch_bounds__(64 * (MW + 4)) void wgrad_adam_ws(TNParams p, int tiles_m, int tiles_n) {
     static_assert(NST >= 3 && NST <= 6, "ring depth");
-    constexpr int BM = 128, BN = 128, BKP = 32, ROWB = 256;
+    constexpr int BM = 128, BN = 128, ROWB = 256, KS = BKP / 32;
+    static_assert(BKP == 32 || BKP == 64, "pixel rows per stage");
     constexpr int ABUF = BKP * ROWB, STAGE = 2 * ABUF, RING = NST * STAGE;
     constexpr int SROW = BN * 4, STG = BM * SROW;   // rows aligned to the 256-B bank period
-    constexpr int PPW = 4;                          // DMA pieces per MFMA wave per stage (2 A + 2 B)
+    // MW MFMA waves: 4 as 2 x 2 of 64 x 64, or 8 as 2 x 4 of 64 x 32 (two per SIMD,
+    // so one wave's DMA issue and fragment waits overlap the other's MFMAs)
+    static_assert(MW == 4 || MW == 8, "MFMA waves");
+    constexpr int NPC = BKP / 4 / MW;               // DMA pieces per operand per MFMA wave per stage
+    constexpr int PPW = 2 * NPC;
+    constexpr int WTN = 128 / (MW / 2), NI = WTN / 16;
     __shared__ __attribute__((aligned(16))) char smem[RING + STG];
     typedef short s16x8 __attribute__((ext_vector_type(8)));
 
@@ -70,7 +79,7 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
     const int first = lo + jb;
     const int nt = first < hi ? (hi - first + nbx - 1) / nbx : 0;
     if (nt == 0) return;
-    auto tile_of = [&](int k, int& m0, int& n0) {
+    auto tile_of = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
         const int q = first + k * nbx;
         const int tn = q / tiles_m;
         m0 = (q - tn * tiles_m) * BM;
@@ -81,9 +90,9 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     char* stg = smem + RING;
 
-    if (w < 4) {
+    if (w < MW) {
         // ================= MFMA waves =================
-        const int wm = w >> 1, wn = w & 1;
+        const int wm = w / (MW / 2), wn = w % (MW / 2);
         const int nimg = p.P / (p.Ha * p.Wa);
         const __amdgpu_buffer_rsrc_t rx =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.x), (short)0, (int)(2 * nimg * p.x_img), 0x00020000);
@@ -98,9 +107,9 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
         const int hw = p.Ha * p.Wa;
         int hoff = 0, woff = 0, ac = 0, bn = 0;
         bool a_mok = false, b_nok = false;
-        int pimg[2], pa[2], pb[2], pp[2];
-        auto setup = [&](int m0, int n0) {
-            if (ABL == 4) m0 = n0 = 0;
+        int pimg[NPC], pa[NPC], pb[NPC], pp[NPC];
+        auto setup = [&](int m0, int n0) __attribute__((always_inline)) {
+            if (ABL & 8) m0 = n0 = 0;
             const int am = m0 + gc * 8;
             a_mok = am < p.M;
             const int atap = a_mok ? am / p.Cg : 0;
@@ -111,8 +120,8 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
             bn = n0 + gc * 8;
             b_nok = bn < p.N;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int pix = (i * 4 + w) * 4 + rsub;
+            for (int i = 0; i < NPC; ++i) {
+                const int pix = (i * MW + w) * 4 + rsub;
                 pp[i] = pix;
                 const int q = pix < p.P ? pix : 0;
                 pimg[i] = q / hw;
@@ -121,15 +130,16 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
                 pb[i] = rem - pa[i] * p.Wa;
             }
         };
-        auto issue = [&](int buf) {
+        auto issue = [&](int buf) __attribute__((always_inline)) {
+            buf = __builtin_amdgcn_readfirstlane(buf);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < NPC; ++i) {
                 const int ih = pa[i] * p.ish + hoff, iw = pb[i] * p.isw + woff;
                 const bool aok = a_mok && pp[i] < p.P && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
                 const unsigned aoffs = aok ? 2u * (unsigned)(pimg[i] * (int)p.x_img + (ih * p.IW + iw) * p.ldx + ac) : OOR;
-                blds16(rx, aoffs, lds0 + buf * STAGE + (i * 4 + w) * 1024);
+                blds16(rx, aoffs, lds0 + buf * STAGE + (i * MW + w) * 1024);
                 const bool bok = b_nok && pp[i] < p.P;
-                blds16(rdy, bok ? 2u * (unsigned)(pp[i] * p.ldb + bn) : OOR, lds0 + buf * STAGE + ABUF + (i * 4 + w) * 1024);
+                blds16(rdy, bok ? 2u * (unsigned)(pp[i] * p.ldb + bn) : OOR, lds0 + buf * STAGE + ABUF + (i * MW + w) * 1024);
                 pp[i] += BKP;
                 pb[i] += BKP;
                 while (pb[i] >= p.Wa) {
@@ -142,95 +152,100 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
         const int fg = lane >> 4, fr = lane & 15;
         const int tq = (lane & 15) >> 2, tpp = lane & 3;
         const int fr1 = 8 * fg + tq, fsw = wadam_swz(fr1);
-        auto lane_off = [&](int col0) {
+        auto lane_off = [&](int col0) __attribute__((always_inline)) {
             const int chk = (col0 >> 3) + (tpp >> 1);
             return (unsigned)(fr1 * ROWB + 16 * (chk ^ fsw) + 8 * (tpp & 1));
         };
-        unsigned aoff[4], boff[4];
+        unsigned aoff[4], boff[NI];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            aoff[i] = lane_off(wm * 64 + i * 16);
-            boff[i] = ABUF + lane_off(wn * 64 + i * 16);
-        }
-        auto frag = [&](SEG_LDS char* a) {
+        for (int i = 0; i < 4; ++i) aoff[i] = lane_off(wm * 64 + i * 16);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) boff[i] = ABUF + lane_off(wn * WTN + i * 16);
+        auto frag = [&](SEG_LDS char* a) __attribute__((always_inline)) {
             const s16x4 l4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)a);
             const s16x4 h4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(a + 4 * ROWB));
             s16x8 v = {l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
             return __builtin_bit_cast(bf16x8, v);
         };
 
-        f32x4 acc[4][4];
+        f32x4 acc[4][NI];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // Per stage: wait, barrier, fragment reads, the DMA of stage it+NST-1
+        // into the slot stage it-1 left (its reads retired at this barrier),
+        // MFMAs.  One barrier per stage, shared with the update waves.
+        auto wait_stages = [&](int y) __attribute__((always_inline)) {
+            if (NST >= 6 && y >= 4) wait_vmcnt<4 * PPW>();
+            else if (NST >= 5 && y >= 3) wait_vmcnt<3 * PPW>();
+            else if (NST >= 4 && y >= 2) wait_vmcnt<2 * PPW>();
+            else if (y >= 1) wait_vmcnt<PPW>();
+            else wait_vmcnt<0>();
+        };
         int m0, n0;
-        tile_of(0, m0, n0);
-        setup(m0, n0);
+        auto prologue = [&](int k) __attribute__((always_inline)) {   // stages 0 .. NST-2 of block tile k
+            tile_of(k, m0, n0);
+            setup(m0, n0);
 #pragma unroll
-        for (int s = 0; s < NST - 1; ++s)
-            if (ABL != 2 && ABL != 3 && s < nk) issue(s);
+            for (int s = 0; s < NST - 1; ++s)
+                if (!(ABL & 6) && s < nk) issue(s);
+        };
+        prologue(0);
         for (int k = 0; k < nt; ++k) {
-            int rbuf = 0, ibuf = NST - 1;   // ring slot read at `it`, written by the DMA issued at `it`
+            int rbuf = 0, ibuf = NST - 1;
 #pragma nounroll
             for (int it = 0; it < nk; ++it) {
-                // stage `it` landed: younger pieces = stages it+1 .. min(it+NST-2, nk-1)
-                const int y = min(NST - 2, nk - 1 - it);
-                if (NST >= 6 && y >= 4) wait_vmcnt<4 * PPW>();
-                else if (NST >= 5 && y >= 3) wait_vmcnt<3 * PPW>();
-                else if (NST >= 4 && y >= 2) wait_vmcnt<2 * PPW>();
-                else if (y >= 1) wait_vmcnt<PPW>();
-                else wait_vmcnt<0>();
-                wa_bar();   // every wave's pieces of stage it visible; stage it-1 reads retired
-                if (ABL == 2) continue;
-                // fragment reads first: the DMA issue below covers their latency
+                wait_stages(min(NST - 2, nk - 1 - it));   // stage it landed
+                wa_bar();   // stage it visible; stage it-1's reads retired; (it == 0) staging published
+                if (ABL & 2) continue;
                 SEG_LDS char* S = (SEG_LDS char*)smem + rbuf * STAGE;
-                bf16x8 af[4], bq[4];
+                bf16x8 af[KS][4], bq[KS][NI];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = frag(S + aoff[i]);
+                for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) bq[i] = frag(S + boff[i]);
-                if (ABL != 3 && it + NST - 1 < nk) issue(ibuf);
+                    for (int i = 0; i < 4; ++i) af[ks][i] = frag(S + ks * 32 * ROWB + aoff[i]);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) bq[ks][i] = frag(S + ks * 32 * ROWB + boff[i]);
+                }
+                if (!(ABL & 4) && it + NST - 1 < nk) issue(ibuf);
                 rbuf = rbuf == NST - 1 ? 0 : rbuf + 1;
                 ibuf = ibuf == NST - 1 ? 0 : ibuf + 1;
                 __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
+                for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-                    for (int ni = 0; ni < 4; ++ni)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bq[ni], acc[mi][ni], 0, 0, 0);
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < NI; ++ni)
+                            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][mi], bq[ks][ni], acc[mi][ni],
+                                                                                  0, 0, 0);
                 __builtin_amdgcn_s_setprio(0);
             }
             wa_bar();   // X: ring reads of tile k retired; the update waves are done with the staging
-            if (k + 1 < nt) {
-                tile_of(k + 1, m0, n0);
-                setup(m0, n0);
-#pragma unroll
-                for (int s = 0; s < NST - 1; ++s)
-                    if (ABL != 2 && ABL != 3 && s < nk) issue(s);
-            }
+            if (k + 1 < nt) prologue(k + 1);
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int ni = 0; ni < 4; ++ni)
+                    for (int ni = 0; ni < NI; ++ni)
                         *reinterpret_cast<float*>(stg + (wm * 64 + mi * 16 + fg * 4 + r) * SROW +
-                                                  (wn * 64 + ni * 16 + fr) * 4) = acc[mi][ni][r];
+                                                  (wn * WTN + ni * 16 + fr) * 4) = acc[mi][ni][r];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             // the next tile's first stage barrier publishes the staging
         }
-        // the update waves' last period: the same barrier count as a tile
+        // the update waves' last period: the nk stage barriers of a tile
         for (int it = 0; it < nk; ++it) wa_bar();
         return;
     }
 
     // ================= update waves =================
     const auto& A = p.adam;
-    const int u = w - 4, rr = lane >> 4, j = lane & 15;
+    const int u = w - MW, rr = lane >> 4, j = lane & 15;
     float pv[4][8], mv[4][8], vv[4][8];
     // Buffer-resource loads / stores (SGPR descriptor + one 32-bit byte offset
     // per slot, the second half an immediate +256 B): out-of-range lanes and
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
     const __amdgpu_buffer_rsrc_t rw =
         __builtin_amdgcn_make_buffer_rsrc(A.rows, (short)0, A.rows ? (int)A.rows_bytes : 0, 0x00020000);
     unsigned eb[4][2], rb[4][2];   // byte offsets per slot and half (OOR: skip)
-    auto load = [&](int slot, int k, int c, bool live) {
+    auto load = [&](int slot, int k, int c, bool live) __attribute__((always_inline)) {
         int m0, n0;
         tile_of(k, m0, n0);
         const int m = m0 + u * 32 + c * 4 + rr;
@@ -268,66 +283,60 @@ __global__ __launch_bounds__(512) void wgrad_adam_ws(TNParams p, int tiles_m, in
             *reinterpret_cast<f32x4*>(vv[slot] + 4 * h) = __builtin_amdgcn_raw_buffer_load_b128(rv, eb[slot][h], 0, CP);
         }
     };
-    // step c of the staged tile (block tile kprev); prefetch step c + 4
-    auto step = [&](int c, int kprev, bool more) {
+    // half h of step c of the staged tile (block tile kprev); after the second
+    // half, prefetch step c + 4.  Halves, spread over the stage barriers, keep
+    // each interval's Adam VALU within the issue slots the MFMA waves leave.
+    auto step = [&](int c, int h, int kprev, bool more) __attribute__((always_inline)) {
         const int slot = c & 3;
         const int row = u * 32 + c * 4 + rr;
-        float gg[8];
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(stg + row * SROW + (h * 64 + j * 4) * 4);
+        float np[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const f32x4 g4 = *reinterpret_cast<const f32x4*>(stg + row * SROW + (h * 64 + j * 4) * 4);
-            gg[4 * h] = g4[0]; gg[4 * h + 1] = g4[1]; gg[4 * h + 2] = g4[2]; gg[4 * h + 3] = g4[3];
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * h + e;
+            const float gc = g4[e] * A.gs;
+            const float mj = A.b1 * mv[slot][q] + (1.f - A.b1) * gc;
+            const float vj = A.b2 * vv[slot][q] + (1.f - A.b2) * gc * gc;
+            np[e] = pv[slot][q] - A.lr_t * mj / (sqrtf(vj) + A.eps);
+            mv[slot][q] = mj;
+            vv[slot][q] = vj;
         }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float np[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int q = 4 * h + e;
-                const float gc = gg[q] * A.gs;
-                const float mj = A.b1 * mv[slot][q] + (1.f - A.b1) * gc;
-                const float vj = A.b2 * vv[slot][q] + (1.f - A.b2) * gc * gc;
-                np[e] = pv[slot][q] - A.lr_t * mj / (sqrtf(vj) + A.eps);
-                mv[slot][q] = mj;
-                vv[slot][q] = vj;
-            }
-            const unsigned e0 = eb[slot][h];
-            __builtin_amdgcn_raw_buffer_store_b128(f32x4{np[0], np[1], np[2], np[3]}, rp, e0, 0, SP);
-            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4*>(mv[slot] + 4 * h), rm, e0, 0, SP);
-            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4*>(vv[slot] + 4 * h), rv, e0, 0, SP);
-            if constexpr (SG)
-                __builtin_amdgcn_raw_buffer_store_b128(f32x4{gg[4 * h], gg[4 * h + 1], gg[4 * h + 2], gg[4 * h + 3]}, rg,
-                                                       e0, 0, 0);
-            const bf16 b0 = (bf16)np[0], b1 = (bf16)np[1], b2 = (bf16)np[2], b3 = (bf16)np[3];
-            const unsigned lo2 = (uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
-            const unsigned hi2 = (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16);
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo2, hi2}, rw, rb[slot][h], 0, 0);
+        const unsigned e0 = eb[slot][h];
+        __builtin_amdgcn_raw_buffer_store_b128(f32x4{np[0], np[1], np[2], np[3]}, rp, e0, 0, SP);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4*>(mv[slot] + 4 * h), rm, e0, 0, SP);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4*>(vv[slot] + 4 * h), rv, e0, 0, SP);
+        if constexpr (SG) __builtin_amdgcn_raw_buffer_store_b128(g4, rg, e0, 0, 0);
+        const bf16 b0 = (bf16)np[0], b1 = (bf16)np[1], b2 = (bf16)np[2], b3 = (bf16)np[3];
+        const unsigned lo2 = (uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+        const unsigned hi2 = (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo2, hi2}, rw, rb[slot][h], 0, 0);
+        if (h == 1) {
+            if (c < 4) load(slot, kprev, c + 4, true);
+            else load(slot, more ? kprev + 1 : kprev, c - 4, more);
         }
-        if (c < 4) load(slot, kprev, c + 4, true);
-        else load(slot, more ? kprev + 1 : kprev, c - 4, more);
     };
 
     // period 0: the MFMA waves compute tile 0; prefetch its first four steps
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-        if (ABL != 1 && ABL != 4) load(c, 0, c, true);
+        if (!(ABL & 1)) load(c, 0, c, true);
     for (int it = 0; it < nk; ++it) wa_bar();
     for (int k = 1; k <= nt; ++k) {
         wa_bar();   // X
-        wa_bar();   // staging of tile k-1 published
+        wa_bar();   // stage barrier 0: staging of tile k-1 published
         const bool more = k < nt;
         // nk - 1 further stage barriers (the MFMA waves' tile k, or their idle
-        // tail after the last tile); step c runs before barrier 1 + c * nk / 8
+        // tail after the last tile); half-step q runs before barrier 1 + q * nk / 16
         int bar = 1;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int ic = 1 + (c * nk) / 8;
-            while (bar < ic) {
+        for (int q = 0; q < 16; ++q) {
+            const int iq = 1 + (q * nk) / 16;
+            while (bar < iq) {
                 wa_bar();
                 ++bar;
             }
-            if (ABL != 1 && ABL != 4) step(c, k - 1, more);
+            if (!(ABL & 1)) step(q >> 1, q & 1, k - 1, more);
         }
         while (bar < nk) {
             wa_bar();
@@ -358,25 +367,42 @@ void launch_wadam(TNParams& p, hipStream_t s) {
     const long taps = (p.M + p.Cg - 1) / p.Cg;
     p.adam.state_bytes = (unsigned)(4 * ((taps - 1) * p.o_tap + (long)(p.c_valid - 1) * p.o_c + p.n_valid));
     p.adam.rows_bytes = (unsigned)(2 * (((taps - 1) * p.adam.rows_ap + p.c_valid - 1) * (long)p.adam.rows_bp + p.n_valid));
-#define WADAM(NST, SG, NT, ABL) hipLaunchKernelGGL((wgrad_adam_ws<NST, SG, NT, ABL>), dim3(g), dim3(512), 0, s, p, tm, tn)
-    switch (g_wadam_abl) {
-        case 1: WADAM(6, false, 0, 1); return;
-        case 2: WADAM(6, false, 0, 2); return;
-        case 3: WADAM(6, false, 0, 3); return;
-        case 4: WADAM(6, false, 0, 4); return;
-    }
-    if (sg) {
-        WADAM(6, true, 0, 0);
+#define WADAM(NST, SG, NT, ABL, MW) \
+    hipLaunchKernelGGL((wgrad_adam_ws<NST, SG, NT, ABL, MW>), dim3(g), dim3(64 * (MW + 4)), 0, s, p, tm, tn)
+    if (g_wadam_bk == 64) {   // 64-pixel stages, 3-stage ring: half the barriers
+#define WADAM64(SG, ABL, MW) \
+    hipLaunchKernelGGL((wgrad_adam_ws<3, SG, 0, ABL, MW, 64>), dim3(g), dim3(64 * (MW + 4)), 0, s, p, tm, tn)
+        if (g_wadam_abl == 1) WADAM64(false, 1, 8);
+        else if (g_wadam_abl == 5) WADAM64(false, 5, 8);
+        else if (sg) WADAM64(true, 0, 8);
+        else WADAM64(false, 0, 8);
+#undef WADAM64
         return;
     }
-    if (g_wadam_nst == 4) {
-        WADAM(4, false, 0, 0);
+    if (g_wadam_mw == 8) {
+        switch (g_wadam_abl) {
+            case 1: WADAM(6, false, 0, 1, 8); return;
+            case 2: WADAM(6, false, 0, 2, 8); return;
+            case 5: WADAM(6, false, 0, 5, 8); return;
+            case 9: WADAM(6, false, 0, 9, 8); return;
+        }
+        if (sg) WADAM(6, true, 0, 0, 8);
+        else WADAM(6, false, 0, 0, 8);
+        return;
+    }
+    switch (g_wadam_abl) {
+        case 1: WADAM(6, false, 0, 1, 4); return;
+        case 2: WADAM(6, false, 0, 2, 4); return;
+        case 4: WADAM(6, false, 0, 4, 4); return;
+    }
+    if (sg) {
+        WADAM(6, true, 0, 0, 4);
         return;
     }
     switch (g_wadam_nt) {
-        case 1: WADAM(6, false, 1, 0); return;
-        case 2: WADAM(6, false, 2, 0); return;
-        default: WADAM(6, false, 0, 0); return;
+        case 1: WADAM(6, false, 1, 0, 4); return;
+        case 2: WADAM(6, false, 2, 0, 4); return;
+        default: WADAM(6, false, 0, 0, 4); return;
     }
 #undef WADAM
 }

@@ -667,18 +667,23 @@ ADAM_FUSED_CASES = [
 ]
 
 
-# (wadam, tn3_half, adam_tr_fused): the warp-specialized kernel (wadam.hip), and
+# (wadam, wadam MFMA waves, wadam stage rows, tn3_half, adam_tr_fused): the warp-specialized kernel (wadam.hip), and
 # igemm_tn3's fused epilogue on half / full tiles (the KRSC copy by the
 # transpose, or in the epilogue -- which always takes igemm_tn3)
-@pytest.fixture(params=[(1, 1, 0), (0, 5, 0), (0, 0, 0), (1, 0, 1)],
-                ids=["wadam", "half-tiles", "full-tiles", "full-tiles-tr-fused"])
+@pytest.fixture(params=[(1, 4, 32, 1, 0), (1, 8, 32, 1, 0), (1, 8, 64, 1, 0), (0, 4, 32, 5, 0), (0, 4, 32, 0, 0),
+                        (1, 4, 32, 0, 1)],
+                ids=["wadam4", "wadam8", "wadam8-bk64", "half-tiles", "full-tiles", "full-tiles-tr-fused"])
 def adam_tiles(request, dev):
-    wadam, half, trf = request.param
+    wadam, mw, bk, half, trf = request.param
     ops.set_option("wadam", wadam)
+    ops.set_option("wadam_mw", mw)
+    ops.set_option("wadam_bk", bk)
     ops.set_option("tn3_half", half)
     ops.set_option("adam_tr_fused", trf)
     yield request.param
     ops.set_option("wadam", 0)
+    ops.set_option("wadam_mw", 4)
+    ops.set_option("wadam_bk", 32)
     ops.set_option("tn3_half", 1)
     ops.set_option("adam_tr_fused", 0)
 
