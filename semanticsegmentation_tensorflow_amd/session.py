@@ -200,6 +200,9 @@ class Session:
         # conv (+bias +ReLU) -> 2x2 MaxPool as one launch (pooled epilogue)
         self.fuse_pool = os.environ.get("SEG_FUSE_POOL", "1") != "0"
         self._red = None                 # (side stream, compute stream) during a step
+        # deferred filter gradients: the kernel too (not only its reduction) on
+        # the side stream (1), and the fused filter-gradient + Adam launches (2)
+        self.side_wgrad = int(os.environ.get("SEG_SIDE_WGRAD", "2"))
         self._side = None
         self._adam_ctx = None
         self._ready_filter = None
@@ -1196,6 +1199,13 @@ class Session:
                 out[id(f)] = t[..., :C].float()
         return out
 
+    def _node_ws(self, p, n):
+        """The conv's own filter-gradient workspace (p.wg_ws) as an ops.Workspace,
+        for launches on the side stream (the shared one belongs to the compute stream)."""
+        w = ops.Workspace(self.device)
+        w.buf = p.wg_ws[id(n)]
+        return w
+
     def _timed(self, desc, op, fn, *args):
         if self.timer is None:
             return fn(*args)
@@ -1453,14 +1463,37 @@ class Session:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
-                    self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)], dz,
-                                store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
-                                opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
-                                store.packed.get((wn, ops.PACK_KRSC)),
-                                store.grad(wn) if self.store_fused_grads else None, fused_db, ws)
+                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 2) else None
+                    if side is not None:
+                        # on the side stream too: its input gradient (the only reader of the
+                        # packed copies it rewrites) is already enqueued on the compute stream
+                        ev = torch.cuda.Event()
+                        ev.record(self._red[1])
+                        side.wait_event(ev)
+                    with torch.cuda.stream(side if side is not None else torch.cuda.current_stream(self.device)):
+                        self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)], dz,
+                                    store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
+                                    opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
+                                    store.packed.get((wn, ops.PACK_KRSC)),
+                                    store.grad(wn) if self.store_fused_grads else None, fused_db,
+                                    self._node_ws(p, n) if side is not None else ws)
                     fdone.add(wn)
                     if self.capture is not None:
                         self.capture[-1]["fused_adam"] = True
+                elif self._red is not None and self.side_wgrad >= 1:
+                    # the whole filter gradient (kernel + split-K reduction) on the
+                    # side stream, beside the input-gradient chain: every operand
+                    # (x, dz, the per-node workspace) stays untouched until the
+                    # join before Adam
+                    side, main = self._red
+                    wsb = p.wg_ws[id(n)]
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    side.wait_event(ev)
+                    with torch.cuda.stream(side):
+                        tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc, buf[id(x)],
+                                          dz, gw, wsb, fused_db)
+                        ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db)
                 elif self._red is not None:
                     # kernel now, its split-K reduction on the side stream
                     side, main = self._red
