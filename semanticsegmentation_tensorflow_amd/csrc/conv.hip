@@ -635,6 +635,11 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_nt3 = value;
         return SEG_OK;
     }
+    if (!strcmp(name, "wgrad_fill")) {   // filter-gradient split-K: blocks as a percentage of the CUs
+        if (value < 1 || value > 800) return SEG_EINVAL;
+        seg::g_wgrad_fill = value;
+        return SEG_OK;
+    }
     if (!strcmp(name, "wgrad_nt32")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_wgrad_nt32 = value;

@@ -289,6 +289,7 @@ extern int g_wgrad_nt;
 extern int g_wgrad_abl;
 extern int g_wgrad_nbias;
 extern int g_wgrad_nt32;
+extern int g_wgrad_fill;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);
