@@ -59,7 +59,7 @@ class Saver:
         self._kept = []
 
     def _vars(self, sess):
-        store = sess._ensure_store(join=True)
+        store = sess._ensure_store()
         if self.var_list is None:
             return list(store.all_vars)
         return list(self.var_list)
@@ -72,7 +72,7 @@ class Saver:
         return int(global_step)
 
     def save(self, sess, save_path, global_step=None):
-        store = sess._ensure_store(join=True)
+        store = sess._ensure_store()
         gs = self._global_step_value(sess, global_step)
         path = save_path if gs is None else f"{save_path}-{gs}"
         out = {}
@@ -103,7 +103,7 @@ class Saver:
         return path
 
     def restore(self, sess, save_path):
-        store = sess._ensure_store(join=True)
+        store = sess._ensure_store()
         names = [v.var_name for v in self._vars(sess)]
         if tf_bundle.is_bundle(save_path):
             index = tf_bundle.read_index(save_path)

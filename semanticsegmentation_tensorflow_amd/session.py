@@ -204,14 +204,7 @@ class Session:
         # deferred filter gradients: the kernel too (not only its reduction) on
         # the side stream (1), and the fused filter-gradient + Adam launches (2)
         self.side_wgrad = int(os.environ.get("SEG_SIDE_WGRAD", "2"))
-        # the fused filter-gradient + Adam launches (FCN conv6 / conv7) issued at
-        # the end of the step on a stream of their own, from private copies of
-        # their operands, so they run beside the next step's forward up to the
-        # first conv that reads those weights (every other Session entry waits)
-        self.carry_fused = os.environ.get("SEG_CARRY_FUSED", "0") != "0"
-        self._carry = None               # (event, variable names, plan) of the update in flight
-        self._deferred = []
-        self._side2 = None
+
         self._side = None
         self._adam_ctx = None
         self._ready_filter = None
@@ -219,11 +212,8 @@ class Session:
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
 
     # ------------------------------------------------------------------ vars
-    def _ensure_store(self, join=False):
-        if join:
-            self._join_pending()
+    def _ensure_store(self):
         if self.store is None or len(self.store.all_vars) != len(self.graph.variables):
-            self._join_pending()
             old = self.store
             self.store = VariableStore(list(self.graph.variables.values()), self.device, self.seed)
             self.store.initialize()
@@ -234,10 +224,9 @@ class Session:
         return self.store
 
     def variable_value(self, name):
-        return self._ensure_store(join=True).read(name)
+        return self._ensure_store().read(name)
 
     def assign(self, name, value):
-        self._join_pending()
         self._ensure_store().assign(name, value)
 
     # ------------------------------------------------------------------- run
@@ -245,9 +234,6 @@ class Session:
         feed_dict = feed_dict or {}
         single = not isinstance(fetches, (list, tuple))
         flist = [fetches] if single else list(fetches)
-        if self._carry is not None and any(_is_op(f, "InitAll") or _is_op(f, "Assign") or _is_op(f, "ApplyGradients")
-                                           for f in flist):
-            self._join_pending()
         if any(_is_op(f, "InitAll") for f in flist):
             self._ensure_store().initialize()
         self._ensure_store()
@@ -268,11 +254,8 @@ class Session:
                    tuple(sorted((id(k), tuple(np.shape(v))) for k, v in feed_dict.items())))
             plan = self.plans.get(key)
             if plan is None:
-                self._join_pending()
                 plan = self._compile(rest, feed_dict)
                 self.plans[key] = plan
-            if self._carry is not None and plan is not self._carry[2]:
-                self._join_pending()
             out.update(self._execute(plan, feed_dict))
         for f in post:
             self._apply_accumulated(f)
@@ -940,7 +923,6 @@ class Session:
         store = self.store
         if self._packed_version == store.version:
             return
-        self._join_pending()
         for (name, mode), (t, ap, bp) in store.packed.items():
             ops.pack_filter(store.param(name), t, ap, bp, mode)
         self._packed_version = store.version
@@ -1040,8 +1022,6 @@ class Session:
             if k == "input":
                 continue
             y = buf[id(n.output)]
-            if self._carry is not None and k in ("conv", "tconv") and n.w.var_name in self._carry[1]:
-                self._join_pending()
             if k == "conv":
                 x = buf[id(n.inputs[0])]
                 kp = self._kp(n.kp, scal)
@@ -1201,8 +1181,6 @@ class Session:
                                       store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
                                       dtype=self._pack_dtype())
             self._fused = None
-            if self._deferred:
-                self._launch_deferred(p)
             if opt is not None:
                 store.version += 1
                 self._packed_version = store.version
@@ -1222,36 +1200,6 @@ class Session:
                 C = p.shapes[id(f)][3]
                 out[id(f)] = t[..., :C].float()
         return out
-
-    def _carry_copy(self, p, key, t):
-        """A private copy of t (the next step's forward rewrites the original)."""
-        c = p.tmp.get(key)
-        if c is None:
-            c = torch.empty_like(t)
-            p.tmp[key] = c
-        c.copy_(t)
-        return c
-
-    def _launch_deferred(self, p):
-        main = torch.cuda.current_stream(self.device)
-        if self._side2 is None:
-            self._side2 = torch.cuda.Stream(device=self.device)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        self._side2.wait_event(ev)
-        with torch.cuda.stream(self._side2):
-            for args, _ in self._deferred:
-                ops.conv2d_bwd_filter_adam(*args)
-        done = torch.cuda.Event()
-        done.record(self._side2)
-        self._carry = (done, {wn for _, wn in self._deferred}, p)
-        self._deferred = []
-
-    def _join_pending(self):
-        """Order the current stream after a carried-over update (see carry_fused)."""
-        if self._carry is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._carry[0])
-            self._carry = None
 
     def _node_ws(self, p, n):
         """The conv's own filter-gradient workspace (p.wg_ws) as an ops.Workspace,
@@ -1517,20 +1465,6 @@ class Session:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
-                    if self.carry_fused and self._red is not None and self.capture is None \
-                            and not self.store_fused_grads:
-                        if fused_db is not None:     # BiasAddGrad now: adam_pack updates the bias this step
-                            self._bias_relu_bwd(dz, None, dz, fused_db, n.desc.k_valid, False, 1.0)
-                        xc = self._carry_copy(p, ("carry_x", id(n)), buf[id(x)])
-                        dzc = self._carry_copy(p, ("carry_dz", id(n)), dz)
-                        self._deferred.append((
-                            (n.desc, xc, dzc, store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr,
-                             store.step, opt.beta1, opt.beta2, opt.epsilon, gs,
-                             store.packed.get((wn, ops.PACK_HWIO)), store.packed.get((wn, ops.PACK_KRSC)), None,
-                             None, self._node_ws(p, n)), wn))
-                        fdone.add(wn)
-                        self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
-                        continue
                     side = self._red[0] if (self._red is not None and self.side_wgrad >= 2) else None
                     if side is not None:
                         # on the side stream too: its input gradient (the only reader of the
@@ -1755,7 +1689,6 @@ class Session:
         ops.bias_relu_bwd(dy, y, dz, dbias, k_valid, relu, self.ws, scale=scale)
 
     def close(self):
-        self._join_pending()
         self.plans = {}
 
     def __enter__(self):
