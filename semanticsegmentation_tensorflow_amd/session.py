@@ -20,6 +20,7 @@ Compilation (per fetch set and fed shapes):
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 
@@ -898,8 +899,9 @@ class Session:
         for n in p.nodes:
             if n.kind == "conv" and ops.wgrad_adam_fusable(n.desc):
                 p.adam_fusable.add(id(n))
-            if n.kind == "conv":
-                p.wg_ws[id(n)] = torch.empty(max(256, ops.conv_workspace(n.desc, ops.OP_BWD_FILTER)),
+            if n.kind in ("conv", "tconv"):
+                op = ops.OP_BWD_FILTER if n.kind == "conv" else ops.OP_TBWD_FILTER
+                p.wg_ws[id(n)] = torch.empty(max(256, ops.conv_workspace(n.desc, op)),
                                              dtype=torch.uint8, device=self.device)
         p.var_names = [v.var_name for v in p.train.attrs["var_list"]]
         p.var_set = set(p.var_names)
@@ -1314,11 +1316,17 @@ class Session:
                 dB.zero_()
             return view, True
 
+        if not hasattr(p, "ncons"):
+            p.ncons = collections.Counter(id(i) for m in p.nodes
+                                          for i in list(m.inputs) + [getattr(m, "residual", None)] if i is not None)
+
         def contribute_alias(t, g):
             if id(t) not in ng:
                 return
             if id(t) not in grad:
-                grad[id(t)] = g
+                # share the buffer only when no later contribution will add into
+                # it (side-stream filter gradients may still be reading g)
+                grad[id(t)] = g if p.ncons[id(t)] <= 1 else g.clone()
             else:
                 ops.add(grad[id(t)], g, grad[id(t)])
 
@@ -1457,10 +1465,18 @@ class Session:
                 if not (want_w or want_b):
                     pass          # frozen layer (outside var_list): no filter gradient
                 elif getattr(n, "pro", None) is not None:
-                    # input relu(BN(x)) recomputed from x while staging (folded BatchNorm)
+                    # input relu(BN(x)) recomputed from x while staging (folded BatchNorm);
+                    # on the side stream beside the input-gradient chain, as below
                     b = n.pro
-                    self._timed(n.desc, ops.OP_BWD_FILTER_PRO, ops.conv2d_bwd_filter_pro, n.desc, buf[id(b.inputs[0])],
-                                self._prologue(b), dz, gw, ws, None, fused_db)
+                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 1) else None
+                    if side is not None:
+                        ev = torch.cuda.Event()
+                        ev.record(self._red[1])
+                        side.wait_event(ev)
+                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                        self._timed(n.desc, ops.OP_BWD_FILTER_PRO, ops.conv2d_bwd_filter_pro, n.desc,
+                                    buf[id(b.inputs[0])], self._prologue(b), dz, gw,
+                                    self._node_ws(p, n) if side is not None else ws, None, fused_db)
                 elif self._fused is not None and id(n) in p.adam_fusable and want_w:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
@@ -1524,9 +1540,17 @@ class Session:
                 want_w = n.w.var_name in p.var_set
                 want_b = n.bias is not None and n.bias.var_name in p.var_set
                 if want_w or want_b:
-                    self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
-                                store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w), ws, None,
-                                gdst(n.bias.var_name) if n.bias is not None else None)
+                    # on the side stream beside the input-gradient chain (as the conv filter gradients)
+                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 1) else None
+                    if side is not None:
+                        ev = torch.cuda.Event()
+                        ev.record(self._red[1])
+                        side.wait_event(ev)
+                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                        self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
+                                    store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w),
+                                    self._node_ws(p, n) if side is not None else ws, None,
+                                    gdst(n.bias.var_name) if n.bias is not None else None)
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
