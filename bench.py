@@ -28,7 +28,11 @@ import time
 # under data parallelism the side stream (filter gradients beside the
 # input-gradient chain) shared a queue with the compute stream and ran serially
 # (world-1 DP step 8.40 -> 7.69 ms with 8 queues; N=1 unchanged).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+try:
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+except ValueError:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
