@@ -610,21 +610,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         seg::g_wadam_abl = value;
         return SEG_OK;
     }
-    if (!strcmp(name, "wadam_bk")) {
-        if (value != 32 && value != 64) return SEG_EINVAL;
-        seg::g_wadam_bk = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wadam_mw")) {
-        if (value != 4 && value != 8) return SEG_EINVAL;
-        seg::g_wadam_mw = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wadam_nt")) {
-        if (value < 0 || value > 2) return SEG_EINVAL;
-        seg::g_wadam_nt = value;
-        return SEG_OK;
-    }
     if (!strcmp(name, "tn3")) {
         if (value != 0 && value != 1) return SEG_EINVAL;
         seg::g_tn3 = value;

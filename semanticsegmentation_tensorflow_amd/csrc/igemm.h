@@ -242,10 +242,7 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype);
 bool tn3_adam_ok(const TNParams& p, int dtype);
 // warp-specialized filter gradient + TF1 Adam (wadam.hip) for the fused conv6 / conv7 launches
 extern int g_wadam;
-extern int g_wadam_nt;
 extern int g_wadam_abl;
-extern int g_wadam_mw;
-extern int g_wadam_bk;
 bool wadam_ok(const TNParams& p, int dtype);
 void launch_wadam(TNParams& p, hipStream_t s);
 

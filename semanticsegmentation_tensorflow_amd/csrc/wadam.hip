@@ -7,15 +7,17 @@
 // 385 GFLOP.  igemm_tn3's fused epilogue runs that stream after each tile's
 // MFMA loop, so HBM idles during the loop and the MFMA pipes idle during the
 // update.  Here every block (one per CU, 8 waves) runs both at once:
-//  * waves 0-3 ("MFMA waves", 2 x 2 of 64 x 64) compute 128 x 128 gradient
-//    tiles from a 4-stage LDS-DMA ring (32-pixel stages of the gathered x
-//    columns and the dy columns, transposed ds_read_b64_tr_b16 fragment reads,
-//    one barrier per stage), then hand the fp32 tile to
-//  * waves 4-7 ("update waves") through a 64 KiB LDS staging tile: while the
-//    MFMA waves compute tile k+1, the update waves apply Adam to tile k, eight
-//    4-row x 128-column steps per wave spread over the stage barriers, with
-//    the p / m / v loads of the next four steps always in flight (two steps
-//    into the next tile at the end of a period).
+//  * waves 0-7 ("MFMA waves", 2 x 4 of 64 x 32, two per SIMD) compute 128 x
+//    128 gradient tiles from a 3-stage LDS ring of 64-pixel stages (the
+//    gathered x columns and the dy columns, buffer-resource LDS-DMA with
+//    32-bit offsets, transposed ds_read_b64_tr_b16 fragment reads, one barrier
+//    per stage), then hand the fp32 tile to
+//  * waves 8-11 ("update waves") through a 64 KiB LDS staging tile: while the
+//    MFMA waves compute tile k+1, the update waves apply Adam to tile k in
+//    sixteen half-steps (4 rows x 64 columns per wave) spread over the stage
+//    barriers, with the p / m / v loads of the next four steps in flight
+//    (branch-free buffer loads / stores: out-of-range lanes carry an offset
+//    past num_records).
 // Both roles pass every barrier (gfx950 has one workgroup barrier), so a
 // period lasts max(MFMA loop, update stream): the update stream, at ~28 B /
 // param, is what the kernel is sized to keep busy.
@@ -34,9 +36,6 @@
 namespace seg {
 
 int g_wadam = 0;   // off until it beats igemm_tn3's fused form
-int g_wadam_nt = 0;   // p / m / v cache policy: 0 plain, 1 nt loads + stores, 2 sc1 stores (dropped from L2)
-int g_wadam_mw = 4;   // MFMA waves per block: 4 (one per SIMD) or 8 (two)
-int g_wadam_bk = 32;  // pixel rows per stage: 32 (6-stage ring) or 64 (3 stages, 8 MFMA waves)
 int g_wadam_abl = 0;  // diagnostics (garbage results), bits: 1 update waves idle, 2 MFMA waves idle,
                       // 4 no operand DMA, 8 every tile's operands from tile 0 (L2-hot)
 __device__ uint4 g_wadam_zero[4];
@@ -57,16 +56,15 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, 
 
 __device__ __forceinline__ void wa_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int NST, bool SG, int NTL, int ABL = 0, int MW = 4, int BKP = 32>
-__global__ __launch_bounds__(64 * (MW + 4)) void wgrad_adam_ws(TNParams p, int tiles_m, int tiles_n) {
+template <int NST, bool SG, int ABL = 0>
+__global__ __launch_bounds__(768) void wgrad_adam_ws(TNParams p, int tiles_m, int tiles_n) {
     static_assert(NST >= 3 && NST <= 6, "ring depth");
+    constexpr int MW = 8, BKP = 64;   // MFMA waves (2 x 4 of 64 x 32), pixel rows per stage
     constexpr int BM = 128, BN = 128, ROWB = 256, KS = BKP / 32;
-    static_assert(BKP == 32 || BKP == 64, "pixel rows per stage");
     constexpr int ABUF = BKP * ROWB, STAGE = 2 * ABUF, RING = NST * STAGE;
     constexpr int SROW = BN * 4, STG = BM * SROW;   // rows aligned to the 256-B bank period
-    // MW MFMA waves: 4 as 2 x 2 of 64 x 64, or 8 as 2 x 4 of 64 x 32 (two per SIMD,
-    // so one wave's DMA issue and fragment waits overlap the other's MFMAs)
-    static_assert(MW == 4 || MW == 8, "MFMA waves");
+    // two MFMA waves per SIMD: one wave's DMA issue and fragment waits overlap
+    // the other's MFMAs
     constexpr int NPC = BKP / 4 / MW;               // DMA pieces per operand per MFMA wave per stage
     constexpr int PPW = 2 * NPC;
     constexpr int WTN = 128 / (MW / 2), NI = WTN / 16;
@@ -254,8 +252,7 @@ __global__ __launch_bounds__(64 * (MW + 4)) void wgrad_adam_ws(TNParams p, int t
     // instruction, and the compiler's vmcnt waits stay counted (a skipped load
     // or store on one path forces it to vmcnt(0)).
     constexpr unsigned OOR = 0x80000000u;
-    // cache policy bits of the p / m / v stream (gfx950: 2 = nt, 16 = sc1)
-    constexpr int CP = NTL == 1 ? 2 : 0, SP = NTL == 1 ? 2 : NTL == 2 ? 16 : 0;
+    constexpr int CP = 0, SP = 0;   // cache policy of the p / m / v stream (nt / sc1 measured no faster)
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(A.p, (short)0, (int)A.state_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(A.m, (short)0, (int)A.state_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(A.v, (short)0, (int)A.state_bytes, 0x00020000);
@@ -367,43 +364,18 @@ void launch_wadam(TNParams& p, hipStream_t s) {
     const long taps = (p.M + p.Cg - 1) / p.Cg;
     p.adam.state_bytes = (unsigned)(4 * ((taps - 1) * p.o_tap + (long)(p.c_valid - 1) * p.o_c + p.n_valid));
     p.adam.rows_bytes = (unsigned)(2 * (((taps - 1) * p.adam.rows_ap + p.c_valid - 1) * (long)p.adam.rows_bp + p.n_valid));
-#define WADAM(NST, SG, NT, ABL, MW) \
-    hipLaunchKernelGGL((wgrad_adam_ws<NST, SG, NT, ABL, MW>), dim3(g), dim3(64 * (MW + 4)), 0, s, p, tm, tn)
-    if (g_wadam_bk == 64) {   // 64-pixel stages, 3-stage ring: half the barriers
-#define WADAM64(SG, ABL, MW) \
-    hipLaunchKernelGGL((wgrad_adam_ws<3, SG, 0, ABL, MW, 64>), dim3(g), dim3(64 * (MW + 4)), 0, s, p, tm, tn)
-        if (g_wadam_abl == 1) WADAM64(false, 1, 8);
-        else if (g_wadam_abl == 5) WADAM64(false, 5, 8);
-        else if (sg) WADAM64(true, 0, 8);
-        else WADAM64(false, 0, 8);
-#undef WADAM64
-        return;
-    }
-    if (g_wadam_mw == 8) {
-        switch (g_wadam_abl) {
-            case 1: WADAM(6, false, 0, 1, 8); return;
-            case 2: WADAM(6, false, 0, 2, 8); return;
-            case 5: WADAM(6, false, 0, 5, 8); return;
-            case 9: WADAM(6, false, 0, 9, 8); return;
-        }
-        if (sg) WADAM(6, true, 0, 0, 8);
-        else WADAM(6, false, 0, 0, 8);
-        return;
-    }
+    // 8 MFMA waves (2 per SIMD), 64-pixel stages in a 3-stage ring: the best of
+    // the measured forms (4 waves, 32-pixel stages in a 6-stage ring: slower)
+#define WADAM(SG, ABL) \
+    hipLaunchKernelGGL((wgrad_adam_ws<3, SG, ABL>), dim3(g), dim3(64 * 12), 0, s, p, tm, tn)
     switch (g_wadam_abl) {
-        case 1: WADAM(6, false, 0, 1, 4); return;
-        case 2: WADAM(6, false, 0, 2, 4); return;
-        case 4: WADAM(6, false, 0, 4, 4); return;
+        case 1: WADAM(false, 1); return;
+        case 2: WADAM(false, 2); return;
+        case 5: WADAM(false, 5); return;
+        case 9: WADAM(false, 9); return;
     }
-    if (sg) {
-        WADAM(6, true, 0, 0, 4);
-        return;
-    }
-    switch (g_wadam_nt) {
-        case 1: WADAM(6, false, 1, 0, 4); return;
-        case 2: WADAM(6, false, 2, 0, 4); return;
-        default: WADAM(6, false, 0, 0, 4); return;
-    }
+    if (sg) WADAM(true, 0);
+    else WADAM(false, 0);
 #undef WADAM
 }
 
