@@ -205,6 +205,12 @@ class Session:
         # deferred filter gradients: the kernel too (not only its reduction) on
         # the side stream (1), and the fused filter-gradient + Adam launches (2)
         self.side_wgrad = int(os.environ.get("SEG_SIDE_WGRAD", "2"))
+        # the fused conv6 / conv7 filter-gradient + Adam launches go to the side
+        # stream after the next `fused_delay` filter gradients there (the
+        # HBM-bound update then overlaps the smaller conv4_x / conv3_x layers
+        # instead of starving conv5_x's input gradients: 547 -> 554 img/s at 5-7)
+        self.fused_delay = int(os.environ.get("SEG_FUSED_DELAY", "6"))
+        self._pending_fused = []
 
         self._side = None
         self._adam_ctx = None
@@ -1143,6 +1149,7 @@ class Session:
                 self._backward(p, scal)
             finally:
                 self._ready_filter = None
+            self._tick_fused(flush=True)
             if self._red is not None:            # pending filter-gradient reductions done before Adam
                 self._red[1].wait_stream(self._red[0])
                 self._red = None
@@ -1202,6 +1209,16 @@ class Session:
                 C = p.shapes[id(f)][3]
                 out[id(f)] = t[..., :C].float()
         return out
+
+    def _tick_fused(self, flush=False):
+        keep = []
+        for item in self._pending_fused:
+            item[0] -= 1
+            if flush or item[0] <= 0:
+                item[1]()
+            else:
+                keep.append(item)
+        self._pending_fused = keep
 
     def _node_ws(self, p, n):
         """The conv's own filter-gradient workspace (p.wg_ws) as an ops.Workspace,
@@ -1482,19 +1499,27 @@ class Session:
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
                     side = self._red[0] if (self._red is not None and self.side_wgrad >= 2) else None
-                    if side is not None:
-                        # on the side stream too: its input gradient (the only reader of the
-                        # packed copies it rewrites) is already enqueued on the compute stream
-                        ev = torch.cuda.Event()
-                        ev.record(self._red[1])
-                        side.wait_event(ev)
-                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
-                        self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)], dz,
-                                    store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
-                                    opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
-                                    store.packed.get((wn, ops.PACK_KRSC)),
-                                    store.grad(wn) if self.store_fused_grads else None, fused_db,
-                                    self._node_ws(p, n) if side is not None else ws)
+
+                    def launch_fused(n=n, x=x, dz=dz, wn=wn, fused_db=fused_db, side=side, opt=opt, gs=gs):
+                        if side is not None:
+                            # on the side stream too: its input gradient (the only reader of the
+                            # packed copies it rewrites) is already enqueued on the compute stream
+                            ev = torch.cuda.Event()
+                            ev.record(self._red[1])
+                            side.wait_event(ev)
+                        with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                            self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)],
+                                        dz, store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
+                                        opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
+                                        store.packed.get((wn, ops.PACK_KRSC)),
+                                        store.grad(wn) if self.store_fused_grads else None, fused_db,
+                                        self._node_ws(p, n) if side is not None else ws)
+                    if side is not None and self.fused_delay > 0:
+                        # issued after the next `fused_delay` side-stream filter gradients, so
+                        # the HBM-bound update does not starve the input-gradient chain early on
+                        self._pending_fused.append([self.fused_delay, launch_fused])
+                    else:
+                        launch_fused()
                     fdone.add(wn)
                     if self.capture is not None:
                         self.capture[-1]["fused_adam"] = True
@@ -1512,6 +1537,7 @@ class Session:
                         tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc, buf[id(x)],
                                           dz, gw, wsb, fused_db)
                         ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db)
+                    self._tick_fused()
                 elif self._red is not None:
                     # kernel now, its split-K reduction on the side stream
                     side, main = self._red
