@@ -1210,6 +1210,24 @@ class Session:
                 out[id(f)] = t[..., :C].float()
         return out
 
+    @contextlib.contextmanager
+    def _beside(self, side):
+        """Run the enclosed launches on `side` (the filter-gradient stream),
+        ordered after everything enqueued so far on the compute stream; a no-op
+        context when side is None (no side stream: CPU plans, disabled)."""
+        if side is None:
+            yield None
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._red[1])
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            yield side
+
+    def _wgrad_side(self, p, n, level=1):
+        """The side stream for node n's filter gradient, or None."""
+        return self._red[0] if (self._red is not None and self.side_wgrad >= level) else None
+
     def _tick_fused(self, flush=False):
         keep = []
         for item in self._pending_fused:
@@ -1485,12 +1503,8 @@ class Session:
                     # input relu(BN(x)) recomputed from x while staging (folded BatchNorm);
                     # on the side stream beside the input-gradient chain, as below
                     b = n.pro
-                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 1) else None
-                    if side is not None:
-                        ev = torch.cuda.Event()
-                        ev.record(self._red[1])
-                        side.wait_event(ev)
-                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                    side = self._wgrad_side(p, n)
+                    with self._beside(side):
                         self._timed(n.desc, ops.OP_BWD_FILTER_PRO, ops.conv2d_bwd_filter_pro, n.desc,
                                     buf[id(b.inputs[0])], self._prologue(b), dz, gw,
                                     self._node_ws(p, n) if side is not None else ws, None, fused_db)
@@ -1498,16 +1512,12 @@ class Session:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
-                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 2) else None
+                    side = self._wgrad_side(p, n, level=2)
 
                     def launch_fused(n=n, x=x, dz=dz, wn=wn, fused_db=fused_db, side=side, opt=opt, gs=gs):
-                        if side is not None:
-                            # on the side stream too: its input gradient (the only reader of the
-                            # packed copies it rewrites) is already enqueued on the compute stream
-                            ev = torch.cuda.Event()
-                            ev.record(self._red[1])
-                            side.wait_event(ev)
-                        with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                        # on the side stream too: its input gradient (the only reader of the
+                        # packed copies it rewrites) is already enqueued on the compute stream
+                        with self._beside(side):
                             self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_adam, n.desc, buf[id(x)],
                                         dz, store.param(wn), store.adam_m(wn), store.adam_v(wn), opt.lr, store.step,
                                         opt.beta1, opt.beta2, opt.epsilon, gs, store.packed.get((wn, ops.PACK_HWIO)),
@@ -1528,12 +1538,8 @@ class Session:
                     # side stream, beside the input-gradient chain: every operand
                     # (x, dz, the per-node workspace) stays untouched until the
                     # join before Adam
-                    side, main = self._red
                     wsb = p.wg_ws[id(n)]
-                    ev = torch.cuda.Event()
-                    ev.record(main)
-                    side.wait_event(ev)
-                    with torch.cuda.stream(side):
+                    with self._beside(self._red[0]):
                         tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc, buf[id(x)],
                                           dz, gw, wsb, fused_db)
                         ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db)
@@ -1567,12 +1573,8 @@ class Session:
                 want_b = n.bias is not None and n.bias.var_name in p.var_set
                 if want_w or want_b:
                     # on the side stream beside the input-gradient chain (as the conv filter gradients)
-                    side = self._red[0] if (self._red is not None and self.side_wgrad >= 1) else None
-                    if side is not None:
-                        ev = torch.cuda.Event()
-                        ev.record(self._red[1])
-                        side.wait_event(ev)
-                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                    side = self._wgrad_side(p, n)
+                    with self._beside(side):
                         self._timed(n.desc, ops.OP_TBWD_FILTER, ops.tconv2d_bwd_filter, n.desc, buf[id(x)], dy,
                                     store.grad(n.w.var_name) if want_w else self._scratch_grad(p, n.w),
                                     self._node_ws(p, n) if side is not None else ws, None,
