@@ -952,36 +952,49 @@ extern "C" int seg_conv_wgrad_adam_fusable(const seg_conv_desc* d) {
 }
 
 // KRSC copy from the HWIO copy the fused-Adam epilogue wrote: tr[n][rs][c] =
-// rows[rs][c][n] for c < C, n < K (padding untouched).  64 x 64 tiles staged
-// through LDS so both sides move 128-byte runs (the epilogue's own transposed
-// 16-byte stores, strided by RS * tr_ap, cost more than this pass).
+// rows[rs][c][n] for c < C, n < K (padding untouched).  One wave per 64 x 64
+// tile, no LDS: lane (cg, nc) loads the 8 x 8 block rows c0+8cg.., columns
+// n0+8nc.. as eight 16-byte row pieces (all eight in flight), transposes it in
+// registers (v_perm pairs) and stores eight 16-byte column pieces; for every
+// load / store instruction the wave touches eight full 128-byte runs.  (The
+// LDS-staged 64 x 64 block form moved 2.8 TB/s on conv6: two loads in flight
+// per lane and eight 2-byte LDS writes per chunk.)
 __global__ __launch_bounds__(256) void rows_to_tr_k(const bf16* __restrict__ rows, bf16* __restrict__ tr, int RS,
-                                                    int C, int K, int rows_ap, int rows_bp, int tr_ap, int ctiles) {
-    __shared__ bf16 t[64][64 + 8];
-    const int rs = blockIdx.y, c0 = (blockIdx.x % ctiles) * 64, n0 = (blockIdx.x / ctiles) * 64;
-    const int tid = threadIdx.x;
-    // load: 64 rows (c) x 64 n, 8 bf16 per thread-chunk: 512 chunks / 256 threads
+                                                    int C, int K, int rows_ap, int rows_bp, int tr_ap, int ctiles,
+                                                    int tiles) {
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= tiles) return;
+    const int rs = blockIdx.y;
+    const int c0 = (tile % ctiles) * 64 + (lane >> 3) * 8;
+    const int n0 = (tile / ctiles) * 64 + (lane & 7) * 8;
+    if (c0 >= C || n0 >= K) return;
+    uint4 v[8];
+    const bf16* src = rows + ((long)rs * rows_ap + c0) * rows_bp + n0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int q = tid + k * 256, cr = q >> 3, nc = (q & 7) * 8;
-        uint4 v = {0u, 0u, 0u, 0u};
-        if (c0 + cr < C && n0 + nc < rows_bp)
-            v = *reinterpret_cast<const uint4*>(rows + ((long)rs * rows_ap + c0 + cr) * rows_bp + n0 + nc);
-        const bf16* e = reinterpret_cast<const bf16*>(&v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[nc + j][cr] = e[j];
+    for (int i = 0; i < 8; ++i) {
+        v[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (c0 + i < C && n0 < rows_bp) v[i] = *reinterpret_cast<const uint4*>(src + (long)i * rows_bp);
     }
-    __syncthreads();
+    const unsigned* w = reinterpret_cast<const unsigned*>(v);   // w[4 * i + k]: row c0+i, columns n0+2k, +2k+1
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int q = tid + k * 256, nr = q >> 3, cc = (q & 7) * 8;
-        const int n = n0 + nr, c = c0 + cc;
-        if (n >= K || c >= C) continue;
-        bf16* dst = tr + ((long)n * RS + rs) * tr_ap + c;
-        if (c + 8 <= C) {
-            *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(&t[nr][cc]);
+    for (int j = 0; j < 8; ++j) {
+        const int n = n0 + j;
+        if (n >= K) break;
+        unsigned o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned a = w[4 * (2 * q) + j / 2], b = w[4 * (2 * q + 1) + j / 2];
+            o[q] = (j & 1) ? ((a >> 16) | (b & 0xffff0000u)) : ((a & 0xffffu) | (b << 16));
+        }
+        bf16* dst = tr + ((long)n * RS + rs) * tr_ap + c0;
+        if (c0 + 8 <= C) {
+            *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
-            for (int j = 0; j < 8 && c + j < C; ++j) dst[j] = t[nr][cc + j];
+            unsigned short* d16 = reinterpret_cast<unsigned short*>(dst);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (c0 + i < C) d16[i] = (unsigned short)(o[i >> 1] >> (16 * (i & 1)));
         }
     }
 }
@@ -1011,9 +1024,10 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     if (tr_after) {
         const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;
         const int ctiles = (C + 63) / 64, ntiles = (K + 63) / 64;
-        hipLaunchKernelGGL(rows_to_tr_k, dim3(ctiles * ntiles, RS), dim3(256), 0, (hipStream_t)stream,
+        const int tiles = ctiles * ntiles;
+        hipLaunchKernelGGL(rows_to_tr_k, dim3((tiles + 3) / 4, RS), dim3(256), 0, (hipStream_t)stream,
                            (const bf16*)a->rows_dst, (bf16*)a->tr_dst, RS, C, K, a->rows_ap, a->rows_bp, a->tr_ap,
-                           ctiles);
+                           ctiles, tiles);
         SEG_CHECK_LAUNCH();
     }
     if (!dbias) return SEG_OK;
