@@ -211,6 +211,11 @@ class Session:
         # instead of starving conv5_x's input gradients: 547 -> 554 img/s at 5-7)
         self.fused_delay = int(os.environ.get("SEG_FUSED_DELAY", "6"))
         self._pending_fused = []
+        # the filter gradients of the first `main_wgrad` convs (the last in the
+        # backward: conv1_1 / conv1_2 in FCN) stay on the compute stream, which
+        # has no input gradient left to run then, beside the side stream's
+        # remaining filter gradients instead of after them
+        self.main_wgrad = int(os.environ.get("SEG_MAIN_WGRAD", "2"))
 
         self._side = None
         self._adam_ctx = None
@@ -1365,6 +1370,12 @@ class Session:
             else:
                 ops.add(grad[id(t)], g, grad[id(t)])
 
+        main_wg = set()
+        if self._red is not None and self.main_wgrad > 0:
+            convs = [m for m in p.nodes if m.kind == "conv" and m.w.var_name in p.var_set
+                     and getattr(m, "pro", None) is None and id(m) not in p.adam_fusable]
+            main_wg = {id(m) for m in convs[:self.main_wgrad]}
+
         for n in reversed(p.nodes):
             k = n.kind
             if k == "input" or id(n.output) not in ng:
@@ -1533,7 +1544,7 @@ class Session:
                     fdone.add(wn)
                     if self.capture is not None:
                         self.capture[-1]["fused_adam"] = True
-                elif self._red is not None and self.side_wgrad >= 1:
+                elif self._red is not None and self.side_wgrad >= 1 and id(n) not in main_wg:
                     # the whole filter gradient (kernel + split-K reduction) on the
                     # side stream, beside the input-gradient chain: every operand
                     # (x, dz, the per-node workspace) stays untouched until the
@@ -1544,7 +1555,7 @@ class Session:
                                           dz, gw, wsb, fused_db)
                         ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db)
                     self._tick_fused()
-                elif self._red is not None:
+                elif self._red is not None and id(n) not in main_wg:
                     # kernel now, its split-K reduction on the side stream
                     side, main = self._red
                     wsb = p.wg_ws[id(n)]
