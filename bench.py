@@ -27,11 +27,11 @@ import time
 # is taken by torch's stream, RCCL's streams and the Session's side stream, so
 # under data parallelism the side stream (filter gradients beside the
 # input-gradient chain) shared a queue with the compute stream and ran serially
-# (world-1 DP step 8.40 -> 7.69 ms with 8 queues; N=1 unchanged).
-try:
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
-except ValueError:
+# (world-1 DP step 8.40 -> 7.69 ms with 8 queues; N=1 unchanged).  Unset or
+# HIP's default 4 (the GPU box exports 4) -> 8; any other value the user set is
+# kept.  The requested and effective values are recorded in the result line.
+_HWQ_USER = os.environ.get("GPU_MAX_HW_QUEUES")
+if _HWQ_USER is None or _HWQ_USER.strip() == "4":
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -659,6 +659,7 @@ def main():
         "conv_gflop_per_step_measured": round(m["conv_gflop_per_step"], 2),
         "loss_after": round(m["loss"], 5),
         "miou_parity": m.get("miou"),
+        "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "GPU_MAX_HW_QUEUES_requested": _HWQ_USER},
     }
     if "loss_scaling" in m:
         result["loss_scaling"] = m["loss_scaling"]

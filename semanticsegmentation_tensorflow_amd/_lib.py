@@ -18,7 +18,11 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip", "wadam.hip"]
+# diagnostic build (-DSEG_DIAG): the kernel-ablation modes of tools/ (no DMA / no
+# MFMA / no stores -- garbage results) exist only in this separate library;
+# SEG_DIAG_LIB=1 loads it instead of the product library
+DIAG_LIB_PATH = os.path.join(PKG_DIR, "build_diag", "libsegkern_diag.so")
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
 HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]   # host-only C++ (g++), linked into the same library
 HOST_LIBS = ["-lz"]
 # per-source extra compiler flags
@@ -37,22 +41,25 @@ def _newer(a, b):
     return os.path.exists(b) and os.path.getmtime(b) >= os.path.getmtime(a)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every HIP source for gfx950 and link libsegkern.so in-tree."""
-    os.makedirs(BUILD_DIR, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """Compile every HIP source for gfx950 and link libsegkern.so in-tree
+    (diag: the -DSEG_DIAG ablation library build_diag/libsegkern_diag.so)."""
+    build_dir = os.path.join(PKG_DIR, "build_diag") if diag else BUILD_DIR
+    lib_path = DIAG_LIB_PATH if diag else LIB_PATH
+    os.makedirs(build_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(REPO_DIR, "include", "segkern.h"))
     newest_header = max(os.path.getmtime(h) for h in headers)
 
     def compile_one(src):
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD_DIR, os.path.splitext(src)[0] + ".o")
+        o = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
         if (not force and _newer(s, o) and os.path.getmtime(o) >= newest_header):
             return o
         if src in HOST_SOURCES:
             cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o]
         else:
-            cmd = [HIPCC, *CFLAGS, *EXTRA_FLAGS.get(src, []), "-c", s, "-o", o]
+            cmd = [HIPCC, *CFLAGS, *EXTRA_FLAGS.get(src, []), *(["-DSEG_DIAG"] if diag else []), "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -62,13 +69,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES + HOST_SOURCES))
-    if force or not os.path.exists(LIB_PATH) or any(
-            os.path.getmtime(o) > os.path.getmtime(LIB_PATH) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs, *HOST_LIBS]
+    if force or not os.path.exists(lib_path) or any(
+            os.path.getmtime(o) > os.path.getmtime(lib_path) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, *HOST_LIBS]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise SegKernelError(f"link failed:\n{r.stderr}")
-    return LIB_PATH
+    return lib_path
 
 
 _LIB = None
@@ -217,7 +224,7 @@ def lib():
     if _LIB is None:
         with _LOCK:
             if _LIB is None:
-                _LIB = load()
+                _LIB = load(DIAG_LIB_PATH if os.environ.get("SEG_DIAG_LIB") == "1" else LIB_PATH)
                 # kernel-selection overrides for experiments: SEG_OPTIONS="nt3=0,tn3_mfast=1"
                 for kv in filter(None, os.environ.get("SEG_OPTIONS", "").split(",")):
                     k, v = kv.split("=")

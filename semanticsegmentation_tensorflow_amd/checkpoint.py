@@ -37,19 +37,33 @@ def _npz(path):
     return path if path.endswith(".npz") else path + ".npz"
 
 
-def _adam_step(d):
+def _adam_step(d, offset=1):
     """Adam t from TF's beta powers.  TF1's AdamOptimizer creates beta1_power =
     beta1 and multiplies it by beta1 after every update (_finish), so after t
-    updates it holds beta1^(t+1) (float32).  beta2_power = 0.999^(t+1) stays a
-    normal float32 up to t ~ 87k (0.9^(t+1) goes denormal past t ~ 830), so it
-    decides; beta1_power is the fallback.  No beta powers: step 0."""
+    updates it holds beta1^(t+1) (float32; `offset` 1, or 0 for the beta^t
+    convention of this package's legacy .npz checkpoints).  beta2_power =
+    0.999^(t+1) is a normal float32 up to t ~ 87k and a denormal (fewer
+    significant bits, still an estimate of t) up to t ~ 103k, so it decides
+    while it is > 0; beta1_power is the fallback.  Both 0 (a run longer than
+    ~103k steps, e.g. the reference's MAX_ITERATION = 100001 loops past their
+    end): float32 underflow, so the bias correction sqrt(1-b2^t)/(1-b1^t) is 1
+    to float32 precision -- `global_step` when the checkpoint holds one, else
+    the first step at which beta2^t underflows.  No beta powers: step 0."""
     b1 = float(d.get("beta1_power", BETA1))
     b2 = float(d.get("beta2_power", BETA2))
-    if 1e-30 < b2 < 1.0:
-        return max(0, int(round(math.log(b2) / math.log(BETA2))) - 1)
-    if 1e-30 < b1 < 1.0:
-        return max(0, int(round(math.log(b1) / math.log(BETA1))) - 1)
+    if 0.0 < b2 < 1.0:
+        return max(0, int(round(math.log(b2) / math.log(BETA2))) - offset)
+    if 0.0 < b1 < 1.0:
+        return max(0, int(round(math.log(b1) / math.log(BETA1))) - offset)
+    if b1 == 0.0 and b2 == 0.0:
+        if "global_step" in d and int(np.asarray(d["global_step"]).reshape(-1)[0]) > 0:
+            return int(np.asarray(d["global_step"]).reshape(-1)[0])
+        return _UNDERFLOW_STEP
     raise ValueError(f"checkpoint beta powers ({b1!r}, {b2!r}) do not encode an Adam step")
+
+
+# first t with float32(0.999^t) == 0 (below half the smallest denormal, 2^-150)
+_UNDERFLOW_STEP = int(math.ceil(-150 * math.log(2) / math.log(BETA2)))
 
 
 class Saver:
@@ -125,7 +139,9 @@ class Saver:
                 raise ValueError(f"{n}: checkpoint shape {np.shape(d[n])} != variable shape {want}")
         # int64 values (global_step) keep their integer width
         d = {k: (v if np.asarray(v).dtype.kind in "iu" else np.asarray(v, np.float32)) for k, v in d.items()}
-        d["beta_step"] = _adam_step(d) if ("beta1_power" in d or "beta2_power" in d) else store.step
+        legacy = not tf_bundle.is_bundle(save_path)      # .npz of earlier versions: beta^t
+        d["beta_step"] = (_adam_step(d, offset=0 if legacy else 1)
+                          if ("beta1_power" in d or "beta2_power" in d) else store.step)
         store.load_state_dict(d)
 
 

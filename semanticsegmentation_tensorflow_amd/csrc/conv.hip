@@ -502,192 +502,74 @@ int g_adam_tr_fused = 0;   // 1: the fused epilogue also writes the KRSC copy (t
 
 extern int g_adam_blocks;   // optim.hip
 
+// Kernel-selection knobs (A/B runs and the variant parity tests): every value
+// an entry accepts selects a parity-tested kernel or schedule.  The ablation
+// modes behind kernel diagnostics (no DMA / no MFMA / no stores: garbage
+// results) exist only in the diagnostic build (-DSEG_DIAG, _lib.build(diag=True)
+// -> libsegkern_diag.so), never in libsegkern.so.
+namespace {
+struct Knob {
+    const char* name;
+    int* var;
+    int lo, hi;        // accepted range ...
+    int step;          // ... in multiples of step (0: any listed in `only`)
+    int only[8];
+};
+}  // namespace
+
 extern "C" int seg_set_option(const char* name, int value) {
     if (!name) return SEG_EINVAL;
-    if (!strcmp(name, "igemm_nt_variant")) {
-        if (value != 1 && value != 2) return SEG_EINVAL;
-        seg::g_nt_variant = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn_nsplit")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_tn_nsplit = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt_nsplit")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt_nsplit = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "halo_duo")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_halo_duo = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt_halo")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt_halo = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_abl")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 3) return SEG_EINVAL;
-        seg::g_tn3_abl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "adam_tr_fused")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        g_adam_tr_fused = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt2_short")) {   // max k tiles (64 deep) of the 2-stage igemm_nt2; 0 = off
-        if (value < 0 || value > 64) return SEG_EINVAL;
-        seg::g_nt2_short = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn_fill")) {        // filter-gradient split-K target, blocks per CU
-        if (value < 1 || value > 64) return SEG_EINVAL;
-        seg::g_tn_fill = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn_split_cap")) {   // max filter-gradient split-K slabs
-        if (value < 1 || value > 4096) return SEG_EINVAL;
-        seg::g_tn_split_cap = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn_reduce_sl")) {   // split-lanes of the filter-gradient split-K reducer
-        if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32 && value != 64)
-            return SEG_EINVAL;
-        seg::g_tn_reduce_sl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn2_smallm")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_tn2_smallm = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "adam_blocks")) {   // grid cap of seg_adam_tf1_pack (0 = one block per tile)
-        if (value < 0) return SEG_EINVAL;
-        g_adam_blocks = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt3_fill")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt3_fill = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_stagger_us")) {
-        if (value < 0 || value > 1000) return SEG_EINVAL;
-        seg::g_tn3_stagger_us = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "s1x1")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_s1x1 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_half")) {
-        if (value < 0 || value > 7) return SEG_EINVAL;
-        seg::g_tn3_half = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_adam_abl")) {
-        if (value < 0 || value > 31) return SEG_EINVAL;
-        seg::g_tn3_adam_abl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3_mfast")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_tn3_mfast = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wadam")) {      // warp-specialized fused filter gradient + Adam (conv6 / conv7)
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_wadam = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wadam_abl")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 15) return SEG_EINVAL;
-        seg::g_wadam_abl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "tn3")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_tn3 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt3")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_nt3 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_fill")) {   // filter-gradient split-K: blocks as a percentage of the CUs
-        if (value < 1 || value > 800) return SEG_EINVAL;
-        seg::g_wgrad_fill = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_nt32")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_wgrad_nt32 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "res16c")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_res16c = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "res16")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_res16 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "res64")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_res64 = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "smallc")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_smallc = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_halo")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_wgrad_halo = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_abl")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 3) return SEG_EINVAL;
-        seg::g_wgrad_abl = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_nbias")) {
-        if (value < 1 || value > 4) return SEG_EINVAL;
-        seg::g_wgrad_nbias = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wgrad_nt")) {
-        if (value != 64 && value != 128) return SEG_EINVAL;
-        seg::g_wgrad_nt = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "wpad")) {
-        if (value < 0 || value > 256 || value % 8) return SEG_EINVAL;
-        g_wpad = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "halo_wide")) {
-        if (value != 0 && value != 1) return SEG_EINVAL;
-        seg::g_halo_wide = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "nt2_ablate")) {   // diagnostic builds only: results are garbage
-        if (value < 0 || value > 9) return SEG_EINVAL;
-        seg::g_nt2_ablate = value;
-        return SEG_OK;
-    }
-    if (!strcmp(name, "igemm_tn_variant")) {
-        if (value != 1 && value != 2) return SEG_EINVAL;
-        seg::g_tn_variant = value;
+    static const Knob knobs[] = {
+        {"igemm_nt_variant", &seg::g_nt_variant, 1, 2, 1, {}},
+        {"igemm_tn_variant", &seg::g_tn_variant, 1, 2, 1, {}},
+        {"tn_nsplit", &seg::g_tn_nsplit, 0, 1, 1, {}},
+        {"nt_nsplit", &seg::g_nt_nsplit, 0, 1, 1, {}},
+        {"halo_duo", &seg::g_halo_duo, 0, 1, 1, {}},
+        {"nt_halo", &seg::g_nt_halo, 0, 1, 1, {}},
+        {"halo_wide", &seg::g_halo_wide, 0, 1, 1, {}},
+        {"halo_min_splits", &seg::g_halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
+        {"adam_tr_fused", &g_adam_tr_fused, 0, 1, 1, {}},
+        {"nt2_short", &seg::g_nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
+        {"tn_fill", &seg::g_tn_fill, 1, 64, 1, {}},                   // filter-gradient split-K target, blocks/CU
+        {"tn_split_cap", &seg::g_tn_split_cap, 1, 4096, 1, {}},
+        {"tn_reduce_sl", &seg::g_tn_reduce_sl, 0, 0, 0, {1, 2, 4, 8, 16, 32, 64}},
+        {"tn2_smallm", &seg::g_tn2_smallm, 0, 1, 1, {}},
+        {"adam_blocks", &g_adam_blocks, 0, 1 << 30, 1, {}},           // grid cap of seg_adam_tf1_pack (0: per tile)
+        {"nt3_fill", &seg::g_nt3_fill, 0, 1, 1, {}},
+        {"tn3_stagger_us", &seg::g_tn3_stagger_us, 0, 1000, 1, {}},
+        {"s1x1", &seg::g_s1x1, 0, 1, 1, {}},
+        {"tn3_half", &seg::g_tn3_half, 0, 7, 1, {}},
+        {"tn3_mfast", &seg::g_tn3_mfast, 0, 1, 1, {}},
+        {"tn3", &seg::g_tn3, 0, 1, 1, {}},
+        {"nt3", &seg::g_nt3, 0, 1, 1, {}},
+        {"wgrad_fill", &seg::g_wgrad_fill, 1, 800, 1, {}},            // filter-gradient split-K, % of the CUs
+        {"wgrad_nt32", &seg::g_wgrad_nt32, 0, 1, 1, {}},
+        {"wgrad_nbias", &seg::g_wgrad_nbias, 1, 4, 1, {}},
+        {"wgrad_nt", &seg::g_wgrad_nt, 0, 0, 0, {64, 128}},
+        {"wgrad_halo", &seg::g_wgrad_halo, 0, 1, 1, {}},
+        {"res16c", &seg::g_res16c, 0, 1, 1, {}},
+        {"res16", &seg::g_res16, 0, 1, 1, {}},
+        {"res64", &seg::g_res64, 0, 1, 1, {}},
+        {"smallc", &seg::g_smallc, 0, 1, 1, {}},
+        {"wpad", &g_wpad, 0, 256, 8, {}},
+#ifdef SEG_DIAG
+        {"tn3_abl", &seg::g_tn3_abl, 0, 3, 1, {}},
+        {"tn3_adam_abl", &seg::g_tn3_adam_abl, 0, 31, 1, {}},
+        {"wgrad_abl", &seg::g_wgrad_abl, 0, 3, 1, {}},
+        {"nt2_ablate", &seg::g_nt2_ablate, 0, 9, 1, {}},
+#endif
+    };
+    for (const Knob& k : knobs) {
+        if (strcmp(name, k.name)) continue;
+        bool ok;
+        if (k.step) {
+            ok = value >= k.lo && value <= k.hi && (value - k.lo) % k.step == 0;
+        } else {
+            ok = false;
+            for (int v : k.only) ok = ok || (v != 0 && v == value);
+        }
+        if (!ok) return SEG_EINVAL;
+        *k.var = value;
         return SEG_OK;
     }
     return SEG_EINVAL;
@@ -1015,11 +897,12 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.lr_t = (float)lr_t; p.adam.b1 = a->beta1; p.adam.b2 = a->beta2; p.adam.eps = a->eps;
     p.adam.gs = a->grad_scale;
     p.adam.store_grad = dw != nullptr;
+#ifdef SEG_DIAG
     p.adam.abl = seg::g_tn3_adam_abl;
+#endif
     p.Mp = p.M;
     p.partial = nullptr;
-    if (seg::wadam_ok(p, SEG_BF16)) seg::launch_wadam(p, (hipStream_t)stream);
-    else seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
+    seg::launch_tn3(p, 1, (hipStream_t)stream, SEG_BF16);
     SEG_CHECK_LAUNCH();
     if (tr_after) {
         const int RS = d->R * d->S, C = d->c_valid, K = d->k_valid;

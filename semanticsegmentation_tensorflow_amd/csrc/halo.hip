@@ -40,6 +40,7 @@ int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
+int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -1534,10 +1535,11 @@ bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* 
     const long tiles = (long)hp->geom[1] * hp->geom[2] * nimg * ((p.N + hp->bn - 1) / hp->bn);
     // split-K over channel chunks: minimise (block rounds x chunks per split),
     // +4% per extra split for the fp32 slab round trip and reduce
-    const int cap = std::min(nchunks, std::max(1, max_splits));
-    int kps = nchunks;
+    const int lo = std::min(nchunks, std::max(1, g_halo_min_splits));
+    const int cap = std::max(lo, std::min(nchunks, std::max(1, max_splits)));
+    int kps = (nchunks + lo - 1) / lo;
     double best_t = 1e30;
-    for (int sp = 1; sp <= cap; ++sp) {
+    for (int sp = lo; sp <= cap; ++sp) {
         const int k = (nchunks + sp - 1) / sp;
         const int s2 = (nchunks + k - 1) / k;
         const long rounds = (tiles * s2 + cus - 1) / cus;
@@ -1568,17 +1570,36 @@ static void launch_halo_duo_t(NTParams& p, const HaloGeom& g, long tiles, hipStr
 }
 
 template <int BW, int HI>
-static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, hipStream_t s, int dtype) {
-    // two blocks per CU when there is no split-K (its 80 KiB LDS takes HI = 7 halos for BN = 64 only)
-    // (32-bit in-image offsets; the f16 BW = 32 / BN = 128 instance spills: conv_halo)
-    if (g_halo_duo && gridz == 1 && !p.partial && (bn == 64 || HI == 6) &&
-        (long)p.IH * p.IW * p.ldx < (1L << 31) && !(dtype == SEG_F16 && BW == 32 && bn == 128)) {
+static void launch_halo_bn(NTParams& p, const HaloGeom& g, int bn, long tiles, int gridz, bool duo, hipStream_t s,
+                           int dtype) {
+    if (duo) {
         if (bn == 64) launch_halo_duo_t<BW, HI, 64>(p, g, tiles, s, dtype);
         else launch_halo_duo_t<BW, 6, 128>(p, g, tiles, s, dtype);
         return;
     }
     if (bn == 64) launch_halo_t<BW, HI, 64>(p, g, tiles, gridz, s, dtype);
     else launch_halo_t<BW, HI, 128>(p, g, tiles, gridz, s, dtype);
+}
+
+// Which halo kernel runs plan hp: conv_halo2 for 256-wide blocks; for 64 / 128
+// conv_halo_duo at two blocks per CU when there is no split-K (its 80 KiB LDS
+// takes HI = 7 halos for BN = 64 only; 32-bit in-image offsets; the f16 BW = 32 /
+// BN = 128 instance spills), else conv_halo.
+int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype) {
+    if (hp.bn == 256) return HALO_K2;
+    if (g_halo_duo && hp.splits == 1 && (hp.bn == 64 || hp.hi == 6) && (long)p.IH * p.IW * p.ldx < (1L << 31) &&
+        !(dtype == SEG_F16 && hp.bw == 32 && hp.bn == 128))
+        return HALO_KDUO;
+    return HALO_K1;
+}
+
+// The kernel has the fused MaxPool epilogue for this plan: conv_halo2 (16- and
+// 32-px tile rows, 64-column wave tiles), conv_halo_duo<16, 6, 128> (32-row
+// staging halves, 8 column chunks per row) -- never with split-K slabs.
+bool halo_pools(const HaloPlan& hp, int kernel) {
+    if (hp.splits != 1) return false;
+    if (kernel == HALO_K2) return true;
+    return kernel == HALO_KDUO && hp.bw == 16 && hp.bn == 128 && hp.hi == 6;
 }
 
 bool res16c_ok(const NTParams& p, int dtype) {
@@ -1620,66 +1641,69 @@ bool res64_ok(const NTParams& p, int dtype) {
            (!p.epi.mask || ((uintptr_t)p.epi.mask % 8 == 0 && p.epi.ld_mask % 4 == 0 && p.epi.mask_img % 4 == 0));
 }
 
-void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
+int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     if (p.N <= 16 && g_res16) {               // two blocks per CU (launch bounds: 4 waves / SIMD)
+        if (p.epi.pool_y) return SEG_EINVAL;  // no pooled epilogue in the 16-wide form
         const int grid = std::min(ntiles, 2 * cus);
         if (dtype == SEG_F16)
             hipLaunchKernelGGL((conv_res64<0, f16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         else
             hipLaunchKernelGGL((conv_res64<0, bf16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
-        return;
+        return SEG_OK;
     }
     const int grid = std::min(ntiles, cus);
-    if (dtype == SEG_F16) {
-        hipLaunchKernelGGL((conv_res64<0, f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
-        return;
-    }
-    switch (g_nt2_ablate) {
-        case 1: hipLaunchKernelGGL(conv_res64<1>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
-        case 2: hipLaunchKernelGGL(conv_res64<2>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
-        case 3: hipLaunchKernelGGL(conv_res64<3>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
-        case 4: hipLaunchKernelGGL(conv_res64<4>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles); return;
-    }
-    hipLaunchKernelGGL(conv_res64<0>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64<0, f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    else hipLaunchKernelGGL(conv_res64<0>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    return SEG_OK;
 }
 
-void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype) {
+// Launch plan hp on the kernel halo_kernel() chose.  A pooled launch (p.y
+// null) on a kernel without the pooled epilogue, or with split-K slabs, is
+// refused here, at the kernel choice itself.
+int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype) {
+    if (p.epi.pool_y && !halo_pools(hp, kernel)) return SEG_EINVAL;
+    if (hp.splits > 1 && !p.partial) return SEG_EINVAL;
     HaloGeom g;
     g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
     g.hwd = hp.geom[4]; g.hrows = hp.geom[5]; g.hy0 = hp.geom[6]; g.hx0 = hp.geom[7];
     g.nchunks = hp.geom[8]; g.kc_per_split = hp.geom[9];
-    if (hp.bn == 256) {
+    const int gridz = hp.splits;
+    if (kernel == HALO_K2) {
         const dim3 grid((unsigned)hp.tiles, 1, gridz);
+#ifdef SEG_DIAG   // ablation builds (garbage results): tools/ only
+        if (g_nt2_ablate && hp.bw == 16 && dtype == SEG_BF16) {
+            switch (g_nt2_ablate) {
+                case 1: hipLaunchKernelGGL((conv_halo2<16, 1>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 2: hipLaunchKernelGGL((conv_halo2<16, 2>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 3: hipLaunchKernelGGL((conv_halo2<16, 3>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 4: hipLaunchKernelGGL((conv_halo2<16, 4>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 5: hipLaunchKernelGGL((conv_halo2<16, 5>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 7: hipLaunchKernelGGL((conv_halo2<16, 7>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+                case 9: hipLaunchKernelGGL((conv_halo2<16, 9>), grid, dim3(512), 0, s, p, g); return SEG_OK;
+            }
+        }
+#endif
         if (dtype == SEG_F16) {
             if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, 0, f16>), grid, dim3(512), 0, s, p, g);
             else hipLaunchKernelGGL((conv_halo2<32, 0, f16>), grid, dim3(512), 0, s, p, g);
-            return;
+        } else {
+            if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<32>), grid, dim3(512), 0, s, p, g);
         }
-        if (g_nt2_ablate && hp.bw == 16) {   // diagnostics
-            switch (g_nt2_ablate) {
-                case 1: hipLaunchKernelGGL((conv_halo2<16, 1>), grid, dim3(512), 0, s, p, g); return;
-                case 2: hipLaunchKernelGGL((conv_halo2<16, 2>), grid, dim3(512), 0, s, p, g); return;
-                case 3: hipLaunchKernelGGL((conv_halo2<16, 3>), grid, dim3(512), 0, s, p, g); return;
-                case 4: hipLaunchKernelGGL((conv_halo2<16, 4>), grid, dim3(512), 0, s, p, g); return;
-                case 5: hipLaunchKernelGGL((conv_halo2<16, 5>), grid, dim3(512), 0, s, p, g); return;
-                case 7: hipLaunchKernelGGL((conv_halo2<16, 7>), grid, dim3(512), 0, s, p, g); return;
-                case 9: hipLaunchKernelGGL((conv_halo2<16, 9>), grid, dim3(512), 0, s, p, g); return;
-            }
-        }
-        if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16>), grid, dim3(512), 0, s, p, g);
-        else hipLaunchKernelGGL((conv_halo2<32>), grid, dim3(512), 0, s, p, g);
-        return;
+        return SEG_OK;
     }
+    const bool duo = kernel == HALO_KDUO;
     switch (hp.bw * 10 + hp.hi) {
-        case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
-        default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, s, dtype); break;
+        case 166: launch_halo_bn<16, 6>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
+        case 167: launch_halo_bn<16, 7>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
+        case 326: launch_halo_bn<32, 6>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
+        case 327: launch_halo_bn<32, 7>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
+        case 646: launch_halo_bn<64, 6>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
+        default: launch_halo_bn<64, 7>(p, g, hp.bn, hp.tiles, gridz, duo, s, dtype); break;
     }
+    return SEG_OK;
 }
 
 }  // namespace seg

@@ -136,8 +136,6 @@ struct TNParams {
         int stagger;           // half tiles: second block per CU starts this many 10 ns ticks late
         int first_round;       // blocks of the first dispatch round (2 per CU)
         int* cu_slots;         // per-CU arrival counters (zeroed per launch)
-        unsigned state_bytes;  // wadam.hip: extent of the p / m / v (and gradient) slices
-        unsigned rows_bytes;   // wadam.hip: extent of the bf16 rows copy
     } adam;
     ProParams pro;             // A = x operand prologue (igemm_tn only)
 };
@@ -240,11 +238,6 @@ inline bool tn3_applies(int M, int N, int dtype) {
 void tn3_info(int M, int N, int P, int cus, int* splits);
 void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype);
 bool tn3_adam_ok(const TNParams& p, int dtype);
-// warp-specialized filter gradient + TF1 Adam (wadam.hip) for the fused conv6 / conv7 launches
-extern int g_wadam;
-extern int g_wadam_abl;
-bool wadam_ok(const TNParams& p, int dtype);
-void launch_wadam(TNParams& p, hipStream_t s);
 
 // halo-tiled direct conv (halo.hip) for stride-1 NT problems
 struct HaloPlan {
@@ -254,9 +247,13 @@ struct HaloPlan {
 };
 extern int g_nt_halo;
 extern int g_halo_wide;
+extern int g_halo_min_splits;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
-void launch_halo(NTParams& p, const HaloPlan& hp, int gridz, hipStream_t s, int dtype = SEG_BF16);
+enum { HALO_K1 = 0, HALO_KDUO = 1, HALO_K2 = 2 };   // conv_halo, conv_halo_duo, conv_halo2
+int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype);
+bool halo_pools(const HaloPlan& hp, int kernel);
+int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype = SEG_BF16);
 extern int g_res64;
 extern int g_res16;
 extern int g_res16c;
@@ -265,7 +262,7 @@ void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
 int res16c_grid(const NTParams& p, int cus);
 void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype);
 bool res64_ok(const NTParams& p, int dtype);
-void launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
+int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 
 // 8-input-channel first layer (smallc.hip)
 extern int g_smallc;

@@ -715,6 +715,7 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
         nt3_info(M, N, K, num_cus(), &s3);
         splits = std::max(splits, s3);
     }
+    if (g_nt_variant == 2 && dtype != SEG_F32) splits = std::max(splits, std::min(g_halo_min_splits, K / 64));
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
@@ -741,105 +742,170 @@ static void launch_nt_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     hipLaunchKernelGGL((igemm_nt<T, BM, BN>), dim3(tiles, 1, gridz), dim3(256), 0, s, p);
 }
 
+// The ONE kernel decision for an NT problem: launch_nt_typed launches the
+// plan, nt_choice names it, nt_pool_ok reads its pooled-epilogue flag, so the
+// host-side checks and the launch can never disagree.
+enum NTKind { NTK_PRO2, NTK_PRO_REG, NTK_RES16C, NTK_RES64, NTK_HALO, NTK_NT3, NTK_NT3_NSPLIT, NTK_NT2, NTK_REG };
+struct NTPlan {
+    int kind, bm, bn, splits;
+    HaloPlan hp;
+    int halo_kernel;     // NTK_HALO: halo_kernel(p, hp, dtype)
+};
+
+static NTPlan nt_plan(const NTParams& p, int dtype, int nphases, int max_m) {
+    NTPlan pl = {};
+    const bool h16 = dtype == SEG_BF16 || dtype == SEG_F16;
+    const int bk = dtype == SEG_F32 ? 32 : 64;
+    choose_nt(max_m, p.N, p.K, bk, pl.bm, pl.bn, pl.splits);
+    if (nphases > 1) pl.splits = 1;
+    if (p.pro.gamma) {
+        if (g_nt_variant == 2 && nt2_pro_ok(p, dtype, nphases)) {   // 1x1: K <= 1024, no split-K
+            pl.kind = NTK_PRO2;
+            pl.splits = 1;
+            return pl;
+        }
+        pl.kind = NTK_PRO_REG;                 // operand prologue: the register-staged kernel
+        pl.bm = 128;
+        const long tiles = (long)((max_m + 127) / 128) * ((p.N + pl.bn - 1) / pl.bn);
+        pl.splits = 1;
+        if (tiles < 2 * num_cus()) {
+            const int kt = (p.K + bk - 1) / bk;
+            pl.splits = std::min<int>(std::max(1, kt / 8), (int)((2 * num_cus() + tiles - 1) / tiles));
+        }
+        return pl;
+    }
+    if (h16 && nphases == 1 && g_nt_variant == 2 && res16c_ok(p, dtype)) {
+        pl.kind = NTK_RES16C;
+        pl.bm = 256; pl.bn = 64; pl.splits = 1;
+        return pl;
+    }
+    if (h16 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dtype)) {
+        pl.kind = NTK_RES64;
+        pl.bn = (p.N <= 16 && g_res16) ? 16 : 64;
+        pl.splits = 1;
+        return pl;
+    }
+    if (h16 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, dtype, pl.splits, num_cus(), &pl.hp)) {
+        pl.kind = NTK_HALO;
+        pl.bm = 256; pl.bn = pl.hp.bn; pl.splits = pl.hp.splits;
+        pl.halo_kernel = halo_kernel(p, pl.hp, dtype);
+        return pl;
+    }
+    if (h16 && g_nt_variant == 2 && nt3_pick(p, dtype, nphases, max_m)) {
+        nt3_info(max_m, p.N, p.K, num_cus(), &pl.splits);
+        if (nphases > 1) pl.splits = 1;
+        pl.bm = pl.bn = 256;
+        // N = 256 k + a tail of <= 128 columns (FC-DenseNet's 320 / 560 / 352 /
+        // 280-wide transposed-conv GEMMs): the 256-aligned head on igemm_nt3, the
+        // tail on igemm_nt2 (256 x 64 / 128 tiles) instead of a 256-wide tile that
+        // is 50-80 % padding.  Not with dropout (its counter uses the full row
+        // width) or the BN-backward epilogue (per-tile column sums).
+        pl.kind = (pl.splits == 1 && g_nt_nsplit && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128 &&
+                   p.epi.keep_prob >= 1.f && !p.epi.bn_x) ? NTK_NT3_NSPLIT : NTK_NT3;
+        return pl;
+    }
+    pl.kind = pl.bm == 256 ? NTK_NT2 : NTK_REG;
+    return pl;
+}
+
+// Whether the planned kernel has the fused MaxPool epilogue (EpiParams
+// pool_y): conv_res64 with 64-wide output blocks, conv_halo_duo with 16-px
+// tile rows and 128-wide blocks, conv_halo2 -- each without split-K.
+static bool nt_plan_pools(const NTPlan& pl) {
+    if (pl.kind == NTK_RES64) return pl.bn == 64;
+    if (pl.kind == NTK_HALO) return halo_pools(pl.hp, pl.halo_kernel);
+    return false;
+}
+
 template <typename T>
 static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BK = 128 / sizeof(T);
-    int bm, bn, splits;
-    choose_nt(max_m, p.N, p.K, BK, bm, bn, splits);
-    if (nphases > 1) splits = 1;
+    const NTPlan pl = nt_plan(p, dt_traits<T>::id, nphases, max_m);
+    // a pooled launch writes no unpooled map (p.y is null): only a kernel with
+    // the pooled epilogue and no split-K slabs may run it
+    if (p.epi.pool_y && !nt_plan_pools(pl)) return SEG_EINVAL;
+    int splits = pl.splits;
     p.partial = nullptr;
-    if (p.pro.gamma && g_nt_variant == 2 && nt2_pro_ok(p, dt_traits<T>::id, nphases)) {
-        launch_nt2_pro(p, dt_traits<T>::id, 1, max_m, s);    // 1x1: K <= 1024, no split-K
-        SEG_CHECK_LAUNCH();
-        return SEG_OK;
-    }
-    if (p.pro.gamma) {                     // operand prologue: the register-staged kernel
-        bm = 128;
-        const long tiles = (long)((max_m + 127) / 128) * ((p.N + bn - 1) / bn);
-        splits = 1;
-        if (tiles < 2 * num_cus()) {
-            const int kt = (p.K + BK - 1) / BK;
-            splits = std::min<int>(std::max(1, kt / 8), (int)((2 * num_cus() + tiles - 1) / tiles));
-        }
-        int gridz = nphases;
-        if (splits > 1) {
-            const int kt = (p.K + BK - 1) / BK;
-            p.kt_per_split = (kt + splits - 1) / splits;
-            splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
-            if (!ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float)) return SEG_EWORKSPACE;
-            p.partial = reinterpret_cast<float*>(ws);
-            gridz = splits;
-        }
-        if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
-        else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
-        SEG_CHECK_LAUNCH();
-        if (p.partial) {
-            const long total = (long)p.M * (p.N / 8);
-            if (total >= (1L << 31)) return SEG_EINVAL;
-            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+    switch (pl.kind) {
+        case NTK_PRO2:
+            launch_nt2_pro(p, dt_traits<T>::id, 1, max_m, s);
             SEG_CHECK_LAUNCH();
-            p.partial = nullptr;
-        }
-        return SEG_OK;
-    }
-    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res16c_ok(p, dt_traits<T>::id)) {
-        launch_res16c(p, num_cus(), s, dt_traits<T>::id);
-        SEG_CHECK_LAUNCH();
-        return SEG_OK;
-    }
-    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dt_traits<T>::id)) {
-        launch_res64(p, num_cus(), s, dt_traits<T>::id);
-        SEG_CHECK_LAUNCH();
-        return SEG_OK;
-    }
-    HaloPlan hp;
-    if (sizeof(T) == 2 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, dt_traits<T>::id, splits, num_cus(), &hp)) {
-        if (hp.splits > 1) {
-            const size_t need = (size_t)hp.splits * p.M * p.N * sizeof(float);
-            if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
-            p.partial = reinterpret_cast<float*>(ws);
-        }
-        launch_halo(p, hp, hp.splits, s, dt_traits<T>::id);
-        SEG_CHECK_LAUNCH();
-        if (p.partial) {
-            const long total = (long)p.M * (p.N / 8);
-            if (total >= (1L << 31)) return SEG_EINVAL;
-            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, hp.splits);
+            return SEG_OK;
+        case NTK_PRO_REG: {
+            int gridz = nphases;
+            if (splits > 1) {
+                const int kt = (p.K + BK - 1) / BK;
+                p.kt_per_split = (kt + splits - 1) / splits;
+                splits = (kt + p.kt_per_split - 1) / p.kt_per_split;
+                if (!ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float)) return SEG_EWORKSPACE;
+                p.partial = reinterpret_cast<float*>(ws);
+                gridz = splits;
+            }
+            if (pl.bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
+            else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
             SEG_CHECK_LAUNCH();
-            p.partial = nullptr;
+            if (p.partial) {
+                const long total = (long)p.M * (p.N / 8);
+                if (total >= (1L << 31)) return SEG_EINVAL;
+                hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+                SEG_CHECK_LAUNCH();
+                p.partial = nullptr;
+            }
+            return SEG_OK;
         }
-        return SEG_OK;
-    }
-    const bool nt3 = sizeof(T) == 2 && g_nt_variant == 2 && nt3_pick(p, dt_traits<T>::id, nphases, max_m);
-    if (nt3) {
-        nt3_info(max_m, p.N, p.K, num_cus(), &splits);
-        if (nphases > 1) splits = 1;
-    }
-    // N = 256 k + a tail of <= 128 columns (FC-DenseNet's 320 / 560 / 352 /
-    // 280-wide transposed-conv GEMMs): the 256-aligned head on igemm_nt3, the
-    // tail on igemm_nt2 (256 x 64 / 128 tiles) instead of a 256-wide tile that
-    // is 50-80 % padding.  Not with dropout (its counter uses the full row
-    // width) or the BN-backward epilogue (per-tile column sums).
-    if (nt3 && splits == 1 && g_nt_nsplit && p.N > 256 && p.N % 256 != 0 && p.N % 256 <= 128 &&
-        p.epi.keep_prob >= 1.f && !p.epi.bn_x) {
-        const int nh = p.N / 256 * 256;
-        NTParams t = p;
-        p.N = nh;
-        launch_nt3(p, nphases, max_m, s, dt_traits<T>::id);
-        SEG_CHECK_LAUNCH();
-        p.N = t.N;
-        t.N -= nh;
-        t.w = reinterpret_cast<const T*>(t.w) + (long)nh * t.w_col;
-        t.y = reinterpret_cast<T*>(t.y) + nh;
-        if (t.epi.bias) t.epi.bias += nh;
-        if (t.epi.scale) t.epi.scale += nh;
-        if (t.epi.shift) t.epi.shift += nh;
-        if (t.epi.residual) t.epi.residual = reinterpret_cast<const T*>(t.epi.residual) + nh;
-        if (t.epi.mask) t.epi.mask = reinterpret_cast<const T*>(t.epi.mask) + nh;
-        t.epi.n_valid = std::max(0, t.epi.n_valid - nh);
-        launch_nt2(t, dt_traits<T>::id, t.N <= 64 ? 64 : 128, nphases, max_m, s);
-        SEG_CHECK_LAUNCH();
-        return SEG_OK;
+        case NTK_RES16C:
+            launch_res16c(p, num_cus(), s, dt_traits<T>::id);
+            SEG_CHECK_LAUNCH();
+            return SEG_OK;
+        case NTK_RES64: {
+            const int st = launch_res64(p, num_cus(), s, dt_traits<T>::id);
+            if (st) return st;
+            SEG_CHECK_LAUNCH();
+            return SEG_OK;
+        }
+        case NTK_HALO: {
+            if (pl.hp.splits > 1) {
+                const size_t need = (size_t)pl.hp.splits * p.M * p.N * sizeof(float);
+                if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
+                p.partial = reinterpret_cast<float*>(ws);
+            }
+            const int st = launch_halo(p, pl.hp, pl.halo_kernel, s, dt_traits<T>::id);
+            if (st) {
+                p.partial = nullptr;
+                return st;
+            }
+            SEG_CHECK_LAUNCH();
+            if (p.partial) {
+                const long total = (long)p.M * (p.N / 8);
+                if (total >= (1L << 31)) return SEG_EINVAL;
+                hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, pl.hp.splits);
+                SEG_CHECK_LAUNCH();
+                p.partial = nullptr;
+            }
+            return SEG_OK;
+        }
+        case NTK_NT3_NSPLIT: {
+            const int nh = p.N / 256 * 256;
+            NTParams t = p;
+            p.N = nh;
+            launch_nt3(p, nphases, max_m, s, dt_traits<T>::id);
+            SEG_CHECK_LAUNCH();
+            p.N = t.N;
+            t.N -= nh;
+            t.w = reinterpret_cast<const T*>(t.w) + (long)nh * t.w_col;
+            t.y = reinterpret_cast<T*>(t.y) + nh;
+            if (t.epi.bias) t.epi.bias += nh;
+            if (t.epi.scale) t.epi.scale += nh;
+            if (t.epi.shift) t.epi.shift += nh;
+            if (t.epi.residual) t.epi.residual = reinterpret_cast<const T*>(t.epi.residual) + nh;
+            if (t.epi.mask) t.epi.mask = reinterpret_cast<const T*>(t.epi.mask) + nh;
+            t.epi.n_valid = std::max(0, t.epi.n_valid - nh);
+            launch_nt2(t, dt_traits<T>::id, t.N <= 64 ? 64 : 128, nphases, max_m, s);
+            SEG_CHECK_LAUNCH();
+            return SEG_OK;
+        }
+        default:
+            break;
     }
     int gridz = nphases;
     if (splits > 1) {
@@ -851,63 +917,41 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
         p.partial = reinterpret_cast<float*>(ws);
         gridz = splits;
     }
-    if (nt3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
-    else if (bm == 256) launch_nt2(p, dt_traits<T>::id, bn, gridz, max_m, s);
-    else if (bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
+    if (pl.kind == NTK_NT3) launch_nt3(p, gridz, max_m, s, dt_traits<T>::id);
+    else if (pl.kind == NTK_NT2) launch_nt2(p, dt_traits<T>::id, pl.bn, gridz, max_m, s);
+    else if (pl.bn == 64) launch_nt_t<T, 128, 64>(p, gridz, max_m, s);
     else launch_nt_t<T, 128, 128>(p, gridz, max_m, s);
     SEG_CHECK_LAUNCH();
     if (p.partial) {
         const long total = (long)p.M * (p.N / 8);
         if (total >= (1L << 31)) return SEG_EINVAL;
-            hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
+        hipLaunchKernelGGL(splitk_reduce_nt<T>, dim3(seg_grid_1d(total, 256)), dim3(256), 0, s, p, splits);
         SEG_CHECK_LAUNCH();
     }
     p.partial = nullptr;
     return SEG_OK;
 }
 
-// Whether launch_nt's kernel for p has the fused MaxPool epilogue (EpiParams
-// pool_y): conv_res64 with 64-wide output blocks, conv_halo_duo with 16-px tile
-// rows and 64-column wave tiles, conv_halo2's 256-wide tiles -- each without
-// split-K (host-only mirror of launch_nt_typed / launch_halo's choices).
 bool nt_pool_ok(const NTParams& p, int dtype) {
-    if ((dtype != SEG_BF16 && dtype != SEG_F16) || g_nt_variant != 2 || p.pro.gamma || p.phase) return false;
-    if (res16c_ok(p, dtype)) return false;
-    if (res64_ok(p, dtype)) return !(p.N <= 16 && g_res16);
-    int bm, bn, splits;
-    choose_nt(p.M, p.N, p.K, 64, bm, bn, splits);
-    HaloPlan hp;
-    if (!halo_plan(p, dtype, splits, num_cus(), &hp) || hp.splits != 1) return false;
-    if (hp.bn == 256) return true;
-    // conv_halo_duo (launch_halo_bn's condition) with BW = 16 and BN = 128
-    return hp.bn == 128 && hp.bw == 16 && g_halo_duo && hp.hi == 6 && (long)p.IH * p.IW * p.ldx < (1L << 31);
+    if ((dtype != SEG_BF16 && dtype != SEG_F16) || p.pro.gamma || p.phase) return false;
+    return nt_plan_pools(nt_plan(p, dtype, 1, p.M));
 }
 
-// The kernel launch_nt would pick for p (host-only mirror of launch_nt_typed).
+// The kernel family launch_nt runs for p (named from the same plan).
 const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int* bm, int* bn, int* splits) {
-    const int bk = dtype == SEG_F32 ? 32 : 64;
-    choose_nt(max_m, p.N, p.K, bk, *bm, *bn, *splits);
-    if (nphases > 1) *splits = 1;
-    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res16c_ok(p, dtype)) {
-        *bm = 256; *bn = 64; *splits = 1;
-        return "conv_res16c";
+    const NTPlan pl = nt_plan(p, dtype, nphases, max_m);
+    *bm = pl.bm; *bn = pl.bn; *splits = pl.splits;
+    switch (pl.kind) {
+        case NTK_PRO2: return "igemm_nt2_pro";
+        case NTK_PRO_REG: return "igemm_nt_pro";
+        case NTK_RES16C: return "conv_res16c";
+        case NTK_RES64: return "conv_res64";
+        case NTK_HALO: return "conv_halo";
+        case NTK_NT3:
+        case NTK_NT3_NSPLIT: return "igemm_nt3";
+        case NTK_NT2: return "igemm_nt2";
+        default: return "igemm_nt";
     }
-    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && res64_ok(p, dtype)) {
-        *bn = (p.N <= 16 && g_res16) ? 16 : 64; *splits = 1;
-        return "conv_res64";
-    }
-    HaloPlan hp;
-    if (dtype != SEG_F32 && nphases == 1 && g_nt_variant == 2 && halo_plan(p, dtype, *splits, num_cus(), &hp)) {
-        *bm = 256; *bn = hp.bn; *splits = hp.splits;
-        return "conv_halo";
-    }
-    if ((dtype == SEG_BF16 || dtype == SEG_F16) && g_nt_variant == 2 && nt3_pick(p, dtype, nphases, max_m)) {
-        nt3_info(max_m, p.N, p.K, num_cus(), splits);
-        if (nphases > 1) *splits = 1;
-        *bm = *bn = 256;
-        return "igemm_nt3";
-    }
-    return *bm == 256 ? "igemm_nt2" : "igemm_nt";
 }
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {

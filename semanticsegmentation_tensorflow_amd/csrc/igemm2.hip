@@ -669,6 +669,7 @@ template <typename T, int BM, int BN, int WM, int WN>
 void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const dim3 g(tiles, 1, gridz), b(WM * WN * 64);
+#ifdef SEG_DIAG   // ablation builds (garbage results): tools/ only
     if constexpr (is_bf16_v<T> && BN == 128) {
         switch (g_nt2_ablate) {
             case 1: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 1>), g, b, 0, s, p); return;
@@ -676,6 +677,7 @@ void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
             case 3: hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN, 3>), g, b, 0, s, p); return;
         }
     }
+#endif
     hipLaunchKernelGGL((igemm_nt2<T, BM, BN, WM, WN>), g, b, 0, s, p);
 }
 

@@ -689,7 +689,11 @@ __global__ __launch_bounds__(BN * 2, 2) void igemm_tn3(TNParams p, int tiles_m, 
         constexpr int WB = QR * SROWF + WTN * SROWT;
         static_assert(NW * WB <= SMEM, "fused epilogue staging must fit");
         const auto& A = p.adam;
-        const int abl = A.abl;
+#ifdef SEG_DIAG
+        const int abl = A.abl;     // ablation bits (garbage results): diagnostic build only
+#else
+        constexpr int abl = 0;
+#endif
         if (abl & 16) {
             if (acc[0][0][0] == 12345.f && acc[7][3][3] == 54321.f) p.out[tid] = acc[3][1][2];
             return;
@@ -901,11 +905,13 @@ void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {
     const dim3 g(tm * tn * splits), b(512);
     const bool mfast = g_tn3_mfast && tm > tn;
 #define TN3(A, MF) hipLaunchKernelGGL((igemm_tn3<A, MF>), g, b, 0, s, p, tm, tn, splits)
+#ifdef SEG_DIAG   // ablation builds (garbage results): tools/ only
     switch (g_tn3_abl) {
         case 1: TN3(1, false); return;
         case 2: TN3(2, false); return;
         case 3: TN3(3, false); return;
     }
+#endif
     if (p.adam.p) {
         if (mfast) hipLaunchKernelGGL((igemm_tn3<0, true, true>), g, b, 0, s, p, tm, tn, splits);
         else hipLaunchKernelGGL((igemm_tn3<0, false, true>), g, b, 0, s, p, tm, tn, splits);

@@ -362,12 +362,14 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
     g.nbias = wp.nbias;
     const dim3 grid((unsigned)wp.blocks), block(512);
     const bool small = g.hrows <= 4 * 64;     // 4 halo pieces -> 3 stages fit
-    if (g_wgrad_abl && wp.nt == 128 && dtype == SEG_BF16) {   // diagnostics
+#ifdef SEG_DIAG   // ablation builds (garbage results): tools/ only
+    if (g_wgrad_abl && wp.nt == 128 && dtype == SEG_BF16) {
         if (g_wgrad_abl == 1) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 1>), grid, block, 0, s, p, g);
         if (g_wgrad_abl == 2) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 2>), grid, block, 0, s, p, g);
         if (g_wgrad_abl == 3) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 3>), grid, block, 0, s, p, g);
         return;
     }
+#endif
     if (dtype == SEG_F16) {
         if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 0, f16>), grid, block, 0, s, p, g);
         else if (wp.nt == 32 && small) hipLaunchKernelGGL((wgrad_halo<32, 3, 4, 0, f16>), grid, block, 0, s, p, g);

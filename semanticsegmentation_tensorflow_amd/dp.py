@@ -125,6 +125,11 @@ class DataParallel:
             self._launch(j)
             j += 1
 
+    def abort_step(self):
+        """A step that raised mid-backward: forget its bucket state (the
+        collectives already issued complete on their own streams)."""
+        self._reset()
+
     def finish(self):
         for i in range(len(self.buckets)):
             if not self.launched[i]:

@@ -1150,18 +1150,30 @@ class Session:
             if self.dp is not None and p.never_ready:
                 self.dp.ready(p.never_ready)
             self._ready_filter = p.var_set
+            ok = False
             try:
                 self._backward(p, scal)
+                self._tick_fused(flush=True)
+                ok = True
             finally:
+                # on an exception: no stale fused conv6 / conv7 update is left
+                # for the next step, and the compute stream does not run ahead
+                # of side-stream kernels still reading this step's buffers
                 self._ready_filter = None
-            self._tick_fused(flush=True)
-            if self._red is not None:            # pending filter-gradient reductions done before Adam
-                self._red[1].wait_stream(self._red[0])
-                self._red = None
-            if self.dp is not None:
-                self.dp.finish()
-                self.dp.on_launch = None
-                self.dp.launch_streams = None
+                if not ok:
+                    self._pending_fused = []
+                    self._fused = None
+                    self._adam_ctx = None
+                if self._red is not None:        # pending filter-gradient reductions done before Adam
+                    self._red[1].wait_stream(self._red[0])
+                    self._red = None
+                if self.dp is not None:
+                    if ok:
+                        self.dp.finish()
+                    else:
+                        self.dp.abort_step()
+                    self.dp.on_launch = None
+                    self.dp.launch_streams = None
             if scaled and not self._grads_finite():
                 # overflow in the scaled fp16 gradients: no update this step
                 # (TF LossScaleOptimizer), halve the scale

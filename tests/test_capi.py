@@ -41,3 +41,47 @@ def test_status_strings_and_descriptor_rules():
     # k16 s8 conv_t3 at 384 -> pad 4/4
     assert lib.seg_tconv_desc_init(ctypes.byref(d), 1, 48, 156, 256, 384, 1248, 2, 16, 16, 8, 0, 1) == 0
     assert (d.pad_top, d.pad_bottom, d.pad_left, d.pad_right) == (4, 4, 4, 4)
+
+
+def test_pooled_conv_refuses_a_split_k_plan():
+    """a MaxPool-fused conv (p.y null, the pooled map only) must
+    never run on split-K slabs or a kernel without the pooled epilogue.  The
+    pooled-plan check (seg_conv2d_fwd_pool_ok) and the launch read the same plan
+    function, and the launch itself refuses a pooled launch on such a plan
+    with SEG_EINVAL -- host-side, before anything reaches the GPU (here: no GPU,
+    so the fake pointers are never touched).  Network/model/FCN.py:54-75."""
+    import ctypes
+    lib = _lib.load()
+    d = _lib.SegConvDesc()
+    # conv3_3 + pool3 of C2 (conv_halo2, 256-wide tiles) and conv2_2 + pool2
+    # (conv_halo_duo): both pooled by default
+    for args in ((4, 96, 312, 256, 256), (4, 192, 624, 128, 128)):
+        assert lib.seg_conv_desc_init(ctypes.byref(d), *args, 3, 3, 1, 1, 0, 1) == 0
+        assert lib.seg_conv2d_fwd_pool_ok(ctypes.byref(d)) == 1
+        assert lib.seg_set_option(b"halo_min_splits", 2) == 0
+        try:
+            name = ctypes.create_string_buffer(64)
+            sp = ctypes.c_int(0)
+            fl = ctypes.c_double(0)
+            assert lib.seg_conv_kernel_info(ctypes.byref(d), 0, name, 64, ctypes.byref(sp), ctypes.byref(fl)) == 0
+            assert name.value.startswith(b"conv_halo") and sp.value >= 2, (name.value, sp.value)
+            assert lib.seg_conv2d_fwd_pool_ok(ctypes.byref(d)) == 0
+            fake = ctypes.c_void_p(1 << 20)
+            st = lib.seg_conv2d_fwd_pool(ctypes.byref(d), fake, fake, None, fake, args[4], None, 0, fake,
+                                         ctypes.c_size_t(1 << 40), None)
+            assert st == 1, st          # SEG_EINVAL, nothing launched
+        finally:
+            assert lib.seg_set_option(b"halo_min_splits", 1) == 0
+        assert lib.seg_conv2d_fwd_pool_ok(ctypes.byref(d)) == 1
+
+
+def test_product_library_has_no_ablation_knobs():
+    """the kernel-ablation modes (garbage results) are not
+    reachable through seg_set_option / SEG_OPTIONS in libsegkern.so."""
+    lib = _lib.load()
+    EINVAL = 1
+    for knob in (b"nt2_ablate", b"tn3_abl", b"tn3_adam_abl", b"wgrad_abl", b"wadam_abl", b"wadam"):
+        assert lib.seg_set_option(knob, 1) == EINVAL, knob
+    assert lib.seg_set_option(b"tn_reduce_sl", 3) == EINVAL
+    assert lib.seg_set_option(b"tn_reduce_sl", 16) == 0
+    assert lib.seg_set_option(b"wpad", 12) == EINVAL

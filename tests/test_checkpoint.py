@@ -121,3 +121,36 @@ def test_saver_beta_powers_at_step0_and_large_steps(dry, tmp_path):  # noqa: F81
     # TF-written powers: 0.9^(t+1) denormal / zero, 0.999^(t+1) still normal
     assert C._adam_step({"beta1_power": np.float32(0.0), "beta2_power": np.float32(0.999 ** 5001)}) == 5000
     assert C._adam_step({}) == 0
+
+
+def test_adam_step_past_float32_range(dry, tmp_path):  # noqa: F811
+    """a run of the reference's length (MAX_ITERATION = 100001)
+    leaves beta2_power = 0.999^(t+1) denormal (t ~ 87k-103k) or 0 (beyond);
+    restore still recovers the step (denormal: an estimate, bias correction
+    is 1 to float32 precision there), falling back to global_step or the
+    underflow step instead of refusing the checkpoint."""
+    from semanticsegmentation_tensorflow_amd import checkpoint as C
+    G.reset_default_graph()
+    image = tf.placeholder(tf.float32, [None, 32, 32, 3])
+    FCN(image, 1.0, 2).create()
+    gstep = tf.Variable(0, trainable=False, name="global_step")
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="f32")
+    sess.run(tf.global_variables_initializer())
+    saver = tf.train.Saver(tf.global_variables())
+    for t, gs in ((100000, 100000), (250000, 250000), (250000, 0)):
+        sess.store.step = t
+        sess.assign("global_step", gs)
+        p = saver.save(sess, str(tmp_path / f"m{t}_{gs}" / "m"))
+        z = tf_bundle.read_bundle(p, ["beta2_power"])
+        assert float(z["beta2_power"]) == np.float32(0.999 ** (t + 1))
+        sess.store.step = 0
+        saver.restore(sess, p)
+        if t == 100000:                 # denormal beta2_power: within its resolution
+            assert abs(sess.store.step - t) <= 50, sess.store.step
+        elif gs:
+            assert sess.store.step == gs
+        else:
+            assert sess.store.step == C._UNDERFLOW_STEP
+    assert np.float32(0.999 ** C._UNDERFLOW_STEP) == 0 and np.float32(0.999 ** (C._UNDERFLOW_STEP - 900)) > 0
+    # legacy .npz convention (beta^t): no off-by-one
+    assert C._adam_step({"beta2_power": np.float32(0.999 ** 7)}, offset=0) == 7

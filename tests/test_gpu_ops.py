@@ -663,22 +663,19 @@ ADAM_FUSED_CASES = [
     (1, 5, 7, 36, 264, 7),      # c_valid = 36 < Cg = 40: padding rows of the packed copies untouched
     (2, 6, 9, 512, 512, 1),     # conv7-like 1x1
     (2, 11, 13, 256, 392, 1),   # 9 pixel stages of 32, N tail of the 128-wide half tile
-    (2, 12, 39, 256, 2048, 7),  # 1568 128x128 tiles: ~6 per persistent wadam block, 15 pixel stages
+    (2, 12, 39, 256, 2048, 7),  # 7x7 over 2048 columns: multi-round half-tile grid, 15 pixel stages
 ]
 
 
-# (wadam, tn3_half, adam_tr_fused): the warp-specialized kernel (wadam.hip), and
-# igemm_tn3's fused epilogue on half / full tiles (the KRSC copy by the
-# transpose, or in the epilogue -- which always takes igemm_tn3)
-@pytest.fixture(params=[(1, 1, 0), (0, 5, 0), (0, 0, 0), (1, 0, 1)],
-                ids=["wadam", "half-tiles", "full-tiles", "full-tiles-tr-fused"])
+# (tn3_half, adam_tr_fused): igemm_tn3's fused epilogue on half / full tiles
+# (the KRSC copy by the transpose, or in the epilogue)
+@pytest.fixture(params=[(1, 0), (5, 0), (0, 0), (0, 1)],
+                ids=["default", "half-tiles", "full-tiles", "full-tiles-tr-fused"])
 def adam_tiles(request, dev):
-    wadam, half, trf = request.param
-    ops.set_option("wadam", wadam)
+    half, trf = request.param
     ops.set_option("tn3_half", half)
     ops.set_option("adam_tr_fused", trf)
     yield request.param
-    ops.set_option("wadam", 0)
     ops.set_option("tn3_half", 1)
     ops.set_option("adam_tr_fused", 0)
 

@@ -82,3 +82,41 @@ def test_conv_pool_rejects_unsupported(dev):
     out2 = torch.empty(2, 20, 35, 64, dtype=torch.bfloat16, device=dev)
     with pytest.raises(Exception):
         ops.conv2d_fwd_pool(d2, x2, w2, out2, None, ops.epilogue(relu=True, keep_prob=0.5))
+
+
+@pytest.mark.parametrize("case", [(2, 96, 312, 256, 256), (4, 96, 128, 128, 128)],
+                         ids=["conv_halo2", "conv_halo_duo"])
+def test_forced_split_plan_refuses_pool_and_stays_exact(dev, case):
+    """VERDICT r03 (the halo_cus hang): force a split-K halo plan on a conv the
+    default plan pools.  The pooled launch is refused on the host (SEG_EINVAL,
+    no kernel runs); the same conv unpooled on the split plan (conv_halo +
+    splitk_reduce_nt) equals the default single-pass kernel's output within
+    bf16 rounding of the fp32 slab sums."""
+    N, H, W, C, K = case
+    d = ops.conv_desc(N, H, W, C, K, 3, 3, dtype=ops.BF16)
+    assert ops.conv2d_fwd_pool_ok(d)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
+    w32 = torch.randn(3, 3, C, K, device=dev, generator=g) / (9 * C) ** 0.5
+    wk = torch.zeros(ops.packed_shape(3, 3, C, K, ops.PACK_KRSC, C), dtype=torch.bfloat16, device=dev)
+    ops.pack_filter(w32, wk, C, K, ops.PACK_KRSC)
+    epi = ops.epilogue(bias=torch.randn(K, device=dev, generator=g) * 0.1, relu=True)
+    ws = ops.Workspace(dev)
+    ref = torch.empty(N, H, W, K, dtype=torch.bfloat16, device=dev)
+    ops.conv2d_fwd(d, x, wk, ref, epi, ws)
+    ops.set_option("halo_min_splits", 2)
+    try:
+        assert ops.conv_kernel_info(d, ops.OP_FWD)[1] >= 2
+        assert not ops.conv2d_fwd_pool_ok(d)
+        pooled = torch.full((N, H // 2, W // 2, K), 7.0, dtype=torch.bfloat16, device=dev)
+        with pytest.raises(RuntimeError):
+            ops.conv2d_fwd_pool(d, x, wk, pooled, None, epi, ws)
+        torch.cuda.synchronize()
+        assert bool((pooled == 7.0).all())          # nothing was written
+        y = torch.full_like(ref, float("nan"))
+        ops.conv2d_fwd(d, x, wk, y, epi, ws)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("halo_min_splits", 1)
+    err = (y.float() - ref.float()).abs().max().item()
+    assert err <= 1e-2 * ref.float().abs().max().item(), err

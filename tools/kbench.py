@@ -5,7 +5,9 @@ with HIP events, interleaved over option sets in ONE process (guide rule 24).
         [--opts 'nt2_ablate=0'] [--opts 'nt2_ablate=1'] [--reps 20] [--rounds 5]
 
 Option sets are applied in full before each use: give every set all the
-knobs it changes (e.g. 'x=0' beside 'x=1').
+knobs it changes (e.g. 'x=0' beside 'x=1').  Ablation knobs (*_abl,
+nt2_ablate: garbage results) exist only in the diagnostic library: build it
+with `_lib.build(diag=True)` and run with SEG_DIAG_LIB=1.
 
 Each spec is LAYER:OP (OP fwd | dgrad | wgrad | wgrad_adam).  Prints, per
 spec and option set, the median and min launch time (us) over rounds, the
