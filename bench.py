@@ -76,6 +76,9 @@ def parse():
                     help="do not fuse TF1 Adam into the conv6/conv7 filter-gradient epilogue")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="seg_set_option kernel knob (A/B runs; repeatable)")
+    ap.add_argument("--schedule", action="append", default=[], metavar="NAME=VALUE",
+                    help="Session schedule attribute for A/B runs (side_wgrad, main_wgrad, fused_delay, "
+                         "fuse_pool, fuse_grad_sum; repeatable)")
     ap.add_argument("--force-dp", action="store_true",
                     help="data-parallel Session over an RCCL ('nccl') process group even at world size 1 "
                          "(e.g. torchrun --nproc-per-node 1): the C4 per-rank step, all-reduces included")
@@ -381,6 +384,9 @@ WORKLOAD = {"fcn": "FCN (reference Network/model/FCN.py topology)",
                        "(semanticsegmentation_tensorflow_amd/deeplab.py; config C5)"}
 
 
+SCHEDULE = {}     # --schedule overrides, applied to every Session build_train_graph makes
+
+
 def build_train_graph(model, H, W, dtype, dp=None, fuse_adam=True, overlap_optimizer=False, fold_bn=True):
     """The benchmarked training graph and Session: `model`'s builder on a
     [None, HP, WP, 3] image placeholder (H x W zero-padded to multiples of
@@ -410,6 +416,10 @@ def build_train_graph(model, H, W, dtype, dp=None, fuse_adam=True, overlap_optim
     sess = tf.Session(compute_dtype=dtype, seed=0, data_parallel=dp, overlap_optimizer=overlap_optimizer,
                       fuse_adam=fuse_adam)
     sess.fold_bn = fold_bn
+    for k, v in SCHEDULE.items():
+        if not hasattr(sess, k):
+            raise ValueError(f"--schedule: no Session attribute {k!r}")
+        setattr(sess, k, v)
     sess.run(tf.global_variables_initializer())
     return {"sess": sess, "image": image, "labels": labels, "keep": keep, "pred": pred, "logits": logits,
             "loss": loss, "train_step": train_step, "HP": HP, "WP": WP}
@@ -577,19 +587,22 @@ def init_rccl(device):
 
 def dp_probe(args, B, H, W, kp, device):
     """The headline step re-timed through the data-parallel Session over a
-    world-1 RCCL process group (config C4's per-rank step: buckets all-reduced
-    over RCCL as backward produces them, Adam after the last bucket; the
-    wgrad+Adam epilogue fusion is off because the all-reduce sits between
-    gradient and update)."""
+    world-1 RCCL process group with the collectives forced on: config C4's
+    per-rank step minus the wire time -- every bucket reduce-scattered over
+    RCCL from the side stream as backward produces it, TF1 Adam on the rank's
+    slices (ZeRO-1), the all-gather of the updated parameters and the repack
+    of the compute copies (the conv6 / conv7 filter-gradient + Adam fusion is
+    off: a collective sits between gradient and update)."""
     import torch.distributed as dist
     from semanticsegmentation_tensorflow_amd.dp import DataParallel
     init_rccl(device)
-    dp = DataParallel(bucket_mb=args.bucket_mb)
+    dp = DataParallel(bucket_mb=args.bucket_mb, force_collectives=True)
     m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, 0)
     return {"backend": dist.get_backend(), "world": dist.get_world_size(), "bucket_mb": args.bucket_mb,
-            "buckets": len(dp.buckets), "value": round(m["value"], 3), "unit": "images/s",
-            "ms_per_step": round(m["ms_per_step"], 3),
-            "note": "same workload as the headline, every gradient bucket all-reduced over RCCL"}
+            "buckets": len(dp.buckets), "exchange": "zero1 (reduce-scatter, sharded Adam, all-gather)",
+            "value": round(m["value"], 3), "unit": "images/s", "ms_per_step": round(m["ms_per_step"], 3),
+            "note": "same workload as the headline; collectives forced on at world 1 (a real world-1 job "
+                    "skips them and runs the single-process plan)"}
 
 
 def main():
@@ -612,6 +625,9 @@ def main():
     for kv in args.option:
         name, val = kv.split("=")
         ops.set_option(name, int(val))
+    for kv in args.schedule:
+        name, val = kv.split("=")
+        SCHEDULE[name] = int(val)
     dH, dW, dB, dkp = DEFAULTS[args.model]
     if args.dtype is None:
         args.dtype = DEFAULT_DTYPE[args.model]

@@ -441,6 +441,13 @@ int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_ad
                       int nsegs, int total_tiles, float lr, float beta1, float beta2, float eps, int t,
                       float grad_scale, int dtype, void* stream);
 
+/* The packed compute copies of seg_adam_tf1_pack's segments rewritten from p
+ * alone (no update): the repack after a data-parallel step whose Adam ran on
+ * each rank's shard and whose parameters were then all-gathered (ZeRO-1).
+ * Replaces a seg_pack_filter per variable and layout. */
+int seg_pack_segments(const float* p, const seg_adam_segment* dev_segs, int nsegs, int total_tiles, int dtype,
+                      void* stream);
+
 /* Conv2DBackpropFilter fused with TF1 Adam (AdamOptimizer.minimize,
  * Network/model/FCN.py:338-340) on that filter, for single-process training
  * where nothing (no all-reduce) sits between the gradient and the update:

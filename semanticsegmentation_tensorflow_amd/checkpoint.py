@@ -87,6 +87,7 @@ class Saver:
 
     def save(self, sess, save_path, global_step=None):
         store = sess._ensure_store()
+        sess.sync_optimizer_slots()        # ZeRO-1 data parallelism: Adam slots gathered first
         gs = self._global_step_value(sess, global_step)
         path = save_path if gs is None else f"{save_path}-{gs}"
         out = {}

@@ -986,7 +986,11 @@ static int red_blocks(long P, int K, int epc) {
     const RedGeom g = red_geom(K, epc);
     const long per = 2L * g.rows;
     long b = (P + per - 1) / per;
-    if (b > RED_BLOCKS) b = RED_BLOCKS;
+    // the fp32 partial rows (blocks x K) are written and read back: for wide
+    // K cap them at ~4 MB (conv6 / conv7 BiasAddGrad, K = 4096: 936 blocks of
+    // 2 pixels each wrote 15 MB of partials for a 3.8 MB input)
+    const long cap = std::max(64L, std::min((long)RED_BLOCKS, (1L << 20) / K));
+    if (b > cap) b = cap;
     if (b < 1) b = 1;
     return (int)b;
 }

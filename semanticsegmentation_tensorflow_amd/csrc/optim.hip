@@ -14,6 +14,8 @@
 // the transposed one through an LDS tile so both stores stay coalesced.
 // Padding entries of the copies are never written (they keep the zeros of the
 // initial pack).  Elementwise arithmetic is identical to adam_k (eltwise.hip).
+// With G == null the same walk only rewrites the copies from P (no update):
+// the repack after a data-parallel all-gather of sharded Adam results.
 #include "common.h"
 
 namespace {
@@ -60,7 +62,14 @@ __device__ __forceinline__ void adam_pack_tile(float* __restrict__ P, const floa
         float pv[4] = {0.f, 0.f, 0.f, 0.f};
         if (a < sg.a && b < sg.b) {
             const long e = sg.offset + ((long)rs * sg.a + a) * sg.b + b;
-            if (vec) {   // b + 4 <= B since B % 4 == 0
+            if (!G) {    // pack only
+                if (vec) {
+                    const float4 pp = *reinterpret_cast<const float4*>(P + e);
+                    pv[0] = pp.x; pv[1] = pp.y; pv[2] = pp.z; pv[3] = pp.w;
+                } else {
+                    for (int j = 0; j < 4 && b + j < sg.b; ++j) pv[j] = P[e + j];
+                }
+            } else if (vec) {   // b + 4 <= B since B % 4 == 0
                 float4 pp = *reinterpret_cast<float4*>(P + e);
                 const float4 gg = *reinterpret_cast<const float4*>(G + e);
                 float4 mm = *reinterpret_cast<float4*>(Mm + e);
@@ -172,6 +181,27 @@ extern "C" int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs) {
         if (total > 0x7fffffff) return -SEG_EINVAL;
     }
     return (int)total;
+}
+
+extern "C" int seg_pack_segments(const float* p, const seg_adam_segment* dev_segs, int nsegs, int total_tiles,
+                                  int dtype, void* stream) {
+    if (!p || !dev_segs || nsegs <= 0 || total_tiles <= 0) return SEG_EINVAL;
+    if ((uintptr_t)p & 15) return SEG_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    float* P = const_cast<float*>(p);    // read only on this path
+    if (dtype == SEG_BF16)
+        hipLaunchKernelGGL(adam_pack_k<bf16>, dim3(total_tiles), dim3(256), 0, st, P, nullptr, nullptr, nullptr,
+                           dev_segs, nsegs, total_tiles, 0.f, 0.f, 0.f, 0.f, 0.f);
+    else if (dtype == SEG_F32)
+        hipLaunchKernelGGL(adam_pack_k<float>, dim3(total_tiles), dim3(256), 0, st, P, nullptr, nullptr, nullptr,
+                           dev_segs, nsegs, total_tiles, 0.f, 0.f, 0.f, 0.f, 0.f);
+    else if (dtype == SEG_F16)
+        hipLaunchKernelGGL(adam_pack_k<f16>, dim3(total_tiles), dim3(256), 0, st, P, nullptr, nullptr, nullptr,
+                           dev_segs, nsegs, total_tiles, 0.f, 0.f, 0.f, 0.f, 0.f);
+    else
+        return SEG_EINVAL;
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
 }
 
 extern "C" int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_adam_segment* dev_segs,

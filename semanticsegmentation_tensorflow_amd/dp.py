@@ -1,80 +1,101 @@
-"""Data-parallel gradient exchange: one process per GPU, RCCL all-reduce over
+"""Data-parallel gradient exchange: one process per GPU, RCCL collectives over
 xGMI through torch.distributed (backend "nccl" is RCCL on ROCm).
 
 The reference has no multi-device code; this is new.  The
 VariableStore keeps every gradient in one flat fp32 buffer laid out in the
 order backward produces them, so a bucket is a contiguous slice.  The Session
 calls `ready(var_names)` right after enqueueing each layer's filter-gradient
-kernel; when a bucket's last variable is in, its all-reduce is issued at once
--- ProcessGroupNCCL makes its stream wait on the compute stream up to that
-point, so the collective overlaps the remaining backward kernels.  `finish()`
-makes the compute stream wait for every bucket before Adam.  Gradients are
-summed; the Session folds 1/world into Adam's grad_scale (mean of per-shard
-means == the global-batch mean for equal shards).
+kernel; when a bucket's last variable is in, its collective is issued at once
+from the Session's side stream, so it overlaps the remaining backward kernels.
+Gradients are summed; the Session folds 1/world into Adam's grad_scale (mean
+of per-shard means == the global-batch mean for equal shards).
+
+Two exchange modes per step:
+
+* "zero" (ZeRO-1, the default for an Adam step at world > 1): each bucket is
+  reduce-SCATTERED -- rank r receives the summed slice r of every bucket --
+  TF1 Adam runs on those slices only (1/world of the parameters: per-rank
+  Adam HBM traffic 28 B/param / world), and the updated fp32 slices are
+  all-gathered back in place before the packed bf16 compute copies are
+  rewritten from the full parameters (Session._zero_update).  Wire bytes equal
+  an all-reduce's (a reduce-scatter + an all-gather); the m / v slots outside
+  a rank's slices are stale until `gather_slots` (checkpoints).
+* "allreduce": every bucket all-reduced, Adam everywhere (the accumulate
+  template's steps, which read the whole gradient, and the overlapped
+  per-layer optimizer).
+
+At world 1 every collective is the identity and none is issued (`active`
+False) -- the Session then runs its single-process plan, fused conv6 / conv7
+filter-gradient + Adam included -- unless `force_collectives` (tests, and the
+bench probe that times the world > 1 per-rank path on one GPU).
 """
 from __future__ import annotations
 
+import torch
 import torch.distributed as dist
 
 
 class DataParallel:
-    def __init__(self, bucket_mb: float = 64.0, group=None):
+    def __init__(self, bucket_mb: float = 64.0, group=None, shard_optimizer: bool = True,
+                 force_collectives: bool = False):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed must be initialised (one process per GPU)")
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.active = self.world > 1 or force_collectives
+        self.shard = shard_optimizer
+        self.backend = dist.get_backend(group)
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.buckets = []
         self.var_bucket = {}
         self.var_buckets = {}
         self.store = None
+        self.mode = "allreduce"       # per step, set by the Session: "zero" or "allreduce"
+        self.slots_stale = False      # m / v outside this rank's slices not gathered since a zero step
         # optional hook (works, var_names) called as each bucket's all-reduce
         # is issued, with the variables whose last piece it carries and the
         # collectives covering them: the Session runs their Adam update on a
-        # side stream once those complete
+        # side stream once those complete (allreduce mode)
         self.on_launch = None
         # (side, compute) streams while the Session defers split-K filter-
-        # gradient reductions to the side stream: a bucket's all-reduce is
+        # gradient reductions to the side stream: a bucket's collective is
         # then issued from the side stream after it has caught up with the
         # compute stream, so it waits for both the kernels enqueued on the
         # compute stream and the deferred reductions -- without the compute
         # stream ever waiting on the side stream
         self.launch_streams = None
 
+    # ------------------------------------------------------------ buckets
     def prepare(self, store):
         """Cut the flat gradient buffer into contiguous buckets of at most
-        bucket_bytes (backward order).  A variable larger than a bucket is
-        chunked (conv6's 411 MB filter gradient -> 64 MB all-reduces), so its
-        first bytes leave while the rest are still queued; a bucket is ready
-        once every variable with a piece in it is."""
+        bucket_bytes (backward order), each a multiple of 4 * world elements
+        long so it splits into world 16-byte-aligned slices (the last one
+        reaches into the store's zero tail slack).  A variable larger than a
+        bucket is chunked (conv6's 411 MB filter gradient -> 64 MB pieces), so
+        its first bytes leave while the rest are still queued; a bucket is
+        ready once every variable with a piece in it is."""
         if self.store is store and self.buckets:
             return
         self.store = store
-        cap = max(1, self.bucket_bytes // 4)              # fp32 elements per bucket
-        spans = []                                        # (name, start, end) in backward order
+        align = 4 * self.world
+        if store.numel + align > store.alloc:
+            raise ValueError(f"world {self.world}: the store's tail slack ({store.alloc - store.numel}) "
+                             f"cannot pad buckets to multiples of {align}")
+        cap = max(align, self.bucket_bytes // 4 // align * align)     # fp32 elements per bucket
+        spans = []                                                    # (name, start, end) in backward order
         order = list(store.order)
         for i, v in enumerate(order):
             s0 = store.offset[v.var_name]
             e0 = store.offset[order[i + 1].var_name] if i + 1 < len(order) else store.numel
             spans.append((v.var_name, s0, e0))
-        self.buckets = []                                 # (start, end, [names with a piece here])
-        cur, start, fill = [], None, 0
-        for name, s0, e0 in spans:
-            pos = s0
-            while pos < e0:
-                if start is None:
-                    start = pos
-                take = min(e0 - pos, cap - fill)
-                if not cur or cur[-1] != name:
-                    cur.append(name)
-                pos += take
-                fill += take
-                if fill >= cap:
-                    self.buckets.append((start, pos, cur))
-                    cur, start, fill = [], None, 0
-        if cur:
-            self.buckets.append((start, store.numel, cur))
+        self.buckets = []                                             # (start, end, [names with a piece here])
+        start = 0
+        while start < store.numel:
+            end = min(start + cap, (store.numel + align - 1) // align * align)
+            names = [nm for nm, s0, e0 in spans if s0 < end and e0 > start]
+            self.buckets.append((start, end, names))
+            start = end
         self.var_buckets = {}
         for i, (_, _, names) in enumerate(self.buckets):
             for nm in names:
@@ -82,28 +103,58 @@ class DataParallel:
         self.var_bucket = {nm: b[-1] for nm, b in self.var_buckets.items()}   # bucket holding its last piece
         self._reset()
 
+    def slice_of(self, i, rank=None):
+        """[a, b) of bucket i owned by `rank` (default: this rank) in zero mode."""
+        s, e, _ = self.buckets[i]
+        c = (e - s) // self.world
+        r = self.rank if rank is None else rank
+        return s + r * c, s + (r + 1) * c
+
+    def owned_ranges(self):
+        """This rank's slices of the flat buffer (zero mode), clipped to the
+        variables' extent."""
+        out = []
+        for i in range(len(self.buckets)):
+            a, b = self.slice_of(i)
+            b = min(b, self.store.numel)
+            if b > a:
+                out.append((a, b))
+        return out
+
     def _reset(self):
         self.remaining = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
         self.bucket_work = [None] * len(self.buckets)
 
+    # --------------------------------------------------------- collectives
+    def _reduce(self, i):
+        s, e, _ = self.buckets[i]
+        g = self.store.grads
+        if self.mode == "zero":
+            a, b = self.slice_of(i)
+            if self.backend == "gloo":
+                # gloo has no reduce-scatter: the all-reduce leaves the same
+                # sums in this rank's slice (the rest is not read)
+                return dist.all_reduce(g[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            # in place: the output is this rank's slice of the input (RCCL in-place form)
+            return dist.reduce_scatter_tensor(g[a:b], g[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True)
+        return dist.all_reduce(g[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
     def _launch(self, i):
         s, e, names = self.buckets[i]
         w = None
         if e > s:
             if self.launch_streams is not None:
-                import torch
                 side, main = self.launch_streams
                 ev = torch.cuda.Event()
                 ev.record(main)
                 side.wait_event(ev)
                 with torch.cuda.stream(side):
-                    w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                        async_op=True)
+                    w = self._reduce(i)
             else:
-                w = dist.all_reduce(self.store.grads[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                    async_op=True)
+                w = self._reduce(i)
             self.works.append(w)
         self.bucket_work[i] = w
         self.launched[i] = True
@@ -136,4 +187,31 @@ class DataParallel:
                 self._launch(i)
         for w in self.works:
             w.wait()
+        if self.mode == "zero":
+            self.slots_stale = True
         self._reset()
+
+    def _gather(self, buf):
+        """All-gather every bucket's slices of `buf` in place (zero mode)."""
+        works = []
+        for i, (s, e, _) in enumerate(self.buckets):
+            a, b = self.slice_of(i)
+            if self.backend == "gloo":
+                c = b - a
+                outs = list(buf[s:e].view(self.world, c).unbind(0))
+                works.append(dist.all_gather(outs, buf[a:b].clone(), group=self.group, async_op=True))
+            else:
+                works.append(dist.all_gather_into_tensor(buf[s:e], buf[a:b], group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+
+    def gather_params(self):
+        """Every rank's updated parameter slices into every rank's flat buffer."""
+        self._gather(self.store.params)
+
+    def gather_slots(self):
+        """The Adam m / v slices likewise (before a checkpoint reads them)."""
+        if self.slots_stale:
+            self._gather(self.store.m)
+            self._gather(self.store.v)
+            self.slots_stale = False

@@ -684,6 +684,12 @@ def adam_tf1_pack(p, g, m, v, plan, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, gra
                                        int(t), float(grad_scale), int(dtype), stream_ptr(stream)), "adam_pack")
 
 
+def pack_segments(p, plan, dtype=BF16, stream=None):
+    """Rewrite every planned variable's packed compute copies from p (no update)."""
+    check(_lib.lib().seg_pack_segments(ptr(p), ptr(plan.table), plan.nsegs, plan.total_tiles, int(dtype),
+                                       stream_ptr(stream)), "pack_segments")
+
+
 def cast(x, y, stream=None):
     """Elementwise dtype conversion x -> y (same number of elements)."""
     assert x.numel() == y.numel()

@@ -22,7 +22,6 @@ from __future__ import annotations
 
 import collections
 import contextlib
-import os
 
 import numpy as np
 import torch
@@ -196,26 +195,29 @@ class Session:
         # BatchNorm(+ReLU) feeding a single 1x1 conv folded into its operand prologue
         self.fold_bn = True
         self.fold_dropout_grad = True   # Conv -> Dropout -> BN: the dropout gradient inside the BN backward
+        # Schedule attributes (measured defaults; every value is exercised by
+        # tests/test_gpu_dp_rccl.py against the default schedule -- bench.py
+        # --schedule NAME=VALUE sets them for A/B runs):
         # a tensor's later input-gradient contributions accumulate in the epilogue
-        self.fuse_grad_sum = os.environ.get("SEG_FUSE_GRAD_SUM", "1") != "0"
+        self.fuse_grad_sum = True
         self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
         # conv (+bias +ReLU) -> 2x2 MaxPool as one launch (pooled epilogue)
-        self.fuse_pool = os.environ.get("SEG_FUSE_POOL", "1") != "0"
+        self.fuse_pool = True
         self._red = None                 # (side stream, compute stream) during a step
         # deferred filter gradients: the kernel too (not only its reduction) on
         # the side stream (1), and the fused filter-gradient + Adam launches (2)
-        self.side_wgrad = int(os.environ.get("SEG_SIDE_WGRAD", "2"))
+        self.side_wgrad = 2
         # the fused conv6 / conv7 filter-gradient + Adam launches go to the side
         # stream after the next `fused_delay` filter gradients there (the
         # HBM-bound update then overlaps the smaller conv4_x / conv3_x layers
         # instead of starving conv5_x's input gradients: 547 -> 554 img/s at 5-7)
-        self.fused_delay = int(os.environ.get("SEG_FUSED_DELAY", "6"))
+        self.fused_delay = 6
         self._pending_fused = []
         # the filter gradients of the first `main_wgrad` convs (the last in the
         # backward: conv1_1 / conv1_2 in FCN) stay on the compute stream, which
         # has no input gradient left to run then, beside the side stream's
         # remaining filter gradients instead of after them
-        self.main_wgrad = int(os.environ.get("SEG_MAIN_WGRAD", "2"))
+        self.main_wgrad = 2
 
         self._side = None
         self._adam_ctx = None
@@ -928,8 +930,52 @@ class Session:
         p.never_ready = [v.var_name for v in self.store.order
                          if v.var_name not in p.var_set or v.var_name not in covered]
         # data parallel bucket schedule (var readiness in backward order)
-        if self.dp is not None:
+        if self._dpa is not None:
             self.dp.prepare(self.store)
+
+    @property
+    def _dpa(self):
+        """The DataParallel whose collectives run (None: single process, or
+        world 1 where every collective is the identity)."""
+        return self.dp if (self.dp is not None and self.dp.active) else None
+
+    def sync_optimizer_slots(self):
+        """After ZeRO-1 steps each rank's Adam m / v are current on its own
+        slices only: gather them (checkpoints, tests)."""
+        if self._dpa is not None and self.store is not None and self.dp.store is self.store:
+            self.dp.gather_slots()
+
+    def _zero_update(self, p, opt, gs):
+        """ZeRO-1 (dp.py): TF1 Adam on this rank's reduce-scattered slices of
+        the variables being trained, the updated fp32 slices all-gathered in
+        place, then every packed compute copy rewritten from the full
+        parameters in one launch (seg_pack_segments)."""
+        store = self.store
+        key = ("zero", tuple(p.adam_names), len(store.packed))
+        ranges = self._adam_groups.get(key)
+        if ranges is None:
+            spans = sorted((store.offset[nm], store.offset[nm] + int(np.prod(store.by_name[nm].shape)))
+                           for nm in p.adam_names)
+            starts = sorted(store.offset.values())
+            ranges = []
+            for a, b in self.dp.owned_ranges():
+                for s0, e0 in spans:
+                    lo, hi = max(a, s0), min(b, e0)
+                    if lo >= hi:
+                        continue
+                    # merge over a gap that is only 16-byte alignment padding
+                    # (zeros, which Adam leaves zero) -- never over a variable
+                    # outside var_list
+                    if ranges and lo - ranges[-1][1] <= 3 and not any(ranges[-1][1] <= o < lo for o in starts):
+                        ranges[-1] = (ranges[-1][0], hi)
+                    else:
+                        ranges.append((lo, hi))
+            self._adam_groups[key] = ranges
+        for a, b in ranges:
+            ops.adam_tf1_step(store.params[a:b], store.grads[a:b], store.m[a:b], store.v[a:b], opt.lr, store.step,
+                              opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs)
+        self.dp.gather_params()
+        ops.pack_segments(store.params, self._adam_plan(p.adam_names), dtype=self._pack_dtype())
 
     # -------------------------------------------------------------- execute
     def _repack(self, p):
@@ -1121,7 +1167,8 @@ class Session:
         if p.train:
             ts = p.train.attrs
             opt = ts["optimizer"]
-            world = self.dp.world if self.dp is not None else 1
+            dpa = self._dpa
+            world = dpa.world if dpa is not None else 1
             S = self.loss_scale                     # the scale this step's loss gradient carries
             scaled = S != 1.0
             gs = ts["grad_scale"] / world / S
@@ -1130,9 +1177,15 @@ class Session:
             if opt is not None:
                 store.step += 1
             self._fused = None
-            if opt is not None and self.fuse_adam and self.dp is None and not self.overlap_optimizer \
+            if opt is not None and self.fuse_adam and dpa is None and not self.overlap_optimizer \
                     and not scaled and p.adam_fusable:
                 self._fused = (opt, gs, set())
+            # ZeRO-1 exchange for an Adam step (dp.py); the accumulate template
+            # and the overlapped per-layer optimizer read whole gradients
+            zero = (dpa is not None and dpa.shard and opt is not None and not self.overlap_optimizer
+                    and not p.train.accum)
+            if dpa is not None:
+                dpa.mode = "zero" if zero else "allreduce"
             self._red = None
             if self.defer_wgrad_reduce and self.device.type == "cuda":
                 # (with the overlapped optimizer the reductions and each layer's
@@ -1140,15 +1193,15 @@ class Session:
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self.device)
                 self._red = (self._side, torch.cuda.current_stream(self.device))
-                if self.dp is not None:
-                    self.dp.launch_streams = self._red
+                if dpa is not None:
+                    dpa.launch_streams = self._red
             if opt is not None and self.overlap_optimizer and self.device.type == "cuda":
                 # per-layer Adam on a side stream as soon as the layer's gradient is final
                 self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set)
-                if self.dp is not None:
-                    self.dp.on_launch = self._adam_ctx.after_work
-            if self.dp is not None and p.never_ready:
-                self.dp.ready(p.never_ready)
+                if dpa is not None:
+                    dpa.on_launch = self._adam_ctx.after_work
+            if dpa is not None and p.never_ready:
+                dpa.ready(p.never_ready)
             self._ready_filter = p.var_set
             ok = False
             try:
@@ -1167,13 +1220,13 @@ class Session:
                 if self._red is not None:        # pending filter-gradient reductions done before Adam
                     self._red[1].wait_stream(self._red[0])
                     self._red = None
-                if self.dp is not None:
+                if dpa is not None:
                     if ok:
-                        self.dp.finish()
+                        dpa.finish()
                     else:
-                        self.dp.abort_step()
-                    self.dp.on_launch = None
-                    self.dp.launch_streams = None
+                        dpa.abort_step()
+                    dpa.on_launch = None
+                    dpa.launch_streams = None
             if scaled and not self._grads_finite():
                 # overflow in the scaled fp16 gradients: no update this step
                 # (TF LossScaleOptimizer), halve the scale
@@ -1199,6 +1252,8 @@ class Session:
             elif self._adam_ctx is not None:
                 self._adam_ctx.finish()
                 self._adam_ctx = None
+            elif zero:
+                self._zero_update(p, opt, gs)
             else:
                 done = self._fused[2] if self._fused is not None else set()
                 rest = [nm for nm in p.adam_names if nm not in done]
@@ -1288,7 +1343,7 @@ class Session:
         optimizer."""
         if self._ready_filter is not None:
             names = [nm for nm in names if nm in self._ready_filter]
-        if self.dp is not None:
+        if self._dpa is not None:
             self.dp.ready(names)
         elif self._adam_ctx is not None:
             self._adam_ctx.launch(names)
@@ -1439,6 +1494,7 @@ class Session:
                     self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
                 dx = None
                 dx_base = None
+                bnb = None          # tests: record of a BatchNorm backward run in this conv's dgrad epilogue
                 pro = getattr(n, "pro", None)
                 if (id(x) in ng and pro is not None and self.fuse_bn_bwd and id(pro.inputs[0]) in ng
                         and ops.conv_bwd_data_bn_workspace(n.desc) > 0):
@@ -1452,9 +1508,15 @@ class Session:
                     else:
                         (dxb, acc), accf = dest(xb), False
                     gn, bn_ = pro.gamma.var_name, pro.beta.var_name
+                    if self.capture is not None:
+                        bnb = {"xb": buf[id(xb)], "gamma": gn, "beta": bn_, "eps": pro.eps, "relu": pro.relu,
+                               "base": dxb.clone() if accf else None, "drop": None, "folded": True}
                     self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
                                 store.param(bn_), dxb, gdst(gn), gdst(bn_), pro.eps, pro.relu, accf, ws)
+                    if bnb is not None:
+                        bnb["dxb"] = dxb.clone()
+                        bnb["kernel"] = ops.conv_kernel_info(n.desc, ops.OP_BWD_DATA_BN)[0]
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
                 elif (id(x) in ng and id(n) in p.bn_before and self.fuse_bn_bwd
@@ -1474,6 +1536,10 @@ class Session:
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
                                 store.param(bn_), dxb, gdst(gn), gdst(bn_), b.eps, b.relu, False, ws,
                                 None, drop)
+                    if self.capture is not None:
+                        bnb = {"xb": buf[id(xb)], "gamma": gn, "beta": bn_, "eps": b.eps, "relu": b.relu,
+                               "base": None, "drop": drop, "folded": False, "dxb": dxb.clone(),
+                               "kernel": ops.conv_kernel_info(n.desc, ops.OP_BWD_DATA_BN)[0]}
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
                 elif id(x) in ng:
@@ -1515,6 +1581,9 @@ class Session:
                                          "dx_masked": mask is not None,
                                          "mask_scale": (mask.mask_scale if mask is not None else 1.0),
                                          "relu": n.relu, "keep_prob": n.kp_val, "seed": n.seed_val,
+                                         # input gradient through a BatchNorm(+ReLU) backward in
+                                         # the dgrad epilogue (igemm_nt2_bn / conv_res16c_bn)
+                                         "bn_bwd": bnb,
                                          "fused_adam": False, "desc": n.desc,
                                          "stride": n.stride, "dilation": n.dilation, "padding": n.padding})
                 want_w = n.w.var_name in p.var_set
@@ -1722,7 +1791,7 @@ class Session:
         if self._finite_flag is None:
             self._finite_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         ops.check_finite(self.store.grads, self._finite_flag)
-        if self.dp is not None:
+        if self._dpa is not None:
             import torch.distributed as dist
             dist.all_reduce(self._finite_flag, op=dist.ReduceOp.MAX, group=self.dp.group)
         return int(self._finite_flag.item()) == 0

@@ -43,6 +43,9 @@ def _aux_dtype(var):
     return torch.int64 if getattr(var, "dtype", None) == G.int64 else torch.float32
 
 
+TAIL_SLACK = 1024
+
+
 class VariableStore:
     """Trainable variables in the flat buffers (`vars`, backward order);
     non-trainable ones (the accumulate template's gradient accumulators,
@@ -63,10 +66,13 @@ class VariableStore:
             n = int(np.prod(v.shape))
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
-        self.params = torch.zeros(off, dtype=torch.float32, device=device)
-        self.grads = torch.zeros(off, dtype=torch.float32, device=device)
-        self.m = torch.zeros(off, dtype=torch.float32, device=device)
-        self.v = torch.zeros(off, dtype=torch.float32, device=device)
+        # zero tail slack: data-parallel buckets are padded to multiples of
+        # 4 * world elements (dp.py), world <= TAIL_SLACK / 4
+        self.alloc = off + TAIL_SLACK
+        self.params = torch.zeros(self.alloc, dtype=torch.float32, device=device)
+        self.grads = torch.zeros(self.alloc, dtype=torch.float32, device=device)
+        self.m = torch.zeros(self.alloc, dtype=torch.float32, device=device)
+        self.v = torch.zeros(self.alloc, dtype=torch.float32, device=device)
         self.by_name = {v.var_name: v for v in self.vars}
         self.aux_by_name = {v.var_name: v for v in self.aux_vars}
         # int64 non-trainables (global_step) stay int64, as TF keeps them: an
@@ -104,7 +110,7 @@ class VariableStore:
         return self._view(self.v, name)
 
     def initialize(self):
-        host = np.zeros(self.numel, dtype=np.float32)
+        host = np.zeros(self.alloc, dtype=np.float32)
         for v in self.vars:
             n = int(np.prod(v.shape))
             o = self.offset[v.var_name]

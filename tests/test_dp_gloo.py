@@ -1,8 +1,11 @@
 """Data-parallel path on CPU: world size 2 over gloo (127.0.0.1).
 
-Checks dp.DataParallel's bucketing / in-order async all-reduce on a store
-shaped like the Session's, and the DP identity the bench relies on: the
-mean of per-shard mean-loss gradients equals the full-batch gradient."""
+Checks dp.DataParallel's bucketing / in-order async collectives on a store
+shaped like the Session's, the DP identity the bench relies on -- the mean
+of per-shard mean-loss gradients equals the full-batch gradient -- and the
+ZeRO-1 exchange: each rank's reduced slices, TF1 Adam on those slices only,
+the all-gather of the updated parameters (and, for checkpoints, of m / v)
+reproducing a single-process Adam step on the full-batch gradient."""
 import os
 import socket
 
@@ -32,7 +35,11 @@ class FakeStore:
             self.offset[v.var_name] = off
             off += (int(np.prod(v.shape)) + 3) // 4 * 4
         self.numel = off
-        self.grads = torch.zeros(off, dtype=torch.float32)
+        self.alloc = off + 1024
+        self.grads = torch.zeros(self.alloc, dtype=torch.float32)
+        self.params = torch.zeros(self.alloc, dtype=torch.float32)
+        self.m = torch.zeros(self.alloc, dtype=torch.float32)
+        self.v = torch.zeros(self.alloc, dtype=torch.float32)
 
     def grad(self, name):
         v = next(x for x in self.vars if x.var_name == name)
@@ -76,7 +83,8 @@ def _worker(rank, world, port, q):
         assert len(dp.var_buckets["c2/weights"]) >= 2             # chunked across buckets
         # contiguous, disjoint, cover the whole buffer
         spans = sorted((s, e) for s, e, _ in dp.buckets)
-        assert spans[0][0] == 0 and spans[-1][1] == store.numel
+        assert spans[0][0] == 0 and store.numel <= spans[-1][1] < store.numel + 4 * world
+        assert all((e - s) % (4 * world) == 0 for s, e in spans)
         assert all(spans[i][1] == spans[i + 1][0] for i in range(len(spans) - 1))
         for v in store.order:                        # backward order, as the Session does
             store.grad(v.var_name).copy_(g[v.var_name])
@@ -86,6 +94,82 @@ def _worker(rank, world, port, q):
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+def _adam_np(p, g, m, v, t, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
+    """TF1 Adam, float32 as the device computes it."""
+    lr_t = lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    m = (b1 * m + (1 - b1) * g).astype(np.float32)
+    v = (b2 * v + (1 - b2) * g * g).astype(np.float32)
+    return (p - lr_t * m / (np.sqrt(v) + eps)).astype(np.float32), m, v
+
+
+def _zero_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(0)
+        weights = {k: (rng.standard_normal(s) * 0.3).astype(np.float32) for k, s in SHAPES.items()}
+        x = rng.standard_normal((4, 8, 12, 3))
+        lab = rng.integers(0, 2, (4, 8, 12))
+        part = slice(rank * 2, rank * 2 + 2)
+        g = grads_of(weights, x[part], lab[part])
+        store = FakeStore(SHAPES)
+        for k, w in weights.items():
+            o = store.offset[k]
+            store.params[o:o + w.size] = torch.from_numpy(w.reshape(-1))
+        dp = DataParallel(bucket_mb=0.002)
+        dp.prepare(store)
+        dp.mode = "zero"
+        for v in store.order:
+            store.grad(v.var_name).copy_(g[v.var_name])
+            dp.ready([v.var_name])
+        dp.finish()
+        assert dp.slots_stale
+        owned = dp.owned_ranges()
+        assert sum(b - a for a, b in owned) <= store.numel // world + 4 * len(dp.buckets)
+        # Adam on this rank's reduced slices only (grad scale 1/world)
+        for a, b in owned:
+            p, m, v = _adam_np(store.params[a:b].numpy(), store.grads[a:b].numpy() / world,
+                               store.m[a:b].numpy(), store.v[a:b].numpy(), 1)
+            store.params[a:b] = torch.from_numpy(p)
+            store.m[a:b] = torch.from_numpy(m)
+            store.v[a:b] = torch.from_numpy(v)
+        dp.gather_params()
+        dp.gather_slots()
+        assert not dp.slots_stale
+        out = {}
+        for k in SHAPES:
+            o, n = store.offset[k], int(np.prod(SHAPES[k]))
+            out[k] = tuple(t[o:o + n].numpy().copy() for t in (store.params, store.m, store.v))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_world2_zero1_sharded_adam():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(0)
+    weights = {k: (rng.standard_normal(s) * 0.3).astype(np.float32) for k, s in SHAPES.items()}
+    x = rng.standard_normal((4, 8, 12, 3))
+    lab = rng.integers(0, 2, (4, 8, 12))
+    full = grads_of(weights, x, lab)
+    for k in SHAPES:
+        for i in range(3):
+            assert np.array_equal(res[0][k][i], res[1][k][i]), (k, i)            # ranks agree bitwise
+        p, m, v = _adam_np(weights[k].reshape(-1), full[k].numpy().reshape(-1), 0.0, 0.0, 1)
+        np.testing.assert_allclose(res[0][k][1], m, rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(res[0][k][2], v, rtol=1e-4, atol=1e-14)
+        np.testing.assert_allclose(res[0][k][0], p, rtol=0, atol=1e-6)
 
 
 def _free_port():

@@ -22,7 +22,7 @@ from oracle import models as M
 from semanticsegmentation_tensorflow_amd import tf
 from tests.model_inputs import he_weights, synthetic_batch
 from tests.test_gpu_fcn import build_fcn
-from tests.workers.dp_session_worker import CASES, H, N_GLOBAL, W
+from tests.workers.dp_session_worker import CASES, H, N_GLOBAL, W, case_tag
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -47,7 +47,9 @@ def _single(dtype):
         sess.assign(k, v)
     sess.run(train_step, feed_dict={image: img, labels: lab, keep: 1.0})
     return ({k: sess.store.grad(k).cpu().numpy() for k in weights},
-            {k: sess.variable_value(k) for k in weights})
+            {k: sess.variable_value(k) for k in weights},
+            {k: sess.store.adam_m(k).cpu().numpy() for k in weights},
+            {k: sess.store.adam_v(k).cpu().numpy() for k in weights})
 
 
 def test_session_dp_world2_matches_single_process(dev, tmp_path):
@@ -68,20 +70,23 @@ def test_session_dp_world2_matches_single_process(dev, tmp_path):
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
     ref = {}
-    for dtype, overlap in CASES:
+    for case in CASES:
+        dtype, overlap, shard = case
         if dtype not in ref:
             ref[dtype] = _single(dtype)
-        g_ref, p_ref = ref[dtype]
-        r = [dict(np.load(os.path.join(tmp_path, f"rank{i}_{dtype}_{int(overlap)}.npz"))) for i in range(2)]
+        g_ref, p_ref, m_ref, v_ref = ref[dtype]
+        r = [dict(np.load(os.path.join(tmp_path, f"rank{i}_{case_tag(*case)}.npz"))) for i in range(2)]
         assert int(r[0]["buckets"]) >= 3
         for k in g_ref:
-            assert np.array_equal(r[0]["g:" + k], r[1]["g:" + k]), (dtype, overlap, k)
-            assert np.array_equal(r[0]["p:" + k], r[1]["p:" + k]), (dtype, overlap, k)
+            for q in ("g:", "p:", "m:", "v:"):
+                assert np.array_equal(r[0][q + k], r[1][q + k]), (case, q, k)
             g = r[0]["g:" + k] / 2.0
             if dtype == "f32":
-                assert np.abs(g - g_ref[k]).max() <= 1e-5 * max(np.abs(g_ref[k]).max(), 1e-30), (overlap, k)
+                assert np.abs(g - g_ref[k]).max() <= 1e-5 * max(np.abs(g_ref[k]).max(), 1e-30), (case, k)
                 pr = p_ref[k]
-                assert np.abs(r[0]["p:" + k] - pr).max() <= 1e-6 + 1e-5 * np.abs(pr).max(), (overlap, k)
+                assert np.abs(r[0]["p:" + k] - pr).max() <= 1e-6 + 1e-5 * np.abs(pr).max(), (case, k)
+                np.testing.assert_allclose(r[0]["m:" + k], m_ref[k], rtol=1e-4, atol=1e-5 * np.abs(m_ref[k]).max())
+                np.testing.assert_allclose(r[0]["v:" + k], v_ref[k], rtol=1e-3, atol=1e-5 * np.abs(v_ref[k]).max())
             else:
                 rel = np.linalg.norm(g - g_ref[k]) / max(np.linalg.norm(g_ref[k]), 1e-30)
                 assert rel <= 2e-2, (k, rel)

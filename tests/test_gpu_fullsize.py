@@ -113,13 +113,14 @@ def _bench_step(model, H, W, N, weights, seed):
             "loss": float(lo), "kernels": names, "kp": kp, "dtype": dtype, "H": H, "W": W}
 
 
-def _uniform(seed, shape, n_images=None):
+def _uniform(seed, shape, n_images=None, image=0):
     """The device's dropout uniforms for a [N, H, W, C] tensor (flat
-    element index), optionally for the first n_images images only."""
+    element index), optionally for `n_images` images starting at `image`."""
     shape = tuple(shape)
+    per = int(np.prod(shape[1:]))
     if n_images is not None:
         shape = (n_images,) + shape[1:]
-    idx = np.arange(int(np.prod(shape)), dtype=np.uint64)
+    idx = np.arange(image * per, image * per + int(np.prod(shape)), dtype=np.uint64)
     return torch.from_numpy(_np_uniform_vec(seed, idx).reshape(shape))
 
 
@@ -209,12 +210,57 @@ def _layer_local(rec, w, b, sess, weights=None, rtol=4e-3, quant=bf16r, images=N
             res["dgrad"] = (dxd - want).abs() - (rtol * want.abs() + 1e-3 * dx.abs().max())
         else:
             res["dgrad"] = (dxd - dx).abs() - (rtol * dx.abs() + 1e-3 * dx.abs().max())
+    bb = rec.get("bn_bwd")
+    if dgrad and bb is not None:
+        res.update(_bn_bwd_local(bb, xg.grad, sess, weights, rtol))
     gw = _dev_grad(sess, rec["name"], rec["fused_adam"])
     res["wgrad"] = (gw - wg.grad.double()).abs() - 1e-3 * wg.grad.abs().max()
     if rec["bias"] is not None:
         db = dz.sum(dim=(0, 1, 2))
         res["bgrad"] = (sess.store.grad(rec["bias"]).cpu() - db).abs() - 1e-3 * db.abs().max()
     return {k: float(v.max()) for k, v in res.items()}
+
+
+def _bn_bwd_local(bb, dr, sess, weights, rtol):
+    """The BatchNorm(+ReLU) backward a conv's input-gradient launch ran in its
+    epilogue (igemm_nt2_bn: the BN folded into a 1x1 conv's prologue, its
+    gradient accumulated in place into the shared concat gradient;
+    conv_res16c_bn: the growth conv's input gradient through the BN before it
+    and the dropout of the conv before that), from dr = the oracle's gradient
+    of the conv input relu(BN(xb)) (Network/model/FCDenseNet.py:25-34,
+    Network/utils/utils.py:300-301):
+        a = xb * gamma / sqrt(1 + eps) + beta,  da = dr * [a > 0]
+        dxb = da * gamma / sqrt(1 + eps) (* floor(kp + u) / kp),
+        dgamma = sum(da * xb) / sqrt(1 + eps),  dbeta = sum(da).
+    Elements whose BN output is within 1e-5 of max |a| of zero (a ReLU
+    decision one fp32 rounding can flip) are left out of the elementwise
+    check (counted: at most 1e-5 of them); the sums include them."""
+    gname, bname = bb["gamma"], bb["beta"]
+    gamma = torch.from_numpy(weights[gname]).double()
+    beta = torch.from_numpy(weights[bname]).double()
+    Cb = gamma.shape[0]
+    xb = _host(bb["xb"], Cb).double()
+    inv = 1.0 / math.sqrt(1.0 + bb["eps"])
+    a = xb * (gamma * inv) + beta
+    dr = dr.double()[..., :Cb]
+    da = dr * (a > 0) if bb["relu"] else dr
+    want = da * (gamma * inv)
+    if bb["drop"] is not None:
+        kp, seed = bb["drop"]
+        want = T.dropout(want, kp, _uniform(seed, want.shape).double())
+    scale = want.abs().max()
+    if bb["base"] is not None:
+        want = want + _host(bb["base"], Cb).double()
+    got = _host(bb["dxb"], Cb).double()
+    amb = (a.abs() <= 1e-5 * a.abs().max()) if bb["relu"] else torch.zeros_like(a, dtype=torch.bool)
+    err = ((got - want).abs() - (rtol * want.abs() + 1e-3 * scale)).masked_fill(amb, -1.0)
+    dg = (da * xb).sum(dim=(0, 1, 2)) * inv
+    db = da.sum(dim=(0, 1, 2))
+    gg = sess.store.grad(gname).cpu().double()
+    gb = sess.store.grad(bname).cpu().double()
+    return {"bn_dx": err.max(), "bn_ambiguous": amb.double().mean() - 1e-5,
+            "dgamma": ((gg - dg).abs() - 1e-3 * dg.abs().max()).max(),
+            "dbeta": ((gb - db).abs() - 1e-3 * db.abs().max()).max()}
 
 
 def _grad_stats(sess, ref_grads, fused=()):
@@ -306,6 +352,7 @@ def test_c2_end_to_end_vs_oracle(c2):
     for cos, l2, k in sorted(stats):
         print(f"GRAD {k:20s} cos={cos:.5f} relL2={l2:.3e}")
     assert min(s[0] for s in stats) >= 0.95
+    assert max(s[1] for s in stats) <= C2_WORST_REL_L2, max(stats, key=lambda s: s[1])
     assert np.median([s[1] for s in stats]) <= 0.1
 
 
@@ -353,17 +400,36 @@ def test_c3_kernel_set_and_concat_views(c3):
         assert any(n.startswith(fam) for n in names), (fam, names)
 
 
-@pytest.mark.timeout(600)
+def _c3_sample(recs):
+    """Dense blocks 1 and 6, their transitions, the stem and the head, plus
+    the middle block's first layers: every kind of input-gradient launch the
+    C3 step runs (plain, in place into a concat gradient, through a folded
+    BatchNorm backward on igemm_nt2_bn and on conv_res16c_bn)."""
+    keep = ("dense_init", "denseblock1", "transition_layer1", "denseblock6", "transition_layer5",
+            "final_conv", "denseblock4bottleneck_layer_0", "denseblock4bottleneck_layer_1")
+    return [r for r in recs if r["name"].startswith(keep)]
+
+
+@pytest.mark.timeout(900)
 def test_c3_layer_local_parity(c3):
+    """Layer-local parity of C3's convs at the benchmarked plan (batch 8,
+    keep_prob 0.2): forward on image 0; input gradient -- including the
+    BatchNorm(+ReLU) backward and dropout re-draw run in the dgrad epilogue,
+    and the in-place accumulation into the dense blocks' shared concat
+    gradients (against the sum before the launch) -- dgamma / dbeta, and the
+    filter gradient over all 8 images (Network/model/FCDenseNet.py:23-61,
+    Network/utils/utils.py:300-301)."""
     _cpu_threads()
     sess, weights = c3["sess"], c3["weights"]
-    recs = sess.capture
-    sample = recs[:6] + recs[len(recs) // 2:len(recs) // 2 + 4] + recs[-6:]
+    sample = _c3_sample(sess.capture)
+    kinds = {r["bn_bwd"]["kernel"].split("<")[0] for r in sample if r["bn_bwd"] is not None}
+    assert {"igemm_nt2_bn", "conv_res16c_bn"} <= kinds, kinds
+    assert any(r["bn_bwd"] is not None and r["bn_bwd"]["base"] is not None for r in sample)
+    assert any(r["bn_bwd"] is not None and r["bn_bwd"]["drop"] is not None for r in sample)
+    assert len(sample) >= 40, len(sample)
     bad = []
     for rec in sample:
-        # dense-block input gradients accumulate in place into shared concat
-        # buffers (checked end to end); forward on image 0, wgrad on all 8
-        r = _layer_local(rec, weights[rec["name"]], None, sess, weights, images=1, dgrad=False)
+        r = _layer_local(rec, weights[rec["name"]], None, sess, weights, images=1, dgrad=True)
         print(rec["name"], rec["keep_prob"], {k: f"{v:+.2e}" for k, v in r.items()})
         bad += [(rec["name"], k, v) for k, v in r.items() if v > 0]
     assert not bad, bad
@@ -391,6 +457,58 @@ def test_c3_end_to_end_logits_image0(c3):
     print("C3 image-0 logits rel err", e, "agreement", agree)
     assert e < 3e-2, e
     assert agree > 0.99, agree
+
+
+# per-variable worst relative L2 of the bf16 step's gradients vs the oracle
+# with bf16 rounding points (measured values in each test's docstring)
+C2_WORST_REL_L2 = 0.25
+C3_WORST_REL_L2 = 0.25
+
+
+@pytest.mark.timeout(1200)
+def test_c3_gradients_end_to_end_bench_plan(c3):
+    """Every FC-DenseNet gradient of the benchmarked step (batch 8,
+    keep_prob 0.2, the bench's kernels and split-K plan) against the oracle
+    with bf16 rounding points and all 118 of the device's dropout masks, image
+    by image (the masked mean loss is the mean of the eight per-image means:
+    equal valid regions).  Every variable -- dense blocks 1..6, transitions,
+    transition-ups (decoder), head -- within cosine >= 0.95 and the per-variable
+    worst relative L2 <= C3_WORST_REL_L2 (ReLU-flip amplification at bf16,
+    tests/test_gpu_fcn.py), median <= 0.1 (Network/model/FCDenseNet.py:83-163)."""
+    _cpu_threads()
+    sess = c3["sess"]
+    sites = []
+    for rec in sess.capture:
+        kp = rec["keep_prob"]
+        if kp is not None and kp < 1.0:
+            d = rec["desc"]
+            sites.append((rec["name"][:-len("/weights")], rec["seed"], (C3_N, d.OH, d.OW, d.k_valid)))
+    assert len(sites) == 118
+    wr = {k: (bf16r(torch.from_numpy(v)) if v.ndim == 4 else torch.from_numpy(v)).requires_grad_(True)
+          for k, v in c3["weights"].items()}
+    x = torch.from_numpy(c3["img"])
+    HP, WP = x.shape[1], x.shape[2]
+    mask = torch.zeros(1, HP, WP)
+    mask[:, :C3_H, :C3_W] = 1
+    lab = torch.from_numpy(c3["lab"]).long()
+    total = 0.0
+    for i in range(C3_N):
+        du = {name: _uniform(seed, shp, 1, image=i) for name, seed, shp in sites}
+        _, logits = M.fcdensenet_forward(wr, x[i:i + 1], keep_prob=c3["kp"], dropout_u=du, quant=bf16r)
+        li = T.mean_softmax_xent(logits, T.one_hot(lab[i:i + 1], 2, torch.float32), mask) / C3_N
+        li.backward()
+        total += li.item()
+        del logits, li, du
+    assert abs(c3["loss"] - total) <= 1e-2 * max(1.0, abs(total)), (c3["loss"], total)
+    stats = _grad_stats(sess, {k: v.grad.numpy() for k, v in wr.items()})
+    for cos, l2, k in sorted(stats, key=lambda s: -s[1]):
+        print(f"GRAD {k:48s} cos={cos:.5f} relL2={l2:.3e}")
+    groups = ("denseblock1", "denseblock6", "transition_up", "final_conv")
+    for g in groups:
+        assert any(k.startswith(g) for _, _, k in stats), g
+    assert min(s[0] for s in stats) >= 0.95, min(stats)
+    assert max(s[1] for s in stats) <= C3_WORST_REL_L2, max(stats, key=lambda s: s[1])
+    assert np.median([s[1] for s in stats]) <= 0.1
 
 
 def test_c3_batch1_gradients_end_to_end(dev):
@@ -424,9 +542,10 @@ def test_c3_batch1_gradients_end_to_end(dev):
     assert np.abs(lg - rl).max() / np.abs(rl).max() < 3e-2
     assert abs(float(lo) - rloss.item()) <= 1e-2 * max(1.0, abs(rloss.item()))
     stats = _grad_stats(sess, {k: v.grad.numpy() for k, v in wr.items()})
-    for cos, l2, k in sorted(stats)[:10]:
+    for cos, l2, k in sorted(stats, key=lambda s: -s[1])[:10]:
         print(f"GRAD {k:40s} cos={cos:.5f} relL2={l2:.3e}")
     assert min(s[0] for s in stats) >= 0.95
+    assert max(s[1] for s in stats) <= C3_WORST_REL_L2, max(stats, key=lambda s: s[1])
     assert np.median([s[1] for s in stats]) <= 0.1
 
 
