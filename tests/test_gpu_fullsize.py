@@ -232,8 +232,8 @@ def _bn_bwd_local(bb, dr, sess, weights, rtol):
         a = xb * gamma / sqrt(1 + eps) + beta,  da = dr * [a > 0]
         dxb = da * gamma / sqrt(1 + eps) (* floor(kp + u) / kp),
         dgamma = sum(da * xb) / sqrt(1 + eps),  dbeta = sum(da).
-    Elements whose BN output is within 1e-5 of max |a| of zero (a ReLU
-    decision one fp32 rounding can flip) are left out of the elementwise
+    Elements whose BN output is nonzero and within 1e-5 of max |a| of zero (a
+    ReLU decision one fp32 rounding can flip) are left out of the elementwise
     check (counted: at most 1e-5 of them); the sums include them."""
     gname, bname = bb["gamma"], bb["beta"]
     gamma = torch.from_numpy(weights[gname]).double()
@@ -252,7 +252,9 @@ def _bn_bwd_local(bb, dr, sess, weights, rtol):
     if bb["base"] is not None:
         want = want + _host(bb["base"], Cb).double()
     got = _host(bb["dxb"], Cb).double()
-    amb = (a.abs() <= 1e-5 * a.abs().max()) if bb["relu"] else torch.zeros_like(a, dtype=torch.bool)
+    # exact zeros are not ambiguous (a dropped input with beta = 0 gives
+    # a == 0 on both sides: no gradient); tiny nonzero ones can flip
+    amb = ((a != 0) & (a.abs() <= 1e-5 * a.abs().max())) if bb["relu"] else torch.zeros_like(a, dtype=torch.bool)
     err = ((got - want).abs() - (rtol * want.abs() + 1e-3 * scale)).masked_fill(amb, -1.0)
     dg = (da * xb).sum(dim=(0, 1, 2)) * inv
     db = da.sum(dim=(0, 1, 2))
