@@ -881,6 +881,22 @@ __global__ __launch_bounds__(256) void rows_to_tr_k(const bf16* __restrict__ row
     }
 }
 
+extern "C" int seg_hwio_to_krsc(const void* rows, void* tr, int R, int S, int C, int K, int rows_ap, int rows_bp,
+                                int tr_ap, int dtype, void* stream) {
+    if (!rows || !tr || R <= 0 || S <= 0 || C <= 0 || K <= 0 || rows_ap < C || rows_bp < K || tr_ap < C ||
+        (rows_bp & 7) || (tr_ap & 7) || (dtype != SEG_BF16 && dtype != SEG_F16))
+        return SEG_EINVAL;
+    if (((uintptr_t)rows | (uintptr_t)tr) & 15) return SEG_EALIGN;
+    const int RS = R * S;
+    const int ctiles = (C + 63) / 64, ntiles = (K + 63) / 64;
+    const int tiles = ctiles * ntiles;
+    // a bit-pattern transpose: the bf16 kernel moves fp16 copies unchanged
+    hipLaunchKernelGGL(rows_to_tr_k, dim3((tiles + 3) / 4, RS), dim3(256), 0, (hipStream_t)stream, (const bf16*)rows,
+                       (bf16*)tr, RS, C, K, rows_ap, rows_bp, tr_ap, ctiles, tiles);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
 extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void* dy, float* dw,
                                           float* dbias, const seg_adam_fused* a, void* ws, size_t ws_bytes,
                                           void* stream) {

@@ -697,6 +697,12 @@ def adam_tf1_shadow(p, g, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_sc
           "adam_shadow")
 
 
+def hwio_to_krsc(rows, tr, R, S, C, K, stream=None):
+    """KRSC compute copy (rows = (tensor, a_pad, b_pad) HWIO, tr = (tensor, a_pad, _))."""
+    check(_lib.lib().seg_hwio_to_krsc(ptr(rows[0]), ptr(tr[0]), R, S, C, K, rows[1], rows[2], tr[1],
+                                      seg_dtype(rows[0]), stream_ptr(stream)), "hwio_to_krsc")
+
+
 def pack_segments(p, plan, dtype=BF16, stream=None):
     """Rewrite every planned variable's packed compute copies from p (no update)."""
     check(_lib.lib().seg_pack_segments(ptr(p), ptr(plan.table), plan.nsegs, plan.total_tiles, int(dtype),

@@ -218,6 +218,12 @@ class Session:
         # has no input gradient left to run then, beside the side stream's
         # remaining filter gradients instead of after them
         self.main_wgrad = 2
+        # conv6 / conv7 (the fused filter-gradient + Adam layers): plain filter
+        # gradient on the side stream, then the update by the register-light
+        # co-resident Adam (seg_adam_tf1_shadow) on a third stream beside the
+        # remaining MFMA-bound backward, instead of the fused launch
+        self.shadow_update = False
+        self._shadow = None
 
         self._side = None
         self._adam_ctx = None
@@ -681,14 +687,24 @@ class Session:
 
         A root qualifies when every part has a multiple of 8 channels (slices
         start on 16-byte chunks and carry no padding), is produced by a node
-        that writes through a row stride (conv, pooling, BatchNorm) and is not
-        already a slice, and every other reader of the group is a BatchNorm or
-        a (copying) concat -- the consumers whose input gradient can land in a
-        shared buffer in place."""
+        that writes through a row stride (conv, pooling, BatchNorm, transposed
+        conv) or is itself a concat root (nested), and is not already a slice,
+        and every other reader of the group is a BatchNorm or a concat -- the
+        consumers whose input gradient can land in a shared buffer in place --
+        except that the root itself may have ONE conv / transposed-conv
+        reader: its input gradient is the first write into the root's gradient
+        buffer (it runs first in backward) and covers it whole.
+
+        Nested roots: FC-DenseNet's decoder concat [transition_up, dense_block]
+        (Network/model/FCDenseNet.py:141-154) has the dense block's own root as
+        a part, so that block buffer becomes a channel slice of the decoder
+        buffer (offsets compose): the transposed conv writes its slice, the
+        block's layers theirs, and neither concat copies."""
         p.alias = {}          # tensor id -> (root tensor id, channel offset)
         p.alias_nodes = set()  # ConcatV2 node ids that became views
         if not self.alias_concat:
             return
+        nested = {}           # concat output id -> (outer root id, offset): a part of an accepted outer root
         shp = p.shapes
         producer = {id(n.output): n for n in p.nodes}
         users = {}
@@ -698,29 +714,48 @@ class Session:
                     users.setdefault(id(t), []).append(n)
         fetched = {id(f) for f in p.fetches if isinstance(f, G.Tensor)}
         concats = [n for n in p.nodes if n.kind == "ConcatV2"]
+        def part_ok(i):
+            prod = producer.get(i)
+            if prod is None or shp[i][3] % 8 or i in fetched:
+                return False
+            if i in p.alias:
+                return False
+            return prod.kind in ("conv", "AvgPool", "MaxPool", "bn", "tconv") or (
+                prod.kind == "ConcatV2" and i not in nested)
+
         for root in reversed(concats):
-            if id(root.output) in p.alias:
-                continue
+            rid = id(root.output)
+            if rid in p.alias and rid not in nested:
+                continue            # a prefix view of an accepted root
             ids = [id(t) for t in root.inputs]
             if len(set(ids)) != len(ids):
                 continue
             prefixes = [c for c in concats if c is not root and id(c.output) not in p.alias and
                         len(c.inputs) < len(ids) and [id(t) for t in c.inputs] == ids[:len(c.inputs)]]
-            ok = all(shp[i][3] % 8 == 0 and i not in p.alias and i not in fetched and
-                     producer.get(i) is not None and producer[i].kind in ("conv", "AvgPool", "MaxPool", "bn")
-                     for i in ids)
+            ok = all(part_ok(i) for i in ids) and (rid in nested or shp[rid][3] % 8 == 0)
             views = {root} | set(prefixes)
             group = {id(c.output) for c in views} | set(ids)
             if ok:
-                ok = all(u in views or u.kind in ("bn", "ConcatV2") for g in group for u in users.get(g, []))
+                root_users = users.get(rid, [])
+                for g in group:
+                    for u in users.get(g, []):
+                        if u in views or u.kind in ("bn", "ConcatV2"):
+                            continue
+                        if (g == rid and len(root_users) == 1 and u.kind in ("conv", "tconv")
+                                and u.inputs[0] is root.output and getattr(u, "residual", None) is not root.output):
+                            continue
+                        ok = False
             if not ok:
                 continue
-            r, off = id(root.output), 0
+            r, base = nested.get(rid, (rid, 0))
+            off = base
             for t in root.inputs:
                 p.alias[id(t)] = (r, off)
+                if producer[id(t)].kind == "ConcatV2":
+                    nested[id(t)] = (r, off)
                 off += shp[id(t)][3]
             for c in views:
-                p.alias[id(c.output)] = (r, 0)
+                p.alias[id(c.output)] = (r, base)
                 p.alias_nodes.add(id(c))
 
     def _allocate(self, p, consumers, feeds):
@@ -1219,6 +1254,9 @@ class Session:
                     self._adam_ctx = None
                 if self._red is not None:        # pending filter-gradient reductions done before Adam
                     self._red[1].wait_stream(self._red[0])
+                    if getattr(self, "_shadow_used", False):
+                        self._red[1].wait_stream(self._shadow)
+                        self._shadow_used = False
                     self._red = None
                 if dpa is not None:
                     if ok:
@@ -1299,6 +1337,15 @@ class Session:
     def _wgrad_side(self, p, n, level=1):
         """The side stream for node n's filter gradient, or None."""
         return self._red[0] if (self._red is not None and self.side_wgrad >= level) else None
+
+    def _shadow_ok(self, n):
+        """The shadow update needs the HWIO copy unpadded (it is written as the
+        flat 16-bit image of the new values) and a 16-bit compute dtype."""
+        if self.cdt not in (ops.BF16, ops.F16):
+            return False
+        R, S_, C_, K_ = n.w.shape
+        rows = self.store.packed.get((n.w.var_name, ops.PACK_HWIO))
+        return rows is None or (rows[1] == C_ and rows[2] == K_ and C_ % 2 == 0 and (R * S_ * C_ * K_) % 4 == 0)
 
     def _tick_fused(self, flush=False):
         keep = []
@@ -1542,6 +1589,17 @@ class Session:
                                "kernel": ops.conv_kernel_info(n.desc, ops.OP_BWD_DATA_BN)[0]}
                     done(dxb, acc)
                     self._grad_ready([gn, bn_])
+                elif id(x) in ng and id(x) in p.alias:
+                    # the input is an aliased concat root (FC-DenseNet decoder
+                    # concat views): the input gradient lands in the shared
+                    # gradient buffer -- whole (first write) or accumulated
+                    # in the epilogue
+                    dx, accf = adest(x)
+                    if accf and self.capture is not None:
+                        dx_base = dx.clone()
+                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None,
+                                ops.epilogue(residual=dx) if accf else None)
                 elif id(x) in ng:
                     dx, acc = dest(x)
                     mepi = self._mask_epi(p, x)
@@ -1600,6 +1658,36 @@ class Session:
                         self._timed(n.desc, ops.OP_BWD_FILTER_PRO, ops.conv2d_bwd_filter_pro, n.desc,
                                     buf[id(b.inputs[0])], self._prologue(b), dz, gw,
                                     self._node_ws(p, n) if side is not None else ws, None, fused_db)
+                elif (self._fused is not None and id(n) in p.adam_fusable and want_w and self.shadow_update
+                      and self._red is not None and self._shadow_ok(n)):
+                    # plain filter gradient beside the input-gradient chain, then
+                    # TF1 Adam + the compute copies on the shadow stream
+                    opt, gs, fdone = self._fused
+                    wn = n.w.var_name
+                    wsb = p.wg_ws[id(n)]
+                    with self._beside(self._red[0]):
+                        tok = self._timed(n.desc, ops.OP_BWD_FILTER, ops.conv2d_bwd_filter_begin, n.desc,
+                                          buf[id(x)], dz, gw, wsb, fused_db)
+                        ops.conv2d_bwd_filter_end(tok, gw, wsb, fused_db)
+                        ev = torch.cuda.Event()
+                        ev.record(self._red[0])
+                    if self._shadow is None:
+                        self._shadow = torch.cuda.Stream(device=self.device)
+                    self._shadow.wait_event(ev)
+                    rows = store.packed.get((wn, ops.PACK_HWIO))
+                    tr = store.packed.get((wn, ops.PACK_KRSC))
+                    R, S_, C_, K_ = n.w.shape
+                    with torch.cuda.stream(self._shadow):
+                        ops.adam_tf1_shadow(store.param(wn).view(-1), store.grad(wn).view(-1),
+                                            store.adam_m(wn).view(-1), store.adam_v(wn).view(-1), opt.lr, store.step,
+                                            opt.beta1, opt.beta2, opt.epsilon, grad_scale=gs,
+                                            copy16=None if rows is None else rows[0], dtype=self.cdt,
+                                            stream=self._shadow)
+                        if rows is not None and tr is not None:
+                            ops.hwio_to_krsc(rows, tr, R, S_, C_, K_, stream=self._shadow)
+                    self._shadow_used = True
+                    fdone.add(wn)
+                    self._tick_fused()
                 elif self._fused is not None and id(n) in p.adam_fusable and want_w:
                     # Conv2DBackpropFilter + AdamOptimizer on the filter in one launch
                     opt, gs, fdone = self._fused
@@ -1655,7 +1743,13 @@ class Session:
                 x = n.inputs[0]
                 if n.residual is not None:
                     contribute_alias(n.residual, dy)
-                if id(x) in ng:
+                if id(x) in ng and id(x) in p.alias:
+                    # the input is an aliased concat root (decoder concat views)
+                    dx, accf = adest(x)
+                    self._timed(n.desc, ops.OP_TBWD_DATA, ops.tconv2d_bwd_data, n.desc, dy,
+                                store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws, None,
+                                ops.epilogue(residual=dx) if accf else None)
+                elif id(x) in ng:
                     dx, acc = dest(x)
                     self._timed(n.desc, ops.OP_TBWD_DATA, ops.tconv2d_bwd_data, n.desc, dy,
                                 store.packed[(n.w.var_name, ops.PACK_TCONV_BWD)][0], dx, ws, None,

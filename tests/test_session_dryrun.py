@@ -140,10 +140,13 @@ def test_tconv_shape_rule_at_375x1242(dry):
 def test_fcdensenet_train_plan(dry):
     """C3 model plans: 125 convs + 5 transposed, pre-activation BN+ReLU fused,
     dropout in the conv epilogues; the concats of dense blocks 1-4 are channel
-    views of one buffer per block.  Block 5 starts from 140 channels (slices
-    would not start on 16-byte chunks) and block 6 feeds a transposed conv
-    (whose input gradient cannot accumulate in place): their 13 + 16 concats
-    and the 5 decoder skip concats run (fwd) and split (bwd)."""
+    views of one buffer per block, and those block buffers are themselves
+    channel slices of the decoder concats [transition_up_k, dense_block]
+    (k = 2..5, nested views: the transposed conv writes its slice, its input
+    gradient is the first write into the decoder concat's gradient buffer).
+    Blocks 5 and 6 start from 140 / 174 channels and decoder concat 1 joins
+    348-channel parts (slices would not start on 16-byte chunks): their
+    13 + 16 + 1 concats run (fwd) and split (bwd)."""
     from semanticsegmentation_tensorflow_amd.fcdensenet import FCDenseNet
     G.reset_default_graph()
     H, W = 64, 96
@@ -168,7 +171,7 @@ def test_fcdensenet_train_plan(dry):
     n_fold = 5 + 6 + 8 + 11 + 4
     assert c.count("seg_conv2d_fwd_pro") == n_fold
     assert c.count("seg_tconv2d_fwd") == 5
-    assert c.count("seg_concat_fwd") == 5 * 1 + (12 + 1) + (15 + 1)
+    assert c.count("seg_concat_fwd") == 1 + (12 + 1) + (15 + 1)
     assert c.count("seg_concat_bwd") == c.count("seg_concat_fwd")
     assert c.count("seg_bn_relu_fwd") == 123 - n_fold
     # the 59 bottleneck conv1 -> Dropout -> BN chains: the dropout gradient

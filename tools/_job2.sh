@@ -1,7 +1,11 @@
 set -o pipefail
 OUT=gpurun_out/r04_j2; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 1100 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -k "c3 or c2_end" --timeout 1000 --timeout-method thread > $OUT/pytest_full.log 2>&1 || { tail -60 $OUT/pytest_full.log; exit 1; }
-tail -3 $OUT/pytest_full.log
 timeout -k 10 200 python tools/shadow_probe.py conv4_2:fwd conv3_2:dgrad conv4_2:wgrad conv2_2:fwd conv1_2:dgrad > $OUT/shadow.txt 2>&1 || { tail -20 $OUT/shadow.txt; exit 1; }
 cat $OUT/shadow.txt
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fcdensenet.py tests/test_gpu_dp_rccl.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest_small.log 2>&1 || { tail -40 $OUT/pytest_small.log; exit 1; }
+tail -2 $OUT/pytest_small.log
+bash tools/ab_bench.sh r04_j2/ab "" "--schedule shadow_update=1" || exit 1
+P="--steps 10 --warmup 3 --no-cpu-baseline --no-traffic --no-miou --no-pipeline --no-extra --no-inference --no-dp-probe"
+timeout -k 10 300 python bench.py $P --model fcdensenet > $OUT/bench_c3.json 2> $OUT/bench_c3.err || { tail -30 $OUT/bench_c3.err; exit 1; }
+cat $OUT/bench_c3.json
 echo done
