@@ -175,8 +175,11 @@ __global__ __launch_bounds__(256) void adam_shadow_k(float* P, const float* G, f
                                                      unsigned n2, float lr_t, float b1, float b2, float eps,
                                                      float gs) {
     // buffer resources: one 32-bit lane offset addresses all five arrays (no
-    // 64-bit address pairs), 8-byte pairs per lane -- the register budget is
-    // the point of this kernel
+    // 64-bit address pairs), 8-byte pairs per lane, and the next pair's four
+    // loads in flight while this one updates (two register sets) -- the
+    // register budget is the point of this kernel.  Offsets past the range
+    // read zeros / drop stores (buffer bounds), so the pipeline needs no
+    // branch around a memory instruction.
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const int bytes = (int)(n2 * 8u);
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, bytes, 0x00020000);
@@ -186,12 +189,21 @@ __global__ __launch_bounds__(256) void adam_shadow_k(float* P, const float* G, f
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(Vv, (short)0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(copy, (short)0, copy ? bytes / 2 : 0,
                                                                         0x00020000);
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n2; i += gridDim.x * 256u) {
-        const unsigned o = i * 8u;
-        f32x2 pp = __builtin_amdgcn_raw_buffer_load_b64(rp, o, 0, 0);
-        const f32x2 gg = __builtin_amdgcn_raw_buffer_load_b64(rg, o, 0, 0);
-        f32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(rm, o, 0, 0);
-        f32x2 vv = __builtin_amdgcn_raw_buffer_load_b64(rv, o, 0, 0);
+    const unsigned stride = gridDim.x * 256u;
+    unsigned i = blockIdx.x * 256u + threadIdx.x;
+    const unsigned first = i;
+    if (first >= n2) return;
+    unsigned o = i * 8u;
+    f32x2 pp = __builtin_amdgcn_raw_buffer_load_b64(rp, o, 0, 0);
+    f32x2 gg = __builtin_amdgcn_raw_buffer_load_b64(rg, o, 0, 0);
+    f32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(rm, o, 0, 0);
+    f32x2 vv = __builtin_amdgcn_raw_buffer_load_b64(rv, o, 0, 0);
+    for (; i < n2; i += stride) {
+        const unsigned on = (i + stride) * 8u;      // out of range past the end: zeros
+        const f32x2 pn = __builtin_amdgcn_raw_buffer_load_b64(rp, on, 0, 0);
+        const f32x2 gn = __builtin_amdgcn_raw_buffer_load_b64(rg, on, 0, 0);
+        const f32x2 mn = __builtin_amdgcn_raw_buffer_load_b64(rm, on, 0, 0);
+        const f32x2 vn = __builtin_amdgcn_raw_buffer_load_b64(rv, on, 0, 0);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const float gc = gg[c] * gs;
@@ -199,6 +211,7 @@ __global__ __launch_bounds__(256) void adam_shadow_k(float* P, const float* G, f
             vv[c] = b2 * vv[c] + (1.f - b2) * gc * gc;
             pp[c] = pp[c] - lr_t * mm[c] / (sqrtf(vv[c]) + eps);
         }
+        o = i * 8u;
         __builtin_amdgcn_raw_buffer_store_b64(pp, rp, o, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b64(mm, rm, o, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b64(vv, rv, o, 0, 0);
@@ -206,6 +219,7 @@ __global__ __launch_bounds__(256) void adam_shadow_k(float* P, const float* G, f
             const T h[2] = {(T)pp[0], (T)pp[1]};
             __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const unsigned*>(h), rc, i * 4u, 0, 0);
         }
+        pp = pn; gg = gn; mm = mn; vv = vn;
     }
 }
 
