@@ -38,6 +38,7 @@ int g_nt_halo = 1;
 int g_halo_wide = 1;
 int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
+int g_res64_pp = 1;     // 64-wide blocks: the two-group ping-pong conv_res64pp
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
@@ -1207,6 +1208,280 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
 }
 
 // ---------------------------------------------------------------------------
+// Ping-pong form of conv_res64 for 64 output channels (conv1_2 fwd + pool1 and
+// its input gradient, Network/model/FCN.py:55-57).  conv_res64 runs one
+// 8-wave pipeline per CU, so a tile's epilogue, its halo commit and the load
+// latency of the next halo all sit between two tiles' MFMAs: ~7.5 us per
+// 256-px tile against ~2.2 us of MFMA.  Here the block's waves form two
+// groups of four (one wave of each on every SIMD); each wave owns 64 px x 64
+// channels (4 x 4 fragments) and a group owns a whole 8 x 32 tile, with its
+// own halo buffer filled by LDS DMA.  The block's tiles k = 0, 1, ... go to
+// group k % 2; tile k is computed in phase k and finished in phase k + 1, so
+// in every phase one group issues MFMAs while the other runs the epilogue of
+// its previous tile, DMAs its next halo and waits for it:
+//
+//   phase   0        1        2        3      ...
+//   group0  mma t0   epi t0   mma t2   epi t2
+//                    dma t2            dma t4
+//   group1  -        mma t1   epi t1   mma t3
+//                             dma t3
+//
+// One block-wide barrier per phase (both groups, nt + 1 phases): it retires
+// the computing group's halo reads before the group's next DMA overwrites
+// the buffer (issued one phase later), and the DMA-ing group's vmcnt(0) before
+// it publishes the new halo for the next phase's MFMAs.  LDS: filter 72 KB +
+// 2 halo buffers (43 DMA pieces of 8 rows) + the epilogue table = 162,304 B.
+// The ReluGrad mask of a tile is requested at the start of its compute phase
+// and reduced to one bit per output (mask > 0) after its MFMAs, so no wait for
+// it lands behind the epilogue phase's DMA (vmcnt retires in issue order).
+// ---------------------------------------------------------------------------
+constexpr int RPP_PIECES = 43;                       // halo DMA pieces (8 rows each, 340 used)
+constexpr int RPP_HS = RPP_PIECES * 8 * 128;         // 44,032 B per halo buffer
+
+template <typename T = bf16>
+__global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+    constexpr int NB = 64, TM = 4, TN = 4;
+    constexpr int BS = 9 * NB * 128;
+    __shared__ __attribute__((aligned(16))) char smem[BS + 2 * RPP_HS + 2 * NB * 4];
+    char* Bs = smem;
+    float* etab = reinterpret_cast<float*>(smem + BS + 2 * RPP_HS);   // [0][NB] scale, [1][NB] shift + bias
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wm = w & 3;
+    const int fr = lane & 15, fg = lane >> 4;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    const void* zero = (const void*)halo_zero_page;
+    const int hy0 = p.tsh < 0 ? 2 * p.tsh : 0, hx0 = p.tsw < 0 ? 2 * p.tsw : 0;
+    const int tpi = tiles_x * tiles_y;
+    const int nt = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const unsigned hbuf = (unsigned)(uintptr_t)(SEG_LDS char*)smem + BS + g * RPP_HS;
+    const char* Hs = smem + BS + g * RPP_HS;
+    const EpiParams& e = p.epi;
+
+    // halo of tile t into this group's buffer: piece i = wm + 4 k holds halo
+    // rows 8 i .. 8 i + 7; lane -> (row lr, LDS chunk lane & 7), which holds
+    // logical chunk (lane & 7) ^ (row & 6) (the swizzle the fragment reads use)
+    const int lr = lane >> 3;
+    const int hc = (lane & 7) ^ (lr & 6);
+    auto dma = [&](int t) {
+        const int img = t / tpi;
+        const int rem = t - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+        const int oy0 = ty * R64_BH + p.ioh + hy0, ox0 = tx * R64_BW + p.iow + hx0;
+        const T* xb = X + (long)img * p.x_img + hc * 8;
+#pragma unroll 1
+        for (int k = 0; k < (RPP_PIECES + 3) / 4; ++k) {
+            const int i = wm + 4 * k;
+            if (i < RPP_PIECES) {
+                const int hr = i * 8 + lr;
+                const int hy = hr / R64_HW, hx = hr - (hr / R64_HW) * R64_HW;
+                const int ih = oy0 + hy, iw = ox0 + hx;
+                const bool ok = hr < R64_HROWS && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+                glds16(ok ? (const void*)(xb + ((long)ih * p.IW + iw) * p.ldx) : zero, hbuf + i * 1024);
+            }
+        }
+    };
+    auto tile_of = [&](int k) { return (int)blockIdx.x + k * (int)gridDim.x; };
+
+    if (g < nt) dma(tile_of(g));
+    // ---- filter: Bs[tap][n][chunk ^ swz(n)] (resident for the whole launch)
+    for (int i = tid; i < 9 * NB * 8; i += 512) {
+        const int c8 = i & 7, n = (i >> 3) % NB, tap = i / (NB * 8);
+        const int j = tap / 3, ii = tap - (tap / 3) * 3;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (n < p.N)
+            v = *reinterpret_cast<const uint4*>(Wt + (long)n * p.w_col +
+                                                (long)((p.rb + p.rstep * j) * p.Sfull + (p.sb + p.sstep * ii)) * p.w_tap +
+                                                c8 * 8);
+        *reinterpret_cast<uint4*>(Bs + (tap * NB + n) * 128 + 16 * (c8 ^ (n & 6))) = v;
+    }
+    if (tid < NB) {
+        const bool cv = tid < e.n_valid;
+        etab[tid] = (e.scale && cv) ? e.scale[tid] : 1.f;
+        etab[NB + tid] = ((e.shift && cv) ? e.shift[tid] : 0.f) + ((e.bias && cv) ? e.bias[tid] : 0.f);
+    }
+    wait_vmcnt<0>();
+    lds_barrier();
+
+    int rowbase[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+        const int ml = wm * 64 + mi * 16;
+        rowbase[mi] = (ml / R64_BW) * R64_HW + (ml % R64_BW) + fr;
+    }
+    f32x4 acc[TM][TN];
+    uint2 mpre[TM][TN];
+    uint64_t mbits = 0;     // ReluGrad mask > 0, bit (mi * TN + ni) * 4 + j
+    for (int ph = 0; ph <= nt; ++ph) {
+        if ((ph & 1) == g) {
+            if (ph < nt) {   // ---- compute phase: tile ph
+                const int t = tile_of(ph);
+                const int img = t / tpi;
+                const int rem = t - img * tpi;
+                const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+                if (e.mask) {       // ReluGrad mask rows, used in the next phase
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi) {
+                        const int ml = wm * 64 + mi * 16 + fr;
+                        const int oy = ty * R64_BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
+                        const bool ok = oy < p.OH && ox < p.OW;
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni) {
+                            const int col0 = ni * 16 + 4 * fg;
+                            mpre[mi][ni] = uint2{0u, 0u};
+                            if (ok && col0 < p.N)
+                                mpre[mi][ni] = *reinterpret_cast<const uint2*>(
+                                    reinterpret_cast<const T*>(e.mask) + img * e.mask_img + ((long)oy * p.OW + ox) * e.ld_mask + col0);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+                // fragment addresses are recomputed in every compute phase (the
+                // laundered bases stop the compiler hoisting all 18 x 8 of them
+                // out of the phase loop into registers)
+                int rb[TM], brow = fr * 128;
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi) {
+                    rb[mi] = rowbase[mi];
+                    asm volatile("" : "+v"(rb[mi]));
+                }
+                asm volatile("" : "+v"(brow));
+                uint4 fa[2][TM], fb[2][TN];
+                auto load_step = [&](int st, uint4* a, uint4* b) {
+                    const int tap = st >> 1, chunk = (st & 1) * 4 + fg;
+                    const char* Bt = Bs + tap * NB * 128;
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi) {
+                        const int row = rb[mi] + ((tap / 3) * p.tsh - hy0) * R64_HW + (tap % 3) * p.tsw - hx0;
+                        a[mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * (chunk ^ (row & 6)));
+                    }
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        // row ni * 16 + fr: (row & 6) == (fr & 6)
+                        b[ni] = *reinterpret_cast<const uint4*>(Bt + ni * 2048 + brow + 16 * (chunk ^ (fr & 6)));
+                    }
+                };
+                load_step(0, fa[0], fb[0]);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int st = 0; st < 18; ++st) {
+                    const int cur = st & 1;
+                    if (st + 1 < 18) load_step(st + 1, fa[cur ^ 1], fb[cur ^ 1]);
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni)   // D^T[n][px] += W[n][k] X[px][k]
+                            acc[mi][ni] = mfma16x16x32<T>(fb[cur][ni], fa[cur][mi], acc[mi][ni]);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                if (e.mask) {       // the loads had the whole MFMA loop to land
+                    mbits = 0;
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni) {
+                            const unsigned short* mh = reinterpret_cast<const unsigned short*>(&mpre[mi][ni]);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (bits16_to_f32<T>(mh[j]) > 0.f) mbits |= 1ull << ((mi * TN + ni) * 4 + j);
+                        }
+                }
+            }
+        } else if (ph >= 1) {   // ---- epilogue phase: tile ph - 1, then the DMA of tile ph + 1
+            const int t = tile_of(ph - 1);
+            const int img = t / tpi;
+            const int rem = t - img * tpi;
+            const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+            if (ph + 1 < nt) dma(tile_of(ph + 1));
+            if (e.pool_y) {    // MaxPool 2x2 / 2 fused (as conv_res64: rows 2 wm, 2 wm + 1 per wave)
+                const int oy = ty * R64_BH + 2 * wm;
+                const int PH = p.OH >> 1, PW = p.OW >> 1;
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi) {
+                    const int ox = tx * R64_BW + mi * 16 + fr;
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const int col0 = ni * 16 + 4 * fg;
+                        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(etab + col0);
+                        const f32x4 ad4 = *reinterpret_cast<const f32x4*>(etab + NB + col0);
+                        T o[4];
+                        unsigned code = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float raw[4] = {acc[mi][ni][j], dpp_swap1(acc[mi][ni][j]),
+                                                  acc[mi + 2][ni][j], dpp_swap1(acc[mi + 2][ni][j])};
+                            const bool cv = col0 + j < e.n_valid;
+                            float q[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                float x = raw[u] * sc4[j] + ad4[j];
+                                if (e.relu) x = fmaxf(x, 0.f);
+                                q[u] = cv ? to_f32(from_f32<T>(x)) : 0.f;
+                            }
+                            unsigned a = 0;
+                            float mx = q[0];
+                            if (q[1] > mx) { mx = q[1]; a = 1; }
+                            if (q[2] > mx) { mx = q[2]; a = 2; }
+                            if (q[3] > mx) { mx = q[3]; a = 3; }
+                            o[j] = from_f32<T>(mx);
+                            code |= (a | (mx > 0.f ? 4u : 0u)) << (8 * j);
+                        }
+                        if ((fr & 1) || oy + 1 >= p.OH || ox + 1 >= p.OW || col0 >= p.N) continue;
+                        const long pix = ((long)img * PH + (oy >> 1)) * PW + (ox >> 1);
+                        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(e.pool_y) + pix * e.ld_pool + col0) =
+                            *reinterpret_cast<const uint2*>(o);
+                        if (e.pool_idx) *reinterpret_cast<unsigned*>(e.pool_idx + pix * e.ld_idx + col0) = code;
+                    }
+                }
+            } else {           // straight from registers: pixel (mi, fr), channels 4 fg .. + 3 of (ni)
+                const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi) {
+                    const int ml = wm * 64 + mi * 16 + fr;
+                    const int oy = oy0 + ml / R64_BW, ox = ox0 + ml % R64_BW;
+                    if (oy >= p.OH || ox >= p.OW) continue;
+                    const long pix = (long)oy * p.OW + ox;
+                    const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const int col0 = ni * 16 + 4 * fg;
+                        if (col0 >= p.N) continue;
+                        float res[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (e.residual) {
+                            const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) res[j] = to_f32(rp[j]);
+                        }
+                        T o[4];
+                        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(etab + col0);
+                        const f32x4 ad4 = *reinterpret_cast<const f32x4*>(etab + NB + col0);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int col = col0 + j;
+                            float x = acc[mi][ni][j] * sc4[j] + ad4[j];
+                            if (e.relu) x = fmaxf(x, 0.f);
+                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            x += res[j];
+                            if (e.mask) x = (mbits >> ((mi * TN + ni) * 4 + j)) & 1 ? x * e.mask_scale : 0.f;
+                            o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+                        }
+                        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
+                            *reinterpret_cast<const uint2*>(o);
+                    }
+                }
+            }
+            wait_vmcnt<0>();   // this group's next halo has landed (and its stores left)
+        }
+        lds_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Resident-filter direct conv for 16 input channels: the input gradient of
 // FC-DenseNet's 64 -> 16 growth convs (dz: 16 channels, dx: 64), which the
 // implicit GEMM ran at ~1.7 TB/s.  One v_mfma_f32_16x16x32 k-step covers two
@@ -1654,6 +1929,11 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
         return SEG_OK;
     }
     const int grid = std::min(ntiles, cus);
+    if (g_res64_pp) {
+        if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64pp<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        else hipLaunchKernelGGL((conv_res64pp<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        return SEG_OK;
+    }
     if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64<0, f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
     else hipLaunchKernelGGL(conv_res64<0>, dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
     return SEG_OK;

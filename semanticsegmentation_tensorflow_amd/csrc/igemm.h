@@ -256,6 +256,7 @@ bool halo_pools(const HaloPlan& hp, int kernel);
 int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype = SEG_BF16);
 extern int g_res64;
 extern int g_res16;
+extern int g_res64_pp;
 extern int g_res16c;
 bool res16c_ok(const NTParams& p, int dtype);
 void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
