@@ -550,7 +550,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res16c", &seg::g_res16c, 0, 1, 1, {}},
         {"res16", &seg::g_res16, 0, 1, 1, {}},
         {"res64", &seg::g_res64, 0, 1, 1, {}},
-        {"res64_pp", &seg::g_res64_pp, 0, 1, 1, {}},
+        {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
 #ifdef SEG_DIAG

@@ -38,7 +38,10 @@ int g_nt_halo = 1;
 int g_halo_wide = 1;
 int g_res64 = 1;
 int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
-int g_res64_pp = 1;     // 64-wide blocks: the two-group ping-pong conv_res64pp
+// 64-wide blocks on the two-group ping-pong conv_res64pp: 0 never, 1 for the
+// pooled forward and the ReluGrad-masked input gradient (conv1_2: 191 vs 192
+// and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
+int g_res64_pp = 1;
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
@@ -1929,7 +1932,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
         return SEG_OK;
     }
     const int grid = std::min(ntiles, cus);
-    if (g_res64_pp) {
+    if (g_res64_pp == 2 || (g_res64_pp == 1 && (p.epi.pool_y || p.epi.mask))) {
         if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64pp<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         else hipLaunchKernelGGL((conv_res64pp<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         return SEG_OK;

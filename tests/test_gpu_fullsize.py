@@ -232,9 +232,12 @@ def _bn_bwd_local(bb, dr, sess, weights, rtol):
         a = xb * gamma / sqrt(1 + eps) + beta,  da = dr * [a > 0]
         dxb = da * gamma / sqrt(1 + eps) (* floor(kp + u) / kp),
         dgamma = sum(da * xb) / sqrt(1 + eps),  dbeta = sum(da).
-    Elements whose BN output is nonzero and within 1e-5 of max |a| of zero (a
-    ReLU decision one fp32 rounding can flip) are left out of the elementwise
-    check (counted: at most 1e-5 of them); the sums include them."""
+    Elements whose BN output is nonzero and within 1e-5 of its own terms
+    (|a| <= 1e-5 (|xb g / sqrt(1 + eps)| + |beta|): a ReLU decision the fp32
+    rounding of those terms can flip) are left out of the elementwise check
+    (counted: at most 1e-5 of them); the sums include them.  The bound is per
+    element: with frozen statistics the deep blocks' activations span ~1e10,
+    so a bound relative to max |a| would exclude most of a layer."""
     gname, bname = bb["gamma"], bb["beta"]
     gamma = torch.from_numpy(weights[gname]).double()
     beta = torch.from_numpy(weights[bname]).double()
@@ -254,7 +257,8 @@ def _bn_bwd_local(bb, dr, sess, weights, rtol):
     got = _host(bb["dxb"], Cb).double()
     # exact zeros are not ambiguous (a dropped input with beta = 0 gives
     # a == 0 on both sides: no gradient); tiny nonzero ones can flip
-    amb = ((a != 0) & (a.abs() <= 1e-5 * a.abs().max())) if bb["relu"] else torch.zeros_like(a, dtype=torch.bool)
+    amb = (((a != 0) & (a.abs() <= 1e-5 * ((xb * (gamma * inv)).abs() + beta.abs()))) if bb["relu"]
+           else torch.zeros_like(a, dtype=torch.bool))
     err = ((got - want).abs() - (rtol * want.abs() + 1e-3 * scale)).masked_fill(amb, -1.0)
     dg = (da * xb).sum(dim=(0, 1, 2)) * inv
     db = da.sum(dim=(0, 1, 2))
@@ -463,7 +467,7 @@ def test_c3_end_to_end_logits_image0(c3):
 
 # per-variable worst relative L2 of the bf16 step's gradients vs the oracle
 # with bf16 rounding points (measured values in each test's docstring)
-C2_WORST_REL_L2 = 0.25
+C2_WORST_REL_L2 = 0.05     # measured 1.13e-2 (conv4_1/weights, round 4)
 C3_WORST_REL_L2 = 0.25
 
 

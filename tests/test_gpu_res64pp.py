@@ -30,8 +30,9 @@ def _operands(dev, N, H, W, dtype, seed):
 
 
 def _both(fn):
-    """fn() under the ping-pong kernel and under the legacy one."""
-    ops.set_option("res64_pp", 1)
+    """fn() under the ping-pong kernel (forced for every epilogue) and under
+    the legacy one."""
+    ops.set_option("res64_pp", 2)
     a = fn()
     ops.set_option("res64_pp", 0)
     try:
