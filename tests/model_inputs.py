@@ -28,10 +28,15 @@ def he_weights(shapes, seed):
     return out
 
 
-def densenet_weights(shapes, seed):
+def densenet_weights(shapes, seed, keep_prob=1.0):
     """FC-DenseNet test weights: He-scaled convs (transposed-conv fan-in =
     (k/stride)^2 * C_in), BN gamma ~ 1, so activations stay O(1) through the
-    pre-activation stack; first conv scaled for raw 0..255 pixels."""
+    pre-activation stack; first conv scaled for raw 0..255 pixels.
+    keep_prob < 1: the dropout-followed convs (the bottlenecks' conv1 / conv2,
+    FCDenseNet.py:28-34) scaled by sqrt(keep_prob), which cancels the
+    dropout's 1/keep_prob variance gain -- with plain He weights and the
+    reference's frozen BatchNorm, 118 dropouts at keep_prob 0.2 grow the
+    activations to ~1e11 by the last dense block and saturate the softmax."""
     rng = np.random.default_rng(seed)
     out = {}
     for name, s in shapes.items():
@@ -44,6 +49,10 @@ def densenet_weights(shapes, seed):
         else:
             out[name] = (0.1 * rng.standard_normal(s)).astype(np.float32)
     out["dense_init/weights"] /= np.float32(128.0)
+    if keep_prob < 1.0:
+        for name in out:
+            if "bottleneck_layer" in name and name.endswith("/weights"):
+                out[name] *= np.float32(math.sqrt(keep_prob))
     return out
 
 

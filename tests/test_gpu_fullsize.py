@@ -393,7 +393,12 @@ C3_H, C3_W, C3_N = 375, 1242, 8
 
 @pytest.fixture(scope="module")
 def c3(dev):
-    weights = densenet_weights(M.fcdensenet_param_shapes(3, 2), 71)
+    # dropout-compensated weights: activations O(1) at keep_prob 0.2 (see
+    # densenet_weights; the plain ones reach ~1e11, a saturated softmax where
+    # bf16 rounding differences are amplified: round 4 measured worst cos
+    # 0.922 / rel-L2 0.39, median 0.127 on them -- a property of those
+    # weights, not of the kernels: layer-local parity holds either way)
+    weights = densenet_weights(M.fcdensenet_param_shapes(3, 2), 71, keep_prob=0.2)
     return _bench_step("fcdensenet", C3_H, C3_W, C3_N, weights, 72)
 
 
