@@ -138,6 +138,9 @@ SIGNATURES = {
     "seg_conv2d_fwd_pool": (_I, [_DP, _P, _P, _EP, _P, _I, _P, _I, _P, _Z, _P]),
     "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_conv2d_fwd_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_fwd_bn2": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _EP, _P, _P, _I, _P, _P, _F, _I, _P, _Z,
+                                _P]),
+    "seg_conv2d_fwd_bn2_ok": (_I, [_DP, _I]),
     "seg_conv_bwd_data_bn_workspace": (_Z, [_DP]),
     "seg_conv2d_bwd_data_bn": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _Z, _P]),
     "seg_conv2d_bwd_filter_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _P, _P, _P, _Z, _P]),

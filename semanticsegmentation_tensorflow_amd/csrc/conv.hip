@@ -668,6 +668,62 @@ extern "C" int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const s
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Conv2D (operand prologue optional) whose output also feeds a frozen
+// BatchNorm(+ReLU): both maps in one launch (FC-DenseNet's bottleneck conv1 ->
+// dropout -> BN -> ReLU, Network/model/FCDenseNet.py:28-31).  The kernel
+// chosen for the conv must be one that writes the second output.
+static int fwd_bn2_params(const seg_conv_desc* d, const void* x, const seg_prologue* pro, const void* w,
+                          const seg_epilogue* epi, void* y, void* y2, int ld_y2, const float* gamma2,
+                          const float* beta2, float eps2, int relu2, NTParams* out, bool* stream1x1) {
+    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return SEG_EINVAL;
+    if (ld_y2 < d->K || ld_y2 % 8) return SEG_EINVAL;
+    if (pro && (!pro->gamma || !pro->beta)) return SEG_EINVAL;
+    NTParams p = conv_fwd_params(d);
+    p.x = x; p.w = w; p.y = y;
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    if (pro) p.pro = make_pro(pro, d->c_valid);
+    p.epi.y2 = y2;
+    p.epi.ld_y2 = ld_y2;
+    p.epi.y2_img = (long)d->OH * d->OW * ld_y2;
+    p.epi.bn2_gamma = gamma2;
+    p.epi.bn2_beta = beta2;
+    p.epi.bn2_inv = 1.0f / sqrtf(1.0f + eps2);   // as seg_bn_relu_fwd
+    p.epi.bn2_relu = relu2 ? 1 : 0;
+    p.epi.bn2_cv = d->k_valid;
+    *stream1x1 = pro && seg::s1x1_ok(p, d->dtype, 1);
+    if (!*stream1x1 && !seg::nt_bn2_ok(p, d->dtype)) return SEG_EINVAL;
+    *out = p;
+    return SEG_OK;
+}
+
+extern "C" int seg_conv2d_fwd_bn2_ok(const seg_conv_desc* d, int with_prologue) {
+    static const float one = 1.f;
+    static seg_prologue pro = {&one, &one, 1e-3f, 1};
+    NTParams p;
+    bool s1;
+    // shape-only query: aligned stand-ins for the buffers
+    const void* a = reinterpret_cast<const void*>(uintptr_t(1) << 20);
+    return fwd_bn2_params(d, a, with_prologue ? &pro : nullptr, a, nullptr, (void*)a, (void*)a,
+                          d ? d->ldy : 0, &one, &one, 1e-3f, 1, &p, &s1) == SEG_OK;
+}
+
+extern "C" int seg_conv2d_fwd_bn2(const seg_conv_desc* d, const void* x, const seg_prologue* pro, const void* w,
+                                  const seg_epilogue* epi, void* y, void* y2, int ld_y2, const float* gamma2,
+                                  const float* beta2, float eps2, int relu2, void* ws, size_t ws_bytes,
+                                  void* stream) {
+    if (!x || !w || !y || !y2 || !gamma2 || !beta2) return SEG_EINVAL;
+    NTParams p;
+    bool s1 = false;
+    int st = fwd_bn2_params(d, x, pro, w, epi, y, y2, ld_y2, gamma2, beta2, eps2, relu2, &p, &s1);
+    if (st) return st;
+    if (s1) {
+        seg::launch_s1x1(p, d->dtype, seg::device_cus(), (hipStream_t)stream);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
 extern "C" int seg_conv2d_bwd_filter_pro(const seg_conv_desc* d, const void* x, const seg_prologue* pro,
                                          const void* dy, float* dw, float* dbias, void* ws, size_t ws_bytes,
                                          void* stream) {

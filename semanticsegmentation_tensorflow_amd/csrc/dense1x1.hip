@@ -54,7 +54,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
     __shared__ __attribute__((aligned(16))) char ring[S1_NST * STG];            // 96 KiB
     __shared__ __attribute__((aligned(16))) char wsm[64 * S1_MAXC * 2];          // 32 KiB
     __shared__ __attribute__((aligned(16))) float ptab[2 * S1_MAXC];
-    __shared__ __attribute__((aligned(16))) float etab[2][64];
+    __shared__ __attribute__((aligned(16))) float etab[4][64];   // scale, shift + bias, BN2 scale, BN2 shift
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -83,7 +83,11 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
         const bool cv = tid < e.n_valid;
         etab[0][tid] = (e.scale && cv) ? e.scale[tid] : 1.f;
         etab[1][tid] = ((e.shift && cv) ? e.shift[tid] : 0.f) + ((e.bias && cv) ? e.bias[tid] : 0.f);
+        const bool c2 = e.y2 && tid < e.bn2_cv;
+        etab[2][tid] = c2 ? e.bn2_gamma[tid] * e.bn2_inv : 0.f;
+        etab[3][tid] = c2 ? e.bn2_beta[tid] : 0.f;
     }
+    const int stn = e.y2 ? 2 * S1_ST : S1_ST;        // epilogue stores per wave per tile
 
     // ---- x DMA: every wave stages its own 16 pixel rows (w*16 + q*8 + lr,
     // physical chunk lane & 7, row swizzle (row >> 1) & 7), so the waves never
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
     auto younger = [&](int s) {
         int n = S1_DMA * (min(S - 1, s + S1_NST - 2) - s);
         for (int j = max(0, s - S1_NST + 1); j < s; ++j)
-            if (j % kt == kt - 1) n += S1_ST;
+            if (j % kt == kt - 1) n += stn;
         return n;
     };
     for (int s = 0; s < S1_NST - 1 && s < S; ++s) issue(s);
@@ -174,6 +178,20 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
                 uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + m * p.ldy + col0)
                                 : s1_trash + (tid & 4095);
                 *dst = *reinterpret_cast<const uint2*>(o);
+                if (e.y2) {      // BN2(+ReLU) of the stored values (seg_bn_relu_fwd's arithmetic)
+                    const f32x4 s2 = *reinterpret_cast<const f32x4*>(&etab[2][col0]);
+                    const f32x4 t2 = *reinterpret_cast<const f32x4*>(&etab[3][col0]);
+                    T o2[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float v2 = __builtin_fmaf(to_f32(o[j]), s2[j], t2[j]);
+                        if (e.bn2_relu) v2 = fmaxf(v2, 0.f);
+                        o2[j] = from_f32<T>(v2);
+                    }
+                    uint2* dst2 = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(e.y2) + m * e.ld_y2 + col0)
+                                     : s1_trash + (tid & 4095);
+                    *dst2 = *reinterpret_cast<const uint2*>(o2);
+                }
                 acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
         }
@@ -192,7 +210,8 @@ bool s1x1_ok(const NTParams& p, int dtype, int nphases) {
            p.IH == p.Ha && p.IW == p.Wa && p.OH == p.Ha && p.OW == p.Wa && p.x_img == (long)p.IH * p.IW * p.ldx &&
            p.y_img == (long)p.OH * p.OW * p.ldy && p.N <= 64 && p.K <= S1_MAXC && p.K % 8 == 0 && p.ldx % 8 == 0 &&
            p.ldy % 4 == 0 && ((uintptr_t)p.x % 16) == 0 && ((uintptr_t)p.y % 8) == 0 && !p.epi.residual &&
-           !p.epi.mask && !p.epi.bn_x && p.M > 0;
+           !p.epi.mask && !p.epi.bn_x && p.M > 0 &&
+           (!p.epi.y2 || (p.epi.ld_y2 % 4 == 0 && ((uintptr_t)p.epi.y2 % 8) == 0 && p.epi.y2_img == (long)p.OH * p.OW * p.epi.ld_y2));
 }
 
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {

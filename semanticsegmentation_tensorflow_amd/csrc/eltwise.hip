@@ -600,7 +600,8 @@ __global__ __launch_bounds__(256) void bn_relu_fwd_k(const T* __restrict__ x, in
             Chunk<T>::unpack(ldc(x + pix * ldx + cc * EPC), v);
 #pragma unroll
             for (int e = 0; e < EPC; ++e) {
-                float o = v[e] * sc[j][e] + sh[j][e];
+                // one fma: the conv epilogues' second output (EpiParams.y2) computes the same
+                float o = __builtin_fmaf(v[e], sc[j][e], sh[j][e]);
                 if (relu) o = fmaxf(o, 0.f);
                 v[e] = o;
             }

@@ -43,6 +43,19 @@ struct EpiParams {
     void* pool_y;
     unsigned char* pool_idx;
     int ld_pool, ld_idx;
+    // Frozen BatchNorm(+ReLU) of this conv's output written beside it
+    // (seg_conv2d_fwd_bn2: FC-DenseNet's bottleneck conv1 -> BN -> ReLU):
+    // y2 = relu(fma(y, bn2_gamma * bn2_inv, bn2_beta)) from the stored
+    // (rounded) y, channels >= bn2_cv 0 -- seg_bn_relu_fwd's arithmetic.
+    // conv1x1_stream and igemm_nt2 (no split-K) only; 16-bit types.
+    void* y2;
+    long y2_img;
+    int ld_y2;
+    const float* bn2_gamma;
+    const float* bn2_beta;
+    float bn2_inv;
+    int bn2_relu;
+    int bn2_cv;
 };
 
 // dgamma / dbeta from per-tile partial rows [nrows][2C] (eltwise.hip);
@@ -257,6 +270,8 @@ int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int 
 extern int g_res64;
 extern int g_res16;
 extern int g_res64_pp;
+// the launch plan for p writes EpiParams.y2 (seg_conv2d_fwd_bn2)
+bool nt_bn2_ok(const NTParams& p, int dtype);
 extern int g_res16c;
 bool res16c_ok(const NTParams& p, int dtype);
 void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);

@@ -817,6 +817,14 @@ static bool nt_plan_pools(const NTPlan& pl) {
     return false;
 }
 
+// Whether the planned kernel writes EpiParams.y2 (the BN(+ReLU) second
+// output): igemm_nt2 with its operand prologue or without, no split-K.
+static bool nt_plan_bn2(const NTPlan& pl, int dtype) {
+    return dtype != SEG_F32 && pl.splits == 1 && (pl.kind == NTK_PRO2 || pl.kind == NTK_NT2);
+}
+
+bool nt_bn2_ok(const NTParams& p, int dtype) { return nt_plan_bn2(nt_plan(p, dtype, 1, p.M), dtype); }
+
 template <typename T>
 static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BK = 128 / sizeof(T);
@@ -824,6 +832,8 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     // a pooled launch writes no unpooled map (p.y is null): only a kernel with
     // the pooled epilogue and no split-K slabs may run it
     if (p.epi.pool_y && !nt_plan_pools(pl)) return SEG_EINVAL;
+    // likewise a second BN output: only the kernels that write it
+    if (p.epi.y2 && (nphases != 1 || !nt_plan_bn2(pl, dt_traits<T>::id))) return SEG_EINVAL;
     int splits = pl.splits;
     p.partial = nullptr;
     switch (pl.kind) {

@@ -196,6 +196,25 @@ def conv2d_fwd_pro(desc, x, pro, w_krsc, y, epi=None, ws=None, stream=None):
     return y
 
 
+def conv2d_fwd_bn2_ok(desc, with_prologue=False):
+    """Whether conv2d_fwd_bn2 runs this conv (the kernel it plans for has the
+    second, BatchNorm(+ReLU), output)."""
+    return bool(_lib.lib().seg_conv2d_fwd_bn2_ok(ctypes.byref(desc), 1 if with_prologue else 0))
+
+
+def conv2d_fwd_bn2(desc, x, pro, w_krsc, y, y2, gamma2, beta2, relu2=True, eps2=1e-3, epi=None, ws=None,
+                   stream=None):
+    """Conv2D (pro: operand prologue or None) writing y and y2 = relu(BN(y))
+    (seg_conv2d_fwd_bn2; y2 bit-identical to bn_relu_fwd(y, y2, ...))."""
+    d = _with_ld(desc, x, y)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_FWD))
+    check(_lib.lib().seg_conv2d_fwd_bn2(ctypes.byref(d), ptr(x), None if pro is None else ctypes.byref(pro),
+                                        ptr(w_krsc), None if epi is None else ctypes.byref(epi), ptr(y), ptr(y2),
+                                        pixel_stride(y2), ptr(gamma2), ptr(beta2), float(eps2),
+                                        1 if relu2 else 0, wsp, wss, stream_ptr(stream)), "conv2d_fwd_bn2")
+    return y
+
+
 def conv_bwd_data_bn_workspace(desc):
     """Bytes for conv2d_bwd_data_bn, 0 where the fused path does not apply."""
     return int(_lib.lib().seg_conv_bwd_data_bn_workspace(ctypes.byref(desc)))

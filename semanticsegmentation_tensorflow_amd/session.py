@@ -203,6 +203,8 @@ class Session:
         self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
         # conv (+bias +ReLU) -> 2x2 MaxPool as one launch (pooled epilogue)
         self.fuse_pool = True
+        # conv -> BatchNorm(+ReLU): the BN output written by the conv epilogue
+        self.fuse_bn_out = True
         self._red = None                 # (side stream, compute stream) during a step
         # deferred filter gradients: the kernel too (not only its reduction) on
         # the side stream (1), and the fused filter-gradient + Adam launches (2)
@@ -857,6 +859,7 @@ class Session:
                     N, H, W, C = xb.shape
                     p.pool_idx[id(n)] = torch.empty(N * (H // 2) * (W // 2) * C, dtype=torch.uint8, device=dev)
         self._plan_pool_fusion(p, consumers)
+        self._plan_bn_outputs(p, consumers)
         ws_need = max(ws_need, 8192)
         self.ws.get(ws_need)
         # packed filter copies
@@ -900,6 +903,36 @@ class Session:
             p.pool_fuse[id(n)] = m
             p.buf[id(y)] = None                # never written
         p.pool_fused = {id(m) for m in p.pool_fuse.values()}
+
+    def _plan_bn_outputs(self, p, consumers):
+        """Conv -> (its epilogue's dropout) -> BatchNorm(+ReLU): FC-DenseNet's
+        bottleneck conv1 -> BN -> ReLU before the growth conv
+        (Network/model/FCDenseNet.py:28-31).  When the BN node is the conv
+        output's only forward reader, the conv launch also writes the BN(+ReLU)
+        map (ops.conv2d_fwd_bn2, bit-identical to bn_relu_fwd) and the BN's own
+        forward pass -- a full re-read of the conv output -- is skipped.  The
+        conv output is still written: the BN backward re-derives its ReLU mask
+        and dgamma from it.  p.bn_out2: conv node id -> BN node."""
+        p.bn_out2 = {}
+        p.bn_out2_done = set()
+        if not self.fuse_bn_out or self.cdt == ops.F32:
+            return
+        producer = {id(n.output): n for n in p.nodes if n.kind == "conv"}
+        for b in p.nodes:
+            if b.kind != "bn" or id(b) in p.folded or id(b.output) in p.fetched:
+                continue
+            c = producer.get(id(b.inputs[0]))
+            if c is None or id(c) in p.pool_fuse or id(c) in p.bn_out2 or id(c.output) in p.fetched:
+                continue
+            cs = consumers.get(id(c.output), [])
+            if len(cs) != 1 or cs[0] is not b.ops[0]:
+                continue
+            if p.buf.get(id(c.output)) is None or p.buf.get(id(b.output)) is None:
+                continue
+            if not ops.conv2d_fwd_bn2_ok(c.desc, getattr(c, "pro", None) is not None):
+                continue
+            p.bn_out2[id(c)] = b
+            p.bn_out2_done.add(id(b))
 
     def _plan_backward(self, p):
         dev = self.device
@@ -1123,7 +1156,15 @@ class Session:
                 n.seed_val = (step_seed + i * 131) & 0xFFFFFFFF
                 epi = ops.epilogue(bias=store.param(n.bias.var_name) if n.bias is not None else None,
                                    relu=n.relu, keep_prob=kp, seed=n.seed_val)
-                if getattr(n, "pro", None) is not None:
+                if id(n) in p.bn_out2:
+                    b2 = p.bn_out2[id(n)]
+                    b = getattr(n, "pro", None)
+                    self._timed(n.desc, ops.OP_FWD_PRO if b is not None else ops.OP_FWD, ops.conv2d_fwd_bn2, n.desc,
+                                x if b is None else buf[id(b.inputs[0])], None if b is None else self._prologue(b),
+                                store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, buf[id(b2.output)],
+                                store.param(b2.gamma.var_name), store.param(b2.beta.var_name), b2.relu, b2.eps,
+                                epi, self.ws)
+                elif getattr(n, "pro", None) is not None:
                     b = n.pro
                     self._timed(n.desc, ops.OP_FWD_PRO, ops.conv2d_fwd_pro, n.desc, buf[id(b.inputs[0])],
                                 self._prologue(b), store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
@@ -1155,8 +1196,8 @@ class Session:
             elif k == "Add":
                 ops.add(buf[id(n.inputs[0])], buf[id(n.inputs[1])], y)
             elif k == "bn":
-                if id(n) in p.folded:
-                    continue                        # applied by its conv's operand prologue
+                if id(n) in p.folded or id(n) in p.bn_out2_done:
+                    continue                        # applied by its conv's operand prologue / written by its conv
                 C = p.shapes[id(n.inputs[0])][3]
                 ops.bn_relu_fwd(buf[id(n.inputs[0])], y, store.param(n.gamma.var_name),
                                 store.param(n.beta.var_name), C, n.relu, n.eps)

@@ -24,7 +24,7 @@ class _Rec:
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
                              "seg_adam_segments_plan", "seg_tconv_filter_apad",
                              "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace",
-                             "seg_conv2d_fwd_pool_ok")
+                             "seg_conv2d_fwd_pool_ok", "seg_conv2d_fwd_bn2_ok")
 
         def fn(*a):
             if host_only:
@@ -167,13 +167,18 @@ def test_fcdensenet_train_plan(dry):
     # operand prologue (the BatchNorm is folded, its output never written):
     # dense blocks 1-4 (5 + 6 + 8 + 11 bottlenecks) and 4 transitions -- blocks
     # 5 and 6 start from 140 / 174 channels (140 + 16 i, 174 + 16 i)
-    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pro") == 125
+    fwd = ("seg_conv2d_fwd", "seg_conv2d_fwd_pro", "seg_conv2d_fwd_bn2")
+    assert sum(c.count(f) for f in fwd) == 125
     n_fold = 5 + 6 + 8 + 11 + 4
-    assert c.count("seg_conv2d_fwd_pro") == n_fold
     assert c.count("seg_tconv2d_fwd") == 5
     assert c.count("seg_concat_fwd") == 1 + (12 + 1) + (15 + 1)
     assert c.count("seg_concat_bwd") == c.count("seg_concat_fwd")
-    assert c.count("seg_bn_relu_fwd") == 123 - n_fold
+    # every bottleneck conv1 also writes the BN2 + ReLU map feeding its growth
+    # conv (seg_conv2d_fwd_bn2: the BN's forward pass never re-reads the conv
+    # output); the n_fold - 4 of them with a folded BN1 prologue among them
+    assert c.count("seg_conv2d_fwd_bn2") == 59
+    assert c.count("seg_conv2d_fwd_pro") == 4
+    assert c.count("seg_bn_relu_fwd") == 123 - n_fold - 59
     # the 59 bottleneck conv1 -> Dropout -> BN chains: the dropout gradient
     # rides in the BN backward; only the growth convs' dropouts keep a pass
     # BN backward inside the consuming conv's input-gradient launch: the n_fold

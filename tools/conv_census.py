@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 from semanticsegmentation_tensorflow_amd import _lib, ops  # noqa: E402
 
-OPCODE = {"seg_conv2d_fwd": 0, "seg_conv2d_fwd_pool": 0, "seg_conv2d_bwd_data": 1, "seg_conv2d_bwd_filter": 2,
+OPCODE = {"seg_conv2d_fwd": 0, "seg_conv2d_fwd_pool": 0, "seg_conv2d_fwd_bn2": 0, "seg_conv2d_bwd_data": 1, "seg_conv2d_bwd_filter": 2,
           "seg_conv2d_bwd_filter_begin": 2, "seg_conv2d_bwd_filter_adam": 2, "seg_tconv2d_fwd": 3,
           "seg_tconv2d_bwd_data": 4, "seg_tconv2d_bwd_filter": 5, "seg_conv2d_bwd_data_bn": 6,
           "seg_conv2d_fwd_pro": 7, "seg_conv2d_bwd_filter_pro": 8}
@@ -31,7 +31,7 @@ OPNAME = ["fwd", "dgrad", "wgrad", "tfwd", "tdgrad", "twgrad", "dgrad_bn", "fwd_
 HOST_ONLY = ("seg_conv_desc_init", "seg_tconv_desc_init", "seg_conv_workspace", "seg_bias_grad_workspace",
              "seg_xent_workspace", "seg_status_string", "seg_adam_segments_plan", "seg_tconv_filter_apad",
              "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace", "seg_conv2d_fwd_pool_ok",
-             "seg_conv_kernel_info")
+             "seg_conv_kernel_info", "seg_conv2d_fwd_bn2_ok")
 
 
 class Recorder:
