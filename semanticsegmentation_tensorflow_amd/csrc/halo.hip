@@ -52,6 +52,15 @@ struct HaloGeom {
     int nchunks, kc_per_split;
 };
 
+// Output pixel (within its image) of GEMM grid point (oy, ox) on the Ha x Wa
+// grid: (oy * osh + ooh, ox * osw + oow).  halo_plan admits only convs
+// (Ha = OH, Wa = OW, stride 1, offset 0: the identity map); a transposed
+// conv's 2x2-tap phases do not fit the halo pipelines, which spread a chunk's
+// halo DMA over at least hi + 1 (conv_halo) / 7 (conv_halo2) taps.
+__device__ __forceinline__ long halo_opix(const NTParams& p, int oy, int ox) {
+    return (long)(oy * p.osh + p.ooh) * p.OW + (ox * p.osw + p.oow);
+}
+
 // value of lane ^ 1 (DPP quad_perm [1, 0, 3, 2]: no LDS crossbar traffic)
 __device__ __forceinline__ float dpp_swap1(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -278,8 +287,8 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             for (int r = 0; r < 4; ++r) {
                 const int ml = wm * WTM + mi * 16 + fg * 4 + r;
                 const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-                if (oy >= p.OH || ox >= p.OW) continue;
-                const long m = ((long)img * p.OH + oy) * p.OW + ox;
+                if (oy >= p.Ha || ox >= p.Wa) continue;
+                const long m = ((long)img * p.Ha + oy) * p.Wa + ox;
                 float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) {
@@ -306,9 +315,9 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
                 const int ml = wm * WTM + rsub + k * RPP;
                 const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
                 mkv[k] = uint4{0u, 0u, 0u, 0u};
-                if (oy < p.OH && ox < p.OW && col0 < p.N)
+                if (oy < p.Ha && ox < p.Wa && col0 < p.N)
                     mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
-                                                             ((long)oy * p.OW + ox) * e.ld_mask + col0);
+                                                             halo_opix(p, oy, ox) * e.ld_mask + col0);
             }
         }
     }
@@ -339,8 +348,8 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
         const int rr = rsub + k * RPP;
         const int ml = wm * WTM + rr;
         const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-        if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
-        const long pix = (long)oy * p.OW + ox;
+        if (oy >= p.Ha || ox >= p.Wa || col0 >= p.N) continue;
+        const long pix = halo_opix(p, oy, ox);
         float v[8];
         splitk_lds8(wbuf + rr * SROW + cch * 32, v);
         float res[8], mk[8];
@@ -544,9 +553,9 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                 const int ml = wm * WTM + hh * HR + rsub + k * RPP;
                 const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
                 mkv[k] = uint4{0u, 0u, 0u, 0u};
-                if (oy < p.OH && ox < p.OW && col0 < p.N)
+                if (oy < p.Ha && ox < p.Wa && col0 < p.N)
                     mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
-                                                             ((long)oy * p.OW + ox) * e.ld_mask + col0);
+                                                             halo_opix(p, oy, ox) * e.ld_mask + col0);
             }
         }
         lds_barrier();
@@ -573,8 +582,8 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
             const int rr = rsub + k * RPP;
             const int ml = wm * WTM + hh * HR + rr;
             const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
-            const long pix = (long)oy * p.OW + ox;
+            if (oy >= p.Ha || ox >= p.Wa || col0 >= p.N) continue;
+            const long pix = halo_opix(p, oy, ox);
             float v[8];
             splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8], mk[8];
@@ -822,8 +831,8 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             for (int r = 0; r < 4; ++r) {
                 const int ml = wm * 128 + mi * 16 + fg * 4 + r;
                 const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-                if (oy >= p.OH || ox >= p.OW) continue;
-                const long m = ((long)img * p.OH + oy) * p.OW + ox;
+                if (oy >= p.Ha || ox >= p.Wa) continue;
+                const long m = ((long)img * p.Ha + oy) * p.Wa + ox;
                 float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < 2 * NFH; ++ni) {
@@ -858,9 +867,9 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         const int ml = wm * 128 + mh * 64 + rsub + k * RPP;
         const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
         mkv[k] = uint4{0u, 0u, 0u, 0u};
-        if (oy < p.OH && ox < p.OW && col0 < p.N)
+        if (oy < p.Ha && ox < p.Wa && col0 < p.N)
             mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
-                                                     ((long)oy * p.OW + ox) * e.ld_mask + col0);
+                                                     halo_opix(p, oy, ox) * e.ld_mask + col0);
     };
     if (e.mask) {
 #pragma unroll
@@ -897,8 +906,8 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 Chunk<T>::unpack(mkv[k], mk);
                 if (mh == 0) load_mask(1, k);
             }
-            if (oy >= p.OH || ox >= p.OW || col0 >= p.N) continue;
-            const long pix = (long)oy * p.OW + ox;
+            if (oy >= p.Ha || ox >= p.Wa || col0 >= p.N) continue;
+            const long pix = halo_opix(p, oy, ox);
             float v[8];
             splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8];

@@ -474,7 +474,7 @@ def test_c3_end_to_end_logits_image0(c3):
 # per-variable worst relative L2 of the bf16 step's gradients vs the oracle
 # with bf16 rounding points (measured values in each test's docstring)
 C2_WORST_REL_L2 = 0.05     # measured 1.13e-2 (conv4_1/weights, round 4)
-C3_WORST_REL_L2 = 0.25
+C3_WORST_REL_L2 = 0.1      # measured 2.46e-2 (denseblock6 layer 3 conv2, bench plan, round 4)
 
 
 @pytest.mark.timeout(1200)
