@@ -552,6 +552,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res64", &seg::g_res64, 0, 1, 1, {}},
         {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
+        {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
 #ifdef SEG_DIAG
         {"tn3_abl", &seg::g_tn3_abl, 0, 3, 1, {}},

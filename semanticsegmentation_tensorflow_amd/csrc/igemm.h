@@ -284,6 +284,10 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 extern int g_smallc;
 bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil);
 void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s);
+// single-tap NT with K <= 16 (a classifier head's input gradient): streaming kernel
+extern int g_smallk;
+bool smallk_ok(const NTParams& p, int dtype);
+void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s);
 bool smallc_wgrad_ok(const TNParams& p, int dtype);
 int smallc_wgrad_splits(const TNParams& p, int cus);
 void launch_smallc_wgrad(TNParams& p, int dtype, int splits, hipStream_t s);

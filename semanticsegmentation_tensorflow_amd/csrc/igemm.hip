@@ -745,7 +745,7 @@ static void launch_nt_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
 // The ONE kernel decision for an NT problem: launch_nt_typed launches the
 // plan, nt_choice names it, nt_pool_ok reads its pooled-epilogue flag, so the
 // host-side checks and the launch can never disagree.
-enum NTKind { NTK_PRO2, NTK_PRO_REG, NTK_RES16C, NTK_RES64, NTK_HALO, NTK_NT3, NTK_NT3_NSPLIT, NTK_NT2, NTK_REG };
+enum NTKind { NTK_SMALLK, NTK_PRO2, NTK_PRO_REG, NTK_RES16C, NTK_RES64, NTK_HALO, NTK_NT3, NTK_NT3_NSPLIT, NTK_NT2, NTK_REG };
 struct NTPlan {
     int kind, bm, bn, splits;
     HaloPlan hp;
@@ -758,6 +758,11 @@ static NTPlan nt_plan(const NTParams& p, int dtype, int nphases, int max_m) {
     const int bk = dtype == SEG_F32 ? 32 : 64;
     choose_nt(max_m, p.N, p.K, bk, pl.bm, pl.bn, pl.splits);
     if (nphases > 1) pl.splits = 1;
+    if (h16 && nphases == 1 && smallk_ok(p, dtype)) {
+        pl.kind = NTK_SMALLK;
+        pl.bm = 1; pl.bn = 8; pl.splits = 1;
+        return pl;
+    }
     if (p.pro.gamma) {
         if (g_nt_variant == 2 && nt2_pro_ok(p, dtype, nphases)) {   // 1x1: K <= 1024, no split-K
             pl.kind = NTK_PRO2;
@@ -837,6 +842,10 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     int splits = pl.splits;
     p.partial = nullptr;
     switch (pl.kind) {
+        case NTK_SMALLK:
+            launch_smallk(p, dt_traits<T>::id, num_cus(), s);
+            SEG_CHECK_LAUNCH();
+            return SEG_OK;
         case NTK_PRO2:
             launch_nt2_pro(p, dt_traits<T>::id, 1, max_m, s);
             SEG_CHECK_LAUNCH();
@@ -952,6 +961,7 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
     const NTPlan pl = nt_plan(p, dtype, nphases, max_m);
     *bm = pl.bm; *bn = pl.bn; *splits = pl.splits;
     switch (pl.kind) {
+        case NTK_SMALLK: return "smallk_nt";
         case NTK_PRO2: return "igemm_nt2_pro";
         case NTK_PRO_REG: return "igemm_nt_pro";
         case NTK_RES16C: return "conv_res16c";

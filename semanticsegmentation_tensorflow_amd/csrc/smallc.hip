@@ -146,6 +146,98 @@ void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s) {
     else launch_smallc_fwd_t<bf16>(p, s);
 }
 
+// ---------------------------------------------------------------------------
+// Single-tap NT problems with a reduction of K <= 16: y[m][n] =
+// epilogue(sum_k x[m][k] w[n][k]).  The input gradient of a classifier head
+// over a few classes (FC-DenseNet final_conv 256 -> 2, Network/model/
+// FCDenseNet.py:160: dx[3.8 M px][256] from dlogits[.][2]) is a pure write
+// stream -- 2 B read per 256 B written -- that the 256 x 64 tile kernel ran
+// at 1.6 TB/s.  Here a thread owns 8 consecutive columns of one pixel
+// (consecutive threads walk the columns: 16-byte stores, 8 threads per 128 B),
+// the filter sits in LDS as fp32 [n][k], the sum runs in k order, and the
+// epilogue is igemm_nt2's (bias, BN affine, ReLU, dropout, residual, ReluGrad).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int SK_MAXK = 16, SK_MAXN = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
+    __shared__ float wsm[SK_MAXN * SK_MAXK];
+    const int K = p.K;
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
+    for (int i = threadIdx.x; i < p.N * K; i += 256) {
+        const int n = i / K, k = i - (i / K) * K;
+        wsm[n * SK_MAXK + k] = to_f32(Wt[(long)n * p.w_col + k]);
+    }
+    __syncthreads();
+    const EpiParams& e = p.epi;
+    const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+    const int CK = p.N / 8;
+    const long hw = (long)p.OH * p.OW;
+    const long total = (long)p.M * CK;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long m = i / CK;
+        const int col0 = (int)(i - m * CK) * 8;
+        const long img = m / hw, pix = m - img * hw;
+        float xv[SK_MAXK];
+        const T* xr = X + img * p.x_img + pix * p.ldx;
+#pragma unroll
+        for (int q = 0; q < SK_MAXK / 8; ++q) {
+            if (q * 8 < K) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xr + q * 8), xv + q * 8);
+            else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[q * 8 + j] = 0.f;
+            }
+        }
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float* wr = wsm + (col0 + j) * SK_MAXK;
+            float a = 0.f;
+            for (int k = 0; k < K; ++k) a += xv[k] * wr[k];
+            v[j] = a;
+        }
+        float res[8], mk[8];
+        if (e.residual) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
+                            reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0), res);
+        if (e.mask) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
+                        reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0), mk);
+        const uint64_t gidx = ((uint64_t)m) * e.n_valid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = col0 + j;
+            const bool cv = col < e.n_valid;
+            const float sc = (e.scale && cv) ? e.scale[col] : 1.f, sh = (e.shift && cv) ? e.shift[col] : 0.f;
+            float x = v[j] * sc + sh + ((e.bias && cv) ? e.bias[col] : 0.f);
+            if (e.relu) x = fmaxf(x, 0.f);
+            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+            if (e.residual) x += res[j];
+            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+            v[j] = cv ? x : 0.f;
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) = Chunk<T>::pack(v);
+    }
+}
+}  // namespace
+
+int g_smallk = 1;
+
+bool smallk_ok(const NTParams& p, int dtype) {
+    return g_smallk && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.taps_w == 1 && p.K == p.C &&
+           p.K <= SK_MAXK && p.K > 0 && p.N % 8 == 0 && p.N <= SK_MAXN && p.ish == 1 && p.isw == 1 && p.ioh == 0 &&
+           p.iow == 0 && p.osh == 1 && p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.IH == p.Ha && p.IW == p.Wa &&
+           p.OH == p.Ha && p.OW == p.Wa && p.M > 0 && p.M % (p.OH * p.OW) == 0 && p.ldx % 8 == 0 &&
+           p.ldy % 8 == 0 && !p.pro.gamma && !p.epi.bn_x && !p.epi.pool_y && !p.epi.y2 &&
+           (!p.epi.residual || p.epi.ld_res % 8 == 0) && (!p.epi.mask || p.epi.ld_mask % 8 == 0);
+}
+
+void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s) {
+    const long total = (long)p.M * (p.N / 8);
+    const int grid = (int)std::min<long>((total + 255) / 256, (long)cus * 16);
+    if (dtype == SEG_F16) hipLaunchKernelGGL(smallk_nt_k<f16>, dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(smallk_nt_k<bf16>, dim3(grid), dim3(256), 0, s, p);
+}
+
 
 // ---------------------------------------------------------------------------
 // Filter gradient of the same layer: dW[r][s][c][n] = sum_p x[p + (r,s)][c] dz[p][n]
