@@ -173,6 +173,33 @@ typedef struct seg_bn_bwd {
     uint64_t seed;
 } seg_bn_bwd;
 size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d);
+/* The same launch with the dgamma / dbeta reduction left to the caller:
+ * the per-tile partial column sums go to `part` ([seg_conv_bwd_data_bn_part_rows(d)]
+ * rows of 2*C fp32: C dgamma partials (unscaled) then C dbeta partials); bn->dgamma /
+ * dbeta are not written.  Finish many of them at once with
+ * seg_bn_grad_finish_batch (a step's BN backward sums in two launches). */
+long seg_conv_bwd_data_bn_part_rows(const seg_conv_desc* d);
+int seg_conv2d_bwd_data_bn_part(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_bn_bwd* bn,
+                                void* dx, float* part, void* stream);
+typedef struct seg_bn_finish_segment {
+    const float* part;      /* [nrows][2*C] partial rows */
+    int nrows, C, cv;
+    float inv;              /* 1 / sqrt(1 + eps): dgamma = inv * sum */
+    float* dgamma;
+    float* dbeta;
+    /* filled by seg_bn_finish_batch_plan */
+    float* scratch;
+    int a_blk0, a_nblk, b_blk0, b_nblk;
+} seg_bn_finish_segment;
+/* Host-side plan: fills the launch offsets and scratch pointers of segs[]
+ * (scratch carved from `scratch`, may be NULL to size it) and returns the
+ * scratch bytes; *a_blocks / *b_blocks: the two launches' grids. */
+size_t seg_bn_finish_batch_plan(seg_bn_finish_segment* segs, int nsegs, float* scratch, int* a_blocks,
+                                int* b_blocks);
+/* dgamma / dbeta of every segment (dev_segs: the planned array in device
+ * memory), bit-identical to seg_conv2d_bwd_data_bn's own finish. */
+int seg_bn_grad_finish_batch(const seg_bn_finish_segment* dev_segs, int nsegs, int a_blocks, int b_blocks,
+                             void* stream);
 int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_bn_bwd* bn,
                            void* dx, void* ws, size_t ws_bytes, void* stream);
 int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,

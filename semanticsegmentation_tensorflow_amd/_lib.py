@@ -113,6 +113,13 @@ class SegBnBwd(ctypes.Structure):
                 ("keep_prob", ctypes.c_float), ("seed", ctypes.c_uint64)]
 
 
+class SegBnFinishSegment(ctypes.Structure):
+    _fields_ = [("part", ctypes.c_void_p), ("nrows", ctypes.c_int), ("C", ctypes.c_int), ("cv", ctypes.c_int),
+                ("inv", ctypes.c_float), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("scratch", ctypes.c_void_p), ("a_blk0", ctypes.c_int), ("a_nblk", ctypes.c_int),
+                ("b_blk0", ctypes.c_int), ("b_nblk", ctypes.c_int)]
+
+
 class SegAdamFused(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
                 ("rows_dst", ctypes.c_void_p), ("rows_ap", ctypes.c_int), ("rows_bp", ctypes.c_int),
@@ -143,6 +150,10 @@ SIGNATURES = {
     "seg_conv2d_fwd_bn2_ok": (_I, [_DP, _I]),
     "seg_conv_bwd_data_bn_workspace": (_Z, [_DP]),
     "seg_conv2d_bwd_data_bn": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _Z, _P]),
+    "seg_conv_bwd_data_bn_part_rows": (_L, [_DP]),
+    "seg_conv2d_bwd_data_bn_part": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _P]),
+    "seg_bn_finish_batch_plan": (_Z, [_P, _I, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "seg_bn_grad_finish_batch": (_I, [_P, _I, _I, _I, _P]),
     "seg_conv2d_bwd_filter_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _P, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_filter": (_I, [_DP, _P, _P, _P, _P, _P, _Z, _P]),
     "seg_tconv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),

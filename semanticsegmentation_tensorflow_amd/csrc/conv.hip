@@ -783,21 +783,25 @@ extern "C" size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d) {
     return (size_t)bwd_data_bn_rows(d, p, kind) * 2 * d->C * sizeof(float) + seg::bn_grad_finish_scratch(d->C);
 }
 
-extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w, const seg_bn_bwd* bn,
-                                      void* dx, void* ws, size_t ws_bytes, void* stream) {
+extern "C" long seg_conv_bwd_data_bn_part_rows(const seg_conv_desc* d) {
+    NTParams p;
+    const int kind = bwd_data_bn_params(d, p);
+    return kind ? bwd_data_bn_rows(d, p, kind) : 0;
+}
+
+// The input-gradient launch through the BN backward; its dgamma / dbeta
+// column sums left as partial rows [nrows][2 C] in `part`.
+static int bwd_data_bn_launch(const seg_conv_desc* d, const void* dy, const void* w, const seg_bn_bwd* bn, void* dx,
+                              float* part, void* stream, long* rows_out) {
     NTParams p;
     const int kind = bwd_data_bn_params(d, p);
     if (!kind) return SEG_EINVAL;
-    if (!dy || !w || !dx || !bn || !bn->x || !bn->gamma || !bn->beta || !bn->dgamma || !bn->dbeta) return SEG_EINVAL;
+    if (!dy || !w || !dx || !bn || !bn->x || !bn->gamma || !bn->beta || !part) return SEG_EINVAL;
     if (bn->ldx % 8 || bn->ldx < d->C) return SEG_EINVAL;
     const bool drop = bn->keep_prob > 0.f && bn->keep_prob < 1.f;
     if ((drop || kind == 2) && bn->accumulate) return SEG_EINVAL;   // the 3x3 / dropout forms write dx
     if (drop && kind != 2) return SEG_EINVAL;
-    const size_t need = seg_conv_bwd_data_bn_workspace(d);
-    if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
-    const long nrows = bwd_data_bn_rows(d, p, kind);
-    float* part = reinterpret_cast<float*>(ws);
-    float* scratch = part + nrows * 2 * d->C;
+    *rows_out = bwd_data_bn_rows(d, p, kind);
     p.x = dy; p.w = w; p.y = dx;
     const float inv = 1.0f / sqrtf(1.0f + bn->eps);
     seg::EpiParams& e = p.epi;
@@ -818,7 +822,28 @@ extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, co
     if (kind == 1) seg::launch_nt2_bn(p, d->dtype, s);
     else seg::launch_res16c_bn(p, seg::device_cus(), s, d->dtype);
     SEG_CHECK_LAUNCH();
-    return seg::bn_grad_finish(part, (int)nrows, d->C, d->c_valid, inv, bn->dgamma, bn->dbeta, scratch, s);
+    return SEG_OK;
+}
+
+extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w, const seg_bn_bwd* bn,
+                                      void* dx, void* ws, size_t ws_bytes, void* stream) {
+    if (!bn || !bn->dgamma || !bn->dbeta) return SEG_EINVAL;
+    const size_t need = seg_conv_bwd_data_bn_workspace(d);
+    if (!need) return SEG_EINVAL;
+    if (!ws || ws_bytes < need) return SEG_EWORKSPACE;
+    float* part = reinterpret_cast<float*>(ws);
+    long nrows = 0;
+    int st = bwd_data_bn_launch(d, dy, w, bn, dx, part, stream, &nrows);
+    if (st) return st;
+    float* scratch = part + nrows * 2 * d->C;
+    return seg::bn_grad_finish(part, (int)nrows, d->C, d->c_valid, 1.0f / sqrtf(1.0f + bn->eps), bn->dgamma,
+                               bn->dbeta, scratch, (hipStream_t)stream);
+}
+
+extern "C" int seg_conv2d_bwd_data_bn_part(const seg_conv_desc* d, const void* dy, const void* w,
+                                           const seg_bn_bwd* bn, void* dx, float* part, void* stream) {
+    long nrows = 0;
+    return bwd_data_bn_launch(d, dy, w, bn, dx, part, stream, &nrows);
 }
 
 extern "C" int seg_conv2d_bwd_filter(const seg_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias,

@@ -1555,4 +1555,98 @@ int bn_grad_finish(const float* part, int nrows, int C, int cv, float inv, float
     return SEG_OK;
 }
 
+
+// ---- many BN backward finishes in two launches (seg_bn_grad_finish_batch):
+// the same two stages and summation order as bn_grad_finish per segment
+__device__ __forceinline__ int bnb_seg(const seg_bn_finish_segment* sg, int n, int b, bool stage_a) {
+    int s = 0;
+    for (int i = 1; i < n; ++i)
+        if ((stage_a ? sg[i].a_blk0 : sg[i].b_blk0) <= b) s = i;
+    return s;
+}
+
+__global__ __launch_bounds__(256) void bn_fold_batch_k(const seg_bn_finish_segment* __restrict__ sg, int n) {
+    __shared__ int ss;
+    if (threadIdx.x == 0) ss = bnb_seg(sg, n, blockIdx.x, true);
+    __syncthreads();
+    const seg_bn_finish_segment& g = sg[ss];
+    const int local = blockIdx.x - g.a_blk0;
+    const int cbs = (2 * g.C + 255) / 256;
+    const int gi = local / cbs, cb = local - gi * cbs;
+    const int width = 2 * g.C;
+    const int c = cb * 256 + threadIdx.x;
+    if (c >= width) return;
+    float s = 0.f;
+    for (int r = gi; r < g.nrows; r += kBnFinishGroups) s += g.part[(long)r * width + c];
+    g.scratch[(long)gi * width + c] = s;
+}
+
+__global__ __launch_bounds__(256) void bn_finish_batch_k(const seg_bn_finish_segment* __restrict__ sg, int n) {
+    __shared__ int ss;
+    __shared__ float sgm[32][9], sbt[32][9];
+    if (threadIdx.x == 0) ss = bnb_seg(sg, n, blockIdx.x, false);
+    __syncthreads();
+    const seg_bn_finish_segment& g = sg[ss];
+    const float* part = g.nrows > kBnFinishGroups ? g.scratch : g.part;
+    const int nrows = g.nrows > kBnFinishGroups ? kBnFinishGroups : g.nrows;
+    const int C = g.C;
+    const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    const int k = (blockIdx.x - g.b_blk0) * 8 + cl;
+    float a = 0.f, b = 0.f;
+    if (k < g.cv)
+        for (int r = rg; r < nrows; r += 32) {
+            a += part[(long)r * 2 * C + k];
+            b += part[(long)r * 2 * C + C + k];
+        }
+    sgm[rg][cl] = a;
+    sbt[rg][cl] = b;
+    __syncthreads();
+    if (threadIdx.x < 8 && k < g.cv) {
+        float tg = 0.f, tb = 0.f;
+        for (int r = 0; r < 32; ++r) {
+            tg += sgm[r][cl];
+            tb += sbt[r][cl];
+        }
+        g.dgamma[k] = tg * g.inv;
+        g.dbeta[k] = tb;
+    }
+}
+
 }  // namespace seg
+
+extern "C" size_t seg_bn_finish_batch_plan(seg_bn_finish_segment* segs, int nsegs, float* scratch, int* a_blocks,
+                                           int* b_blocks) {
+    size_t bytes = 0;
+    int a = 0, b = 0;
+    for (int i = 0; i < nsegs; ++i) {
+        seg_bn_finish_segment& g = segs[i];
+        g.a_blk0 = a;
+        g.a_nblk = 0;
+        g.scratch = nullptr;
+        if (g.nrows > seg::kBnFinishGroups) {
+            g.a_nblk = ((2 * g.C + 255) / 256) * seg::kBnFinishGroups;
+            g.scratch = scratch ? reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + bytes) : nullptr;
+            bytes += (size_t)seg::kBnFinishGroups * 2 * g.C * sizeof(float);
+        }
+        a += g.a_nblk;
+        g.b_blk0 = b;
+        g.b_nblk = (g.cv + 7) / 8;
+        b += g.b_nblk;
+    }
+    if (a_blocks) *a_blocks = a;
+    if (b_blocks) *b_blocks = b;
+    return bytes;
+}
+
+extern "C" int seg_bn_grad_finish_batch(const seg_bn_finish_segment* dev_segs, int nsegs, int a_blocks, int b_blocks,
+                                        void* stream) {
+    if (!dev_segs || nsegs <= 0 || b_blocks <= 0) return SEG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (a_blocks > 0) {
+        hipLaunchKernelGGL(seg::bn_fold_batch_k, dim3(a_blocks), dim3(256), 0, s, dev_segs, nsegs);
+        SEG_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(seg::bn_finish_batch_k, dim3(b_blocks), dim3(256), 0, s, dev_segs, nsegs);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}

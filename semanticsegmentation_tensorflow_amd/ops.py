@@ -10,10 +10,11 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
-from ._lib import SegBnBwd, SegConvDesc, SegEpilogue, SegKernelError, SegPrologue, check
+from ._lib import SegBnBwd, SegBnFinishSegment, SegConvDesc, SegEpilogue, SegKernelError, SegPrologue, check
 
 F32, BF16, F16 = 0, 1, 2
 _TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
@@ -238,6 +239,56 @@ def conv2d_bwd_data_bn(desc, dy, w_hwio, x, gamma, beta, dx, dgamma, dbeta, eps=
     check(_lib.lib().seg_conv2d_bwd_data_bn(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(bn), ptr(dx),
                                             wsp, wss, stream_ptr(stream)), "conv2d_backprop_input_bn")
     return dx
+
+
+def conv_bwd_data_bn_part_rows(desc):
+    """Partial rows conv2d_bwd_data_bn_part writes (0: the fused form does not apply)."""
+    return int(_lib.lib().seg_conv_bwd_data_bn_part_rows(ctypes.byref(desc)))
+
+
+def conv2d_bwd_data_bn_part(desc, dy, w_hwio, x, gamma, beta, dx, part, eps=1e-3, relu=True, accumulate=False,
+                            stream=None, dropout=None):
+    """conv2d_bwd_data_bn with the dgamma / dbeta sums left as partial rows in
+    `part` (fp32, conv_bwd_data_bn_part_rows(desc) x 2 C): finish them with
+    BnFinishBatch (seg_conv2d_bwd_data_bn_part)."""
+    d = _with_ld(desc, dx, dy)
+    kp, seed = dropout if dropout is not None else (1.0, 0)
+    bn = SegBnBwd(x.data_ptr(), pixel_stride(x), gamma.data_ptr(), beta.data_ptr(), float(eps), 1 if relu else 0,
+                  1 if accumulate else 0, None, None, float(kp), int(seed) & (2 ** 64 - 1))
+    check(_lib.lib().seg_conv2d_bwd_data_bn_part(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(bn), ptr(dx),
+                                                 ptr(part), stream_ptr(stream)), "conv2d_backprop_input_bn")
+    return dx
+
+
+class BnFinishBatch:
+    """dgamma / dbeta of many BatchNorm backward launches (partial rows left
+    by conv2d_bwd_data_bn_part) in two kernel launches (seg_bn_grad_finish_batch).
+    segments: [(part, nrows, C, c_valid, eps, dgamma, dbeta)] with fp32 tensors;
+    the segment table and the fold scratch live on the device for reuse."""
+
+    def __init__(self, segments, device):
+        n = len(segments)
+        arr = (SegBnFinishSegment * n)()
+        self._keep = [(s[0], s[5], s[6]) for s in segments]
+        for i, (part, nrows, C, cv, eps, dg, db) in enumerate(segments):
+            arr[i].part, arr[i].nrows, arr[i].C, arr[i].cv = part.data_ptr(), int(nrows), int(C), int(cv)
+            # 1.0f / sqrtf(1.0f + eps) in fp32, as the C-ABI's own finish
+            arr[i].inv = float(np.float32(1.0) / np.sqrt(np.float32(1.0) + np.float32(eps)))
+            arr[i].dgamma, arr[i].dbeta = dg.data_ptr(), db.data_ptr()
+        a, b = ctypes.c_int(0), ctypes.c_int(0)
+        lib = _lib.lib()
+        need = lib.seg_bn_finish_batch_plan(ctypes.cast(arr, ctypes.c_void_p), n, None, ctypes.byref(a), ctypes.byref(b))
+        self.scratch = torch.empty(max(1, need // 4), dtype=torch.float32, device=device)
+        lib.seg_bn_finish_batch_plan(ctypes.cast(arr, ctypes.c_void_p), n, ctypes.c_void_p(self.scratch.data_ptr()),
+                                     ctypes.byref(a), ctypes.byref(b))
+        raw = bytes(arr)
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.n, self.a_blocks, self.b_blocks = n, a.value, b.value
+        self.key = tuple((s[0].data_ptr(), int(s[1]), s[5].data_ptr()) for s in segments)
+
+    def run(self, stream=None):
+        check(_lib.lib().seg_bn_grad_finish_batch(ptr(self.table), self.n, self.a_blocks, self.b_blocks,
+                                                  stream_ptr(stream)), "bn_grad_finish_batch")
 
 
 def conv2d_bwd_filter_pro(desc, x, pro, dy, dw, ws=None, stream=None, dbias=None):

@@ -205,6 +205,10 @@ class Session:
         self.fuse_pool = True
         # conv -> BatchNorm(+ReLU): the BN output written by the conv epilogue
         self.fuse_bn_out = True
+        # the dgamma / dbeta sums of the BN backwards fused into input-gradient
+        # launches finished together at the end of backward (two launches per
+        # step instead of one or two per BatchNorm; single-process steps)
+        self.defer_bn_finish = True
         self._red = None                 # (side stream, compute stream) during a step
         # deferred filter gradients: the kernel too (not only its reduction) on
         # the side stream (1), and the fused filter-gradient + Adam launches (2)
@@ -1492,6 +1496,19 @@ class Session:
 
         ginit = set()      # aliased-concat roots whose gradient buffer holds data this step
 
+        # deferred BN-backward finishes: (segment, variable names) per fused launch
+        bn_defer = ([] if (self.defer_bn_finish and self._dpa is None and self._adam_ctx is None
+                           and self.device.type == "cuda") else None)
+
+        def bn_part(n):
+            """Persistent partial-row buffer of node n's fused BN backward."""
+            t = p.tmp.get(("bnpart", id(n)))
+            if t is None:
+                t = torch.empty(max(1, ops.conv_bwd_data_bn_part_rows(n.desc)) * 2 * n.desc.C,
+                                dtype=torch.float32, device=self.device)
+                p.tmp[("bnpart", id(n))] = t
+            return t
+
         def adest(t):
             """Slice of the root's gradient buffer for aliased t, and whether the
             kernel must accumulate into it (False only for the first write
@@ -1599,14 +1616,23 @@ class Session:
                     if self.capture is not None:
                         bnb = {"xb": buf[id(xb)], "gamma": gn, "beta": bn_, "eps": pro.eps, "relu": pro.relu,
                                "base": dxb.clone() if accf else None, "drop": None, "folded": True}
-                    self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
-                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
-                                store.param(bn_), dxb, gdst(gn), gdst(bn_), pro.eps, pro.relu, accf, ws)
+                    if bn_defer is not None:
+                        part = bn_part(n)
+                        self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn_part, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                    store.param(bn_), dxb, part, pro.eps, pro.relu, accf)
+                        bn_defer.append(((part, ops.conv_bwd_data_bn_part_rows(n.desc), n.desc.C, n.desc.c_valid,
+                                          pro.eps, gdst(gn), gdst(bn_)), [gn, bn_]))
+                    else:
+                        self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                    store.param(bn_), dxb, gdst(gn), gdst(bn_), pro.eps, pro.relu, accf, ws)
                     if bnb is not None:
                         bnb["dxb"] = dxb.clone()
                         bnb["kernel"] = ops.conv_kernel_info(n.desc, ops.OP_BWD_DATA_BN)[0]
                     done(dxb, acc)
-                    self._grad_ready([gn, bn_])
+                    if bn_defer is None:
+                        self._grad_ready([gn, bn_])
                 elif (id(x) in ng and id(n) in p.bn_before and self.fuse_bn_bwd
                       and id(p.bn_before[id(n)].inputs[0]) in ng and id(p.bn_before[id(n)].inputs[0]) not in p.alias
                       and id(p.bn_before[id(n)].inputs[0]) not in grad
@@ -1620,16 +1646,25 @@ class Session:
                     drop = (c1.kp_val, c1.seed_val) if (c1 is not None and c1.kp_val is not None
                                                          and c1.kp_val < 1.0) else None
                     gn, bn_ = b.gamma.var_name, b.beta.var_name
-                    self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
-                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
-                                store.param(bn_), dxb, gdst(gn), gdst(bn_), b.eps, b.relu, False, ws,
-                                None, drop)
+                    if bn_defer is not None:
+                        part = bn_part(n)
+                        self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn_part, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                    store.param(bn_), dxb, part, b.eps, b.relu, False, None, drop)
+                        bn_defer.append(((part, ops.conv_bwd_data_bn_part_rows(n.desc), n.desc.C, n.desc.c_valid,
+                                          b.eps, gdst(gn), gdst(bn_)), [gn, bn_]))
+                    else:
+                        self._timed(n.desc, ops.OP_BWD_DATA_BN, ops.conv2d_bwd_data_bn, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0], buf[id(xb)], store.param(gn),
+                                    store.param(bn_), dxb, gdst(gn), gdst(bn_), b.eps, b.relu, False, ws,
+                                    None, drop)
                     if self.capture is not None:
                         bnb = {"xb": buf[id(xb)], "gamma": gn, "beta": bn_, "eps": b.eps, "relu": b.relu,
                                "base": None, "drop": drop, "folded": False, "dxb": dxb.clone(),
                                "kernel": ops.conv_kernel_info(n.desc, ops.OP_BWD_DATA_BN)[0]}
                     done(dxb, acc)
-                    self._grad_ready([gn, bn_])
+                    if bn_defer is None:
+                        self._grad_ready([gn, bn_])
                 elif id(x) in ng and id(x) in p.alias:
                     # the input is an aliased concat root (FC-DenseNet decoder
                     # concat views): the input gradient lands in the shared
@@ -1919,6 +1954,17 @@ class Session:
                 continue
             else:
                 raise NotImplementedError(f"backward of {k}")
+        if bn_defer:
+            # every deferred dgamma / dbeta in two launches (the same sums as
+            # each launch's own finish); the segment table is built once per plan
+            segs = [s for s, _ in bn_defer]
+            key = tuple((s[0].data_ptr(), int(s[1]), s[5].data_ptr()) for s in segs)
+            batch = getattr(p, "bn_batch", None)
+            if batch is None or batch.key != key:
+                batch = ops.BnFinishBatch(segs, self.device)
+                p.bn_batch = batch
+            batch.run()
+            self._grad_ready([nm for _, names in bn_defer for nm in names])
 
     def _grads_finite(self):
         """All gradients finite (every rank's, under data parallelism)?  One

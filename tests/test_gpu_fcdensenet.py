@@ -94,3 +94,32 @@ def test_fcdensenet_bf16_dropout_trains(dev):
         losses.append(float(l))
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0], losses
+
+
+def test_fcdensenet_bf16_deferred_bn_finish_bit_identical(dev):
+    """The step's dgamma / dbeta finished together at the end of backward
+    (Session.defer_bn_finish: one segment table, two launches) equal the
+    per-launch finishes bit for bit -- every gradient and the Adam step, at
+    keep_prob 0.2 (the folded BN backwards of both the 1x1 and the growth
+    convs)."""
+    N, H, W = 2, 64, 96
+    image, labels, keep, pred, logits, loss, train_step = build(H, W)
+    weights = densenet_weights(M.fcdensenet_param_shapes(3, 2), 11, keep_prob=0.2)
+    img, lab = synthetic_batch(N, H, W, 12)
+    out = []
+    for defer in (True, False):
+        sess = tf.Session(compute_dtype="bf16", seed=3)
+        sess.defer_bn_finish = defer
+        sess.run(tf.global_variables_initializer())
+        for k, v in weights.items():
+            sess.assign(k, v)
+        sess.run(train_step, feed_dict={image: img, labels: lab, keep: 0.2})
+        torch.cuda.synchronize()
+        out.append({k: (sess.store.grad(k).cpu().clone(), torch.from_numpy(sess.variable_value(k)))
+                    for k in weights})
+    a, b = out
+    gammas = [k for k in a if k.endswith("gamma")]
+    assert len(gammas) >= 100
+    for k in a:
+        assert torch.equal(a[k][0], b[k][0]), k
+        assert torch.equal(a[k][1], b[k][1]), k
