@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--keep-prob", type=float, default=None,
                     help="fcn 0.8 (FCN.py:395), fcdensenet 0.2 (FCDenseNet.py:13)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--dp-mode", default="allreduce", choices=["allreduce", "zero"],
+                    help="gradient exchange at N > 1: all-reduce + every rank's Adam (default: the shorter "
+                         "post-backward critical path, DESIGN.md section 6) or ZeRO-1 (reduce-scatter, "
+                         "sharded Adam, all-gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 side lines")
@@ -596,10 +600,12 @@ def dp_probe(args, B, H, W, kp, device):
     import torch.distributed as dist
     from semanticsegmentation_tensorflow_amd.dp import DataParallel
     init_rccl(device)
-    dp = DataParallel(bucket_mb=args.bucket_mb, force_collectives=True)
+    dp = DataParallel(bucket_mb=args.bucket_mb, force_collectives=True, shard_optimizer=args.dp_mode == "zero")
     m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, 0)
+    exchange = ("zero1 (reduce-scatter, sharded Adam, all-gather)" if args.dp_mode == "zero"
+                else "all-reduce per bucket during backward, every rank's Adam")
     return {"backend": dist.get_backend(), "world": dist.get_world_size(), "bucket_mb": args.bucket_mb,
-            "buckets": len(dp.buckets), "exchange": "zero1 (reduce-scatter, sharded Adam, all-gather)",
+            "buckets": len(dp.buckets), "exchange": exchange,
             "value": round(m["value"], 3), "unit": "images/s", "ms_per_step": round(m["ms_per_step"], 3),
             "note": "same workload as the headline; collectives forced on at world 1 (a real world-1 job "
                     "skips them and runs the single-process plan)"}
@@ -619,7 +625,7 @@ def main():
     if world > 1 or args.force_dp:
         init_rccl(device)
         from semanticsegmentation_tensorflow_amd.dp import DataParallel
-        dp = DataParallel(bucket_mb=args.bucket_mb)
+        dp = DataParallel(bucket_mb=args.bucket_mb, shard_optimizer=args.dp_mode == "zero")
 
     from semanticsegmentation_tensorflow_amd import ops
     for kv in args.option:
@@ -668,6 +674,7 @@ def main():
             "batch_per_gpu": B,
             "image": f"{H}x{W} -> {HP}x{WP}",
             "parallelism": f"dp{world}",
+            "dp_mode": args.dp_mode if world > 1 else None,
             "keep_prob": kp,
         },
         "roofline": m["roofline"],
