@@ -176,11 +176,13 @@ size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d);
 /* The same launch with the dgamma / dbeta reduction left to the caller:
  * the per-tile partial column sums go to `part` ([seg_conv_bwd_data_bn_part_rows(d)]
  * rows of 2*C fp32: C dgamma partials (unscaled) then C dbeta partials); bn->dgamma /
- * dbeta are not written.  Finish many of them at once with
- * seg_bn_grad_finish_batch (a step's BN backward sums in two launches). */
+ * dbeta are not written.  part_rows must equal seg_conv_bwd_data_bn_part_rows(d)
+ * (the row count a finish plan was made for; SEG_EWORKSPACE otherwise).  Finish
+ * many of them at once with seg_bn_grad_finish_batch (a step's BN backward sums
+ * in two launches). */
 long seg_conv_bwd_data_bn_part_rows(const seg_conv_desc* d);
 int seg_conv2d_bwd_data_bn_part(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_bn_bwd* bn,
-                                void* dx, float* part, void* stream);
+                                void* dx, float* part, long part_rows, void* stream);
 typedef struct seg_bn_finish_segment {
     const float* part;      /* [nrows][2*C] partial rows */
     int nrows, C, cv;

@@ -151,7 +151,7 @@ SIGNATURES = {
     "seg_conv_bwd_data_bn_workspace": (_Z, [_DP]),
     "seg_conv2d_bwd_data_bn": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _Z, _P]),
     "seg_conv_bwd_data_bn_part_rows": (_L, [_DP]),
-    "seg_conv2d_bwd_data_bn_part": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _P]),
+    "seg_conv2d_bwd_data_bn_part": (_I, [_DP, _P, _P, ctypes.POINTER(SegBnBwd), _P, _P, _L, _P]),
     "seg_bn_finish_batch_plan": (_Z, [_P, _I, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "seg_bn_grad_finish_batch": (_I, [_P, _I, _I, _I, _P]),
     "seg_conv2d_bwd_filter_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _P, _P, _P, _Z, _P]),

@@ -551,6 +551,8 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res16", &seg::g_res16, 0, 1, 1, {}},
         {"res64", &seg::g_res64, 0, 1, 1, {}},
         {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
+        {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
+        {"res16c_bh", &seg::g_res16c_bh, 2, 8, 4, {2, 4, 8}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
@@ -841,7 +843,10 @@ extern "C" int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, co
 }
 
 extern "C" int seg_conv2d_bwd_data_bn_part(const seg_conv_desc* d, const void* dy, const void* w,
-                                           const seg_bn_bwd* bn, void* dx, float* part, void* stream) {
+                                           const seg_bn_bwd* bn, void* dx, float* part, long part_rows, void* stream) {
+    const long rows = seg_conv_bwd_data_bn_part_rows(d);
+    if (!rows) return SEG_EINVAL;
+    if (part_rows != rows) return SEG_EWORKSPACE;   // planned for another launch geometry
     long nrows = 0;
     return bwd_data_bn_launch(d, dy, w, bn, dx, part, stream, &nrows);
 }

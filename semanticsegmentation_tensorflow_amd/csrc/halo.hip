@@ -42,6 +42,8 @@ int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 // pooled forward and the ReluGrad-masked input gradient (conv1_2: 191 vs 192
 // and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
 int g_res64_pp = 1;
+int g_res16_dma = 1;
+int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8, 4 or 2)   // 16-wide conv_res64: halo by LDS DMA (two blocks / CU) or VGPR staging
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
@@ -944,19 +946,27 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 // ---------------------------------------------------------------------------
 constexpr int R64_BH = 8, R64_BW = 32, R64_HW = R64_BW + 2, R64_HROWS = (R64_BH + 2) * R64_HW;   // 340
 constexpr int R64_PER = (R64_HROWS * 8 + 511) / 512;                                             // 6
+constexpr int RPP_PIECES = (R64_HROWS + 7) / 8;     // halo LDS-DMA pieces of 8 rows (43: 340 rows used)
 
 // ABL (diagnostics only, garbage results): 1 no halo fetch, 2 no MFMA,
 // 3 no epilogue stores, 4 no LDS fragment reads.
 // NB = output channels per block: 64, or 16 for N <= 16 (FC-DenseNet's
 // growth convs, 64 -> 16): one 16-row filter fragment, all 8 waves along the
 // pixels, a quarter of the MFMAs and a 18 KB filter, so two blocks share a CU.
-template <int ABL = 0, typename T = bf16, int NB = 64>
-__global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+// DMA (NB = 16): the halo comes by LDS DMA into one buffer instead of through
+// 24 prefetch VGPRs per thread -- that register staging held the 16-wide
+// kernel at 145 VGPRs, one block per CU; without it the kernel fits the 128
+// that two resident blocks need, and the other block's MFMAs cover each
+// block's DMA round trip.
+template <int ABL = 0, typename T = bf16, int NB = 64, bool DMA = false>
+__global__ __launch_bounds__(512, NB == 16 ? (DMA ? 4 : 2) : 1) void conv_res64(NTParams p, int tiles_x, int tiles_y,
+                                                                                int ntiles) {
     static_assert(NB == 64 || NB == 16, "output block width");
+    static_assert(!DMA || (NB == 16 && ABL == 0), "the DMA halo is the 16-wide form");
     constexpr int NW = 8, WN = NB == 64 ? 2 : 1, WTM = 256 / (NW / WN), WTN = NB / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int BS = 9 * NB * 128;                 // resident filter
-    constexpr int HS = R64_HROWS * 128;              // halo
+    constexpr int HS = DMA ? RPP_PIECES * 8 * 128 : R64_HROWS * 128;   // halo (DMA: 43 whole 8-row pieces)
     __shared__ __attribute__((aligned(16))) char smem[BS + HS];
     char* Bs = smem;
     char* Hs = smem + BS;
@@ -1011,6 +1021,29 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
             if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 128 + 16 * (c8 ^ (hr & 6))) = hv[k];
         }
     };
+    // DMA: halo piece i = w + 8 k holds rows 8 i .. 8 i + 7; lane -> (row
+    // lane >> 3, LDS chunk lane & 7) = logical chunk (lane & 7) ^ (row & 6)
+    const void* zero = (const void*)halo_zero_page;
+    const unsigned hbase = (unsigned)(uintptr_t)(SEG_LDS char*)smem + BS;
+    auto dma = [&](int t) {
+        const int img = t / tpi;
+        const int rem = t - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
+        const int oy0 = ty * R64_BH + p.ioh + hy0, ox0 = tx * R64_BW + p.iow + hx0;
+        const int lr = lane >> 3;
+        const T* xb = X + (long)img * p.x_img + ((lane & 7) ^ (lr & 6)) * 8;
+#pragma unroll 1
+        for (int k = 0; k < (RPP_PIECES + NW - 1) / NW; ++k) {
+            const int i = w + NW * k;
+            if (i < RPP_PIECES) {
+                const int hr = i * 8 + lr;
+                const int hy = hr / R64_HW, hx = hr - (hr / R64_HW) * R64_HW;
+                const int ih = oy0 + hy, iw = ox0 + hx;
+                const bool ok = hr < R64_HROWS && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+                glds16(ok ? (const void*)(xb + ((long)ih * p.IW + iw) * p.ldx) : zero, hbase + i * 1024);
+            }
+        }
+    };
 
     int rowbase[TM];
 #pragma unroll
@@ -1035,8 +1068,13 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
     }
 
     int t = blockIdx.x;
-    if (t < ntiles) fetch(t);
-    commit();
+    if constexpr (DMA) {
+        if (t < ntiles) dma(t);
+        wait_vmcnt<0>();
+    } else {
+        if (t < ntiles) fetch(t);
+        commit();
+    }
     __syncthreads();
     for (; t < ntiles; t += gridDim.x) {
         const int tn = t + gridDim.x;
@@ -1062,7 +1100,7 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                 }
             }
         }
-        if (tn < ntiles) fetch(tn);                  // in flight during this tile's MFMAs
+        if (!DMA && tn < ntiles) fetch(tn);          // in flight during this tile's MFMAs
         f32x4 acc[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1107,6 +1145,10 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                         acc[mi][ni] = mfma16x16x32<T>(fb[cur][ni], fa[cur][mi], acc[mi][ni]);
                     }
                 }
+        }
+        if constexpr (DMA) {       // every wave is done with the halo: the next one may land
+            __syncthreads();
+            if (tn < ntiles) dma(tn);
         }
         // ---- MaxPool 2x2 / 2 fused (conv1_2 -> pool1, Network/model/FCN.py:56-57): a
         // wave's 64 pixels are image rows 2 wm (mi 0, 1) and 2 wm + 1 (mi 2, 3), so a
@@ -1213,9 +1255,14 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
                 }
             }
         }
-        __syncthreads();                             // all taps read the halo
-        commit();                                    // next tile's halo (waits for its loads)
-        __syncthreads();
+        if constexpr (DMA) {
+            wait_vmcnt<0>();                         // the next halo landed (and this tile's stores left)
+            __syncthreads();
+        } else {
+            __syncthreads();                         // all taps read the halo
+            commit();                                // next tile's halo (waits for its loads)
+            __syncthreads();
+        }
     }
 }
 
@@ -1247,7 +1294,6 @@ __global__ __launch_bounds__(512, NB == 16 ? 2 : 1) void conv_res64(NTParams p, 
 // and reduced to one bit per output (mask > 0) after its MFMAs, so no wait for
 // it lands behind the epilogue phase's DMA (vmcnt retires in issue order).
 // ---------------------------------------------------------------------------
-constexpr int RPP_PIECES = 43;                       // halo DMA pieces (8 rows each, 340 used)
 constexpr int RPP_HS = RPP_PIECES * 8 * 128;         // 44,032 B per halo buffer
 
 template <typename T = bf16>
@@ -1503,17 +1549,25 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
 // conv_res64.  Swizzles: filter rows chunk ^ ((n >> 2) & 3), halo rows
 // chunk ^ ((row >> 3) & 1).
 // ---------------------------------------------------------------------------
-constexpr int R16_PER = (R64_HROWS * 2 + 511) / 512;   // halo chunks per thread (2)
-
 // BNB: the epilogue continues through the BatchNorm(+ReLU) backward of the
 // layer whose output this conv read (EpiParams.bn_*; then the standard
 // dropout fields re-draw the dropout of the conv before that BN), and the
 // block's column sums of dz*x / dz over all its tiles go to bn_part[block].
-template <typename T = bf16, bool BNB = false>
-__global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int tiles_x, int tiles_y, int ntiles) {
+// BH: tile rows (tile BH x 32 px, BH waves of 64 px x 32 channels).  The BNB
+// epilogue (BN-input reads, the dropout hash and the BN sums per element)
+// holds the kernel at 160 VGPRs, three waves per SIMD: 8-row tiles (8-wave
+// blocks) fit one block per CU, 4-row tiles (4-wave blocks) three, and the
+// blocks' epilogues, MFMAs and loads then overlap.
+template <typename T = bf16, bool BNB = false, int BH = 8>
+__global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res16c(NTParams p, int tiles_x, int tiles_y,
+                                                                                  int ntiles) {
+    static_assert(BH == 8 || BH == 4 || BH == 2, "tile rows");
+    constexpr int NT = BH * 64, NW = BH;
+    constexpr int HROWS = (BH + 2) * R64_HW;
+    constexpr int R16_PER = (HROWS * 2 + NT - 1) / NT;   // halo chunks per thread
     constexpr int WN = 2, WTM = 64, WTN = 32, TM = 4, TN = 2, KS = 5;
     constexpr int BS = KS * 64 * 64;
-    constexpr int HS = R64_HROWS * 32;
+    constexpr int HS = HROWS * 32 > NW * 2 * 32 * 4 ? HROWS * 32 : NW * 2 * 32 * 4;
     __shared__ __attribute__((aligned(16))) char smem[BS + HS];
     char* Bs = smem;
     char* Hs = smem + BS;
@@ -1528,7 +1582,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
     const int tpi = tiles_x * tiles_y;
 
     // ---- filter: Bs[ks][n][q ^ swz(n)], chunk q = (tap 2ks + (q >> 1), channels 8 (q & 1)..)
-    for (int i = tid; i < KS * 64 * 4; i += 512) {
+    for (int i = tid; i < KS * 64 * 4; i += NT) {
         const int q = i & 3, n = (i >> 2) & 63, ks = i >> 8;
         const int tap = 2 * ks + (q >> 1), c8 = q & 1;
         uint4 v = {0u, 0u, 0u, 0u};
@@ -1546,13 +1600,13 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
         const int img = t / tpi;
         const int rem = t - img * tpi;
         const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
-        const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+        const int oy0 = ty * BH, ox0 = tx * R64_BW;
 #pragma unroll
         for (int k = 0; k < R16_PER; ++k) {
-            const int q = tid + k * 512;
+            const int q = tid + k * NT;
             const int hr = q >> 1, c8 = q & 1;
             uint4 v = {0u, 0u, 0u, 0u};
-            if (hr < R64_HROWS) {
+            if (hr < HROWS) {
                 const int hy = hr / R64_HW, hx = hr - (hr / R64_HW) * R64_HW;
                 const int ih = oy0 + p.ioh + hy0 + hy, iw = ox0 + p.iow + hx0 + hx;
                 if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW)
@@ -1564,9 +1618,9 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
     auto commit = [&]() {
 #pragma unroll
         for (int k = 0; k < R16_PER; ++k) {
-            const int q = tid + k * 512;
+            const int q = tid + k * NT;
             const int hr = q >> 1, c8 = q & 1;
-            if (hr < R64_HROWS) *reinterpret_cast<uint4*>(Hs + hr * 32 + 16 * (c8 ^ ((hr >> 3) & 1))) = hv[k];
+            if (hr < HROWS) *reinterpret_cast<uint4*>(Hs + hr * 32 + 16 * (c8 ^ ((hr >> 3) & 1))) = hv[k];
         }
     };
 
@@ -1620,7 +1674,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 const int ml = wm * WTM + mi * 16 + fr;
-                const int oy = ty * R64_BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
+                const int oy = ty * BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
                 const bool ok = oy < p.OH && ox < p.OW;
                 const long pix = ok ? (long)oy * p.OW + ox : 0;
 #pragma unroll
@@ -1663,7 +1717,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
             const int img = t / tpi;
             const int rem = t - img * tpi;
             const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
-            const int oy0 = ty * R64_BH, ox0 = tx * R64_BW;
+            const int oy0 = ty * BH, ox0 = tx * R64_BW;
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 const int ml = wm * WTM + mi * 16 + fr;
@@ -1729,7 +1783,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
     }
     if constexpr (BNB) {
         // lanes fr = 0..15 share channels: butterfly over them, then the
-        // four M waves of each column half meet in LDS (the halo is free)
+        // M waves of each column half meet in LDS (the halo is free)
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
@@ -1739,7 +1793,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
                     sgm[ni][j] += __shfl_xor(sgm[ni][j], off);
                     sbt[ni][j] += __shfl_xor(sbt[ni][j], off);
                 }
-        float* red = reinterpret_cast<float*>(Hs);   // [8 waves][2 kinds][32 columns]
+        float* red = reinterpret_cast<float*>(Hs);   // [NW waves][2 kinds][32 columns]
         if (fr == 0) {
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni)
@@ -1754,7 +1808,7 @@ __global__ __launch_bounds__(512, BNB ? 2 : 4) void conv_res16c(NTParams p, int 
         if (tid < 2 * 64) {
             const int kind = tid / 64, c = tid % 64, wn_ = c / 32, lc = c % 32;
             float sum = 0.f;
-            for (int wm_ = 0; wm_ < 4; ++wm_) sum += red[((wm_ * WN + wn_) * 2 + kind) * 32 + lc];
+            for (int wm_ = 0; wm_ < NW / WN; ++wm_) sum += red[((wm_ * WN + wn_) * 2 + kind) * 32 + lc];
             if (c < e.bn_C) e.bn_part[(long)blockIdx.x * 2 * e.bn_C + kind * e.bn_C + c] = sum;
         }
     }
@@ -1905,19 +1959,29 @@ void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype) {
     else hipLaunchKernelGGL((conv_res16c<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
 }
 
+// grid of the BN-backward form (= its bn_part rows): tiles of g_res16c_bh rows,
+// two rounds of the resident blocks (8 rows: one per CU, 4 or 2 rows: three)
 int res16c_grid(const NTParams& p, int cus) {
-    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
-    return std::min((p.M / (p.OH * p.OW)) * tx * ty, 2 * cus);
+    const int bh = g_res16c_bh;
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + bh - 1) / bh;
+    return std::min((p.M / (p.OH * p.OW)) * tx * ty, (bh == 8 ? 2 : 6) * cus);
+}
+
+template <typename T, int BH>
+static void launch_res16c_bn_t(NTParams& p, int grid, hipStream_t s) {
+    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + BH - 1) / BH;
+    const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
+    hipLaunchKernelGGL((conv_res16c<T, true, BH>), dim3(grid), dim3(BH * 64), 0, s, p, tx, ty, ntiles);
 }
 
 void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype) {
-    const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
-    const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     const int grid = res16c_grid(p, cus);
-    if (dtype == SEG_F16)
-        hipLaunchKernelGGL((conv_res16c<f16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
-    else
-        hipLaunchKernelGGL((conv_res16c<bf16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+    const bool h = dtype == SEG_F16;
+    switch (g_res16c_bh) {
+        case 8: h ? launch_res16c_bn_t<f16, 8>(p, grid, s) : launch_res16c_bn_t<bf16, 8>(p, grid, s); break;
+        case 2: h ? launch_res16c_bn_t<f16, 2>(p, grid, s) : launch_res16c_bn_t<bf16, 2>(p, grid, s); break;
+        default: h ? launch_res16c_bn_t<f16, 4>(p, grid, s) : launch_res16c_bn_t<bf16, 4>(p, grid, s); break;
+    }
 }
 
 bool res64_ok(const NTParams& p, int dtype) {
@@ -1931,13 +1995,19 @@ bool res64_ok(const NTParams& p, int dtype) {
 int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
-    if (p.N <= 16 && g_res16) {               // two blocks per CU (launch bounds: 4 waves / SIMD)
+    if (p.N <= 16 && g_res16) {
         if (p.epi.pool_y) return SEG_EINVAL;  // no pooled epilogue in the 16-wide form
         const int grid = std::min(ntiles, 2 * cus);
-        if (dtype == SEG_F16)
+        if (g_res16_dma) {                    // two blocks per CU (launch bounds: 4 waves / SIMD)
+            if (dtype == SEG_F16)
+                hipLaunchKernelGGL((conv_res64<0, f16, 16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+            else
+                hipLaunchKernelGGL((conv_res64<0, bf16, 16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        } else if (dtype == SEG_F16) {
             hipLaunchKernelGGL((conv_res64<0, f16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
-        else
+        } else {
             hipLaunchKernelGGL((conv_res64<0, bf16, 16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
+        }
         return SEG_OK;
     }
     const int grid = std::min(ntiles, cus);

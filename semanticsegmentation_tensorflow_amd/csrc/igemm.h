@@ -270,6 +270,8 @@ int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int 
 extern int g_res64;
 extern int g_res16;
 extern int g_res64_pp;
+extern int g_res16_dma;
+extern int g_res16c_bh;
 // the launch plan for p writes EpiParams.y2 (seg_conv2d_fwd_bn2)
 bool nt_bn2_ok(const NTParams& p, int dtype);
 extern int g_res16c;

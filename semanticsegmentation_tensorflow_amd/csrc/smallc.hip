@@ -154,20 +154,22 @@ void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s) {
 // stream -- 2 B read per 256 B written -- that the 256 x 64 tile kernel ran
 // at 1.6 TB/s.  Here a thread owns 8 consecutive columns of one pixel
 // (consecutive threads walk the columns: 16-byte stores, 8 threads per 128 B),
-// the filter sits in LDS as fp32 [n][k], the sum runs in k order, and the
-// epilogue is igemm_nt2's (bias, BN affine, ReLU, dropout, residual, ReluGrad).
+// the filter sits in LDS as fp32 [k][n] (a k step reads 32 contiguous bytes per
+// lane, consecutive lanes adjacent: no bank conflicts), the sum runs in k
+// order, and the epilogue is igemm_nt2's (bias, BN affine, ReLU, dropout,
+// residual, ReluGrad).
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int SK_MAXK = 16, SK_MAXN = 1024;
 
 template <typename T>
 __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
-    __shared__ float wsm[SK_MAXN * SK_MAXK];
-    const int K = p.K;
+    extern __shared__ __attribute__((aligned(16))) float wsm[];   // [K][N]
+    const int K = p.K, NN = p.N;
     const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
-    for (int i = threadIdx.x; i < p.N * K; i += 256) {
+    for (int i = threadIdx.x; i < NN * K; i += 256) {
         const int n = i / K, k = i - (i / K) * K;
-        wsm[n * SK_MAXK + k] = to_f32(Wt[(long)n * p.w_col + k]);
+        wsm[k * NN + n] = to_f32(Wt[(long)n * p.w_col + k]);
     }
     __syncthreads();
     const EpiParams& e = p.epi;
@@ -189,13 +191,15 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
                 for (int j = 0; j < 8; ++j) xv[q * 8 + j] = 0.f;
             }
         }
-        float v[8];
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float* wr = wsm + (col0 + j) * SK_MAXK;
-            float a = 0.f;
-            for (int k = 0; k < K; ++k) a += xv[k] * wr[k];
-            v[j] = a;
+        for (int k = 0; k < SK_MAXK; ++k) {
+            if (k >= K) break;
+            const float4 w0 = *reinterpret_cast<const float4*>(wsm + k * NN + col0);
+            const float4 w1 = *reinterpret_cast<const float4*>(wsm + k * NN + col0 + 4);
+            const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += xv[k] * wk[j];
         }
         float res[8], mk[8];
         if (e.residual) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
@@ -234,8 +238,9 @@ bool smallk_ok(const NTParams& p, int dtype) {
 void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s) {
     const long total = (long)p.M * (p.N / 8);
     const int grid = (int)std::min<long>((total + 255) / 256, (long)cus * 16);
-    if (dtype == SEG_F16) hipLaunchKernelGGL(smallk_nt_k<f16>, dim3(grid), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(smallk_nt_k<bf16>, dim3(grid), dim3(256), 0, s, p);
+    const size_t lds = (size_t)p.N * p.K * sizeof(float);
+    if (dtype == SEG_F16) hipLaunchKernelGGL(smallk_nt_k<f16>, dim3(grid), dim3(256), lds, s, p);
+    else hipLaunchKernelGGL(smallk_nt_k<bf16>, dim3(grid), dim3(256), lds, s, p);
 }
 
 

@@ -255,8 +255,9 @@ def conv2d_bwd_data_bn_part(desc, dy, w_hwio, x, gamma, beta, dx, part, eps=1e-3
     kp, seed = dropout if dropout is not None else (1.0, 0)
     bn = SegBnBwd(x.data_ptr(), pixel_stride(x), gamma.data_ptr(), beta.data_ptr(), float(eps), 1 if relu else 0,
                   1 if accumulate else 0, None, None, float(kp), int(seed) & (2 ** 64 - 1))
+    rows = part.numel() // (2 * desc.C)
     check(_lib.lib().seg_conv2d_bwd_data_bn_part(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(bn), ptr(dx),
-                                                 ptr(part), stream_ptr(stream)), "conv2d_backprop_input_bn")
+                                                 ptr(part), rows, stream_ptr(stream)), "conv2d_backprop_input_bn")
     return dx
 
 

@@ -160,14 +160,22 @@ def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate):
 
 # the 3x3 form (FC-DenseNet growth conv, 64 -> 16): the input gradient runs on
 # conv_res16c and continues through the BN(+ReLU) that produced the conv's
-# input and, with keep_prob < 1, the dropout of the conv before that BN
+# input and, with keep_prob < 1, the dropout of the conv before that BN; every
+# tile height of the kernel (option res16c_bh: 8, 4 = the default, 2)
 BNB3_CASES = [(2, 21, 67, 64, 16), (1, 30, 70, 64, 16), (2, 9, 11, 32, 16)]
+
+
+@pytest.fixture(params=[4, 8, 2], ids=["bh4", "bh8", "bh2"])
+def res16c_bh(request):
+    ops.set_option("res16c_bh", request.param)
+    yield request.param
+    ops.set_option("res16c_bh", 4)
 
 
 @pytest.mark.parametrize("kp", [1.0, 0.6], ids=["no-dropout", "dropout"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", BNB3_CASES)
-def test_conv3x3_bwd_data_through_bn_relu_dropout(dev, case, dtype, kp):
+def test_conv3x3_bwd_data_through_bn_relu_dropout(dev, case, dtype, kp, res16c_bh):
     from tests.test_gpu_ops import _np_uniform
     N, H, W, C, K = case
     x, w, gamma, beta, xr, wr, a = _pro_case((N, H, W, C, K, 3), dtype, dev)

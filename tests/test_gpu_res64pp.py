@@ -130,3 +130,50 @@ def test_res64pp_input_gradient_relu_mask(dev, shape, dtype):
     assert torch.equal(_bits(a), _bits(b))
     zero = (mask == 0)
     assert bool((a[zero] == 0).all()) and 0.3 < zero.float().mean().item() < 0.7
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("K", [16, 8])
+def test_res16_dma_halo_equals_register_halo(dev, shape, dtype, K):
+    """The 16-wide conv_res64 (FC-DenseNet's growth conv, 64 -> 16 channels,
+    Network/model/FCDenseNet.py:33-34) with its halo landed by LDS DMA (two
+    blocks per CU) against the VGPR-staged form: same fragments, same MFMA
+    order, same epilogue -> bit-equal, for the forward epilogues and the
+    ReluGrad-masked input gradient (64 -> 16 of the transposed filter)."""
+    N, H, W = shape
+    dt = ops.BF16 if dtype == torch.bfloat16 else ops.F16
+    d = ops.conv_desc(N, H, W, 64, K, 3, 3, dtype=dt)
+    assert ops.conv_kernel_info(d, ops.OP_FWD)[0].startswith("conv_res64")
+    x, w32, bias, other = _operands(dev, N, H, W, dtype, 13)
+    w32, bias = w32[..., :K].contiguous(), bias[:K].contiguous()
+    res = other[..., :K].contiguous()
+    wk = torch.zeros(ops.packed_shape(3, 3, 64, K, ops.PACK_KRSC, 64), dtype=dtype, device=dev)
+    ops.pack_filter(w32, wk, 64, K, ops.PACK_KRSC)
+    ws = ops.Workspace(dev)
+
+    def both(fn):
+        a = fn()
+        ops.set_option("res16_dma", 0)
+        try:
+            b = fn()
+        finally:
+            ops.set_option("res16_dma", 1)
+        torch.cuda.synchronize()
+        return a, b
+    for epi in (ops.epilogue(bias=bias, relu=True), ops.epilogue(residual=res),
+                ops.epilogue(bias=bias, keep_prob=0.8, seed=5)):
+        def run():
+            y = torch.full((N, H, W, K), float("nan"), dtype=dtype, device=dev)
+            ops.conv2d_fwd(d, x, wk, y, epi, ws)
+            return y
+        a, b = both(run)
+        assert torch.equal(_bits(a), _bits(b))
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2),
+                                     w32.to(dtype).float().permute(3, 2, 0, 1), padding=1)
+    ref = torch.relu(ref + bias.view(1, -1, 1, 1)).permute(0, 2, 3, 1)
+    y = torch.empty(N, H, W, K, dtype=dtype, device=dev)
+    ops.conv2d_fwd(d, x, wk, y, ops.epilogue(bias=bias, relu=True), ws)
+    torch.cuda.synchronize()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1.2e-2 * ref.abs().max().item() + 1e-3, err

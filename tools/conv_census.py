@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--pflops", type=float, default=1.25, help="rate for the 'ideal us' column")
+    ap.add_argument("--fills", action="store_true",
+                    help="also list the torch zero-fills / allocations a steady-state step issues, by call site")
     a = ap.parse_args()
     import bench
     H, W, B, kp = bench.DEFAULTS[a.model]
@@ -83,7 +85,34 @@ def main():
     g["sess"].run(g["train_step"], feed_dict=feed)    # first step: one-time filter packing
     rec.launches.clear()
     rec.calls.clear()
+    fills = collections.Counter()
+    if a.fills:
+        import traceback
+
+        def site():
+            for fr in reversed(traceback.extract_stack()[:-2]):
+                if "semanticsegmentation_tensorflow_amd" in fr.filename:
+                    return f"{os.path.basename(fr.filename)}:{fr.lineno}"
+            return "?"
+
+        def wrap(obj, name):
+            orig = getattr(obj, name)
+
+            def fn(*args, **kw):
+                out = orig(*args, **kw)
+                t = out if isinstance(out, torch.Tensor) else None
+                fills[(name, site())] += t.numel() * t.element_size() if t is not None else 0
+                return out
+            setattr(obj, name, fn)
+        for n in ("zero_", "fill_"):
+            wrap(torch.Tensor, n)
+        for n in ("zeros", "zeros_like", "empty", "empty_like", "full", "full_like"):
+            wrap(torch, n)
     g["sess"].run(g["train_step"], feed_dict=feed)
+    if a.fills:
+        print("torch allocations / fills in a steady-state step (bytes by call site):")
+        for (n, s), b in fills.most_common():
+            print(f"  {n:12s} {s:28s} {b / 1e6:10.1f} MB")
     rows = collections.OrderedDict()
     total = 0.0
     for name, d in rec.launches:
