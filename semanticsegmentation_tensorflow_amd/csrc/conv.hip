@@ -552,7 +552,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res64", &seg::g_res64, 0, 1, 1, {}},
         {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
-        {"res16c_bh", &seg::g_res16c_bh, 2, 8, 4, {2, 4, 8}},
+        {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {2, 4, 8}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
