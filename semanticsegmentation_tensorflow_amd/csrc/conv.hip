@@ -553,6 +553,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
         {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {2, 4, 8}},
+        {"nt2bn_bm", &seg::g_nt2bn_bm, 0, 0, 0, {128, 256}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
@@ -775,7 +776,7 @@ static int bwd_data_bn_params(const seg_conv_desc* d, NTParams& p) {
 
 // per-tile (1x1) or per-block (3x3) partial rows + the finish scratch
 static long bwd_data_bn_rows(const seg_conv_desc* d, const NTParams& p, int kind) {
-    return kind == 1 ? (p.M + 255) / 256 : seg::res16c_grid(p, seg::device_cus());
+    return kind == 1 ? seg::nt2_bn_rows(p.M) : seg::res16c_grid(p, seg::device_cus());
 }
 
 extern "C" size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d) {

@@ -164,6 +164,8 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
 void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
+extern int g_nt2bn_bm;
+long nt2_bn_rows(int M);
 extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;

@@ -174,15 +174,30 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
     __syncthreads();
     const EpiParams& e = p.epi;
     const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
-    const int CK = p.N / 8;
-    const long hw = (long)p.OH * p.OW;
-    const long total = (long)p.M * CK;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const long m = i / CK;
-        const int col0 = (int)(i - m * CK) * 8;
-        const long img = m / hw, pix = m - img * hw;
+    // thread -> (pixel row of the block pass, 8-column chunk): the chunk and
+    // its epilogue constants are fixed per thread; pixels advance by a
+    // constant step with (image, pixel) carried incrementally (no divisions
+    // in the loop)
+    const int CK = p.N / 8, PB = 256 / CK;
+    const int prow = threadIdx.x / CK, ck = threadIdx.x - prow * CK;
+    if (prow >= PB) return;
+    const int col0 = ck * 8;
+    float sc[8], ad[8], bs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        const bool cv = col < e.n_valid;
+        sc[j] = (e.scale && cv) ? e.scale[col] : 1.f;
+        ad[j] = (e.shift && cv) ? e.shift[col] : 0.f;
+        bs[j] = (e.bias && cv) ? e.bias[col] : 0.f;
+    }
+    const int hw = p.OH * p.OW;
+    const int step = gridDim.x * PB;
+    int m = blockIdx.x * PB + prow;
+    int img = m / hw, pix = m - img * hw;
+    for (; m < p.M; m += step) {
         float xv[SK_MAXK];
-        const T* xr = X + img * p.x_img + pix * p.ldx;
+        const T* xr = X + img * p.x_img + (long)pix * p.ldx;
 #pragma unroll
         for (int q = 0; q < SK_MAXK / 8; ++q) {
             if (q * 8 < K) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xr + q * 8), xv + q * 8);
@@ -203,23 +218,28 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
         }
         float res[8], mk[8];
         if (e.residual) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
-                            reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0), res);
+                            reinterpret_cast<const T*>(e.residual) + img * e.res_img + (long)pix * e.ld_res + col0), res);
         if (e.mask) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
-                        reinterpret_cast<const T*>(e.mask) + img * e.mask_img + pix * e.ld_mask + col0), mk);
+                        reinterpret_cast<const T*>(e.mask) + img * e.mask_img + (long)pix * e.ld_mask + col0), mk);
         const uint64_t gidx = ((uint64_t)m) * e.n_valid;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int col = col0 + j;
             const bool cv = col < e.n_valid;
-            const float sc = (e.scale && cv) ? e.scale[col] : 1.f, sh = (e.shift && cv) ? e.shift[col] : 0.f;
-            float x = v[j] * sc + sh + ((e.bias && cv) ? e.bias[col] : 0.f);
+            float x = v[j] * sc[j] + ad[j] + bs[j];
             if (e.relu) x = fmaxf(x, 0.f);
             if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
             if (e.residual) x += res[j];
             if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = cv ? x : 0.f;
         }
-        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) = Chunk<T>::pack(v);
+        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img * p.y_img + (long)pix * p.ldy + col0) =
+            Chunk<T>::pack(v);
+        pix += step;
+        while (pix >= hw) {
+            pix -= hw;
+            ++img;
+        }
     }
 }
 }  // namespace
@@ -236,8 +256,8 @@ bool smallk_ok(const NTParams& p, int dtype) {
 }
 
 void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s) {
-    const long total = (long)p.M * (p.N / 8);
-    const int grid = (int)std::min<long>((total + 255) / 256, (long)cus * 16);
+    const int pb = 256 / (p.N / 8);                  // pixels per block pass
+    const int grid = (int)std::min<long>((p.M + pb - 1) / pb, (long)cus * 16);
     const size_t lds = (size_t)p.N * p.K * sizeof(float);
     if (dtype == SEG_F16) hipLaunchKernelGGL(smallk_nt_k<f16>, dim3(grid), dim3(256), lds, s, p);
     else hipLaunchKernelGGL(smallk_nt_k<bf16>, dim3(grid), dim3(256), lds, s, p);

@@ -124,10 +124,18 @@ BNB_CASES = [(2, 9, 11, 48, 64, 1), (1, 12, 10, 136, 64, 1), (1, 33, 41, 200, 13
              (1, 17, 19, 24, 8, 1), (2, 40, 52, 112, 64, 1)]
 
 
+@pytest.fixture(params=[256, 128], ids=["bm256", "bm128"])
+def nt2bn_bm(request):
+    """Both M-tile heights of the 1x1 form (option nt2bn_bm)."""
+    ops.set_option("nt2bn_bm", request.param)
+    yield request.param
+    ops.set_option("nt2bn_bm", 256)
+
+
 @pytest.mark.parametrize("accumulate", [False, True], ids=["write", "accumulate"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", BNB_CASES)
-def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate):
+def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate, nt2bn_bm):
     N, H, W, C, K, R = case
     x, w, gamma, beta, xr, wr, a = _pro_case(case, dtype, dev)
     g = torch.Generator().manual_seed(9)

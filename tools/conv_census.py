@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 from semanticsegmentation_tensorflow_amd import _lib, ops  # noqa: E402
 
-OPCODE = {"seg_conv2d_fwd": 0, "seg_conv2d_fwd_pool": 0, "seg_conv2d_fwd_bn2": 0, "seg_conv2d_bwd_data": 1, "seg_conv2d_bwd_filter": 2,
+OPCODE = {"seg_conv2d_fwd": 0, "seg_conv2d_fwd_pool": 0, "seg_conv2d_fwd_bn2": 0, "seg_conv2d_fwd_bn2_pro": 7, "seg_conv2d_bwd_data": 1, "seg_conv2d_bwd_filter": 2,
           "seg_conv2d_bwd_filter_begin": 2, "seg_conv2d_bwd_filter_adam": 2, "seg_tconv2d_fwd": 3,
           "seg_tconv2d_bwd_data": 4, "seg_tconv2d_bwd_filter": 5, "seg_conv2d_bwd_data_bn": 6,
           "seg_conv2d_fwd_pro": 7, "seg_conv2d_bwd_filter_pro": 8}
@@ -50,7 +50,8 @@ class Recorder:
             if name in OPCODE:
                 d = _lib.SegConvDesc()
                 ctypes.pointer(d)[0] = a[0]._obj
-                self.launches.append((name, d))
+                pro = name == "seg_conv2d_fwd_bn2" and a[2] is not None   # BN1 prologue: the FWD_PRO plan
+                self.launches.append((name + ("_pro" if pro else ""), d))
             return 0
         return fn
 
