@@ -467,7 +467,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             const int kind = bwd_data_bn_params(d, p);
             if (!kind) return SEG_EINVAL;
             macs = macs_conv;
-            if (kind == 1) { fam = "igemm_nt2_bn"; bm = 256; bn = 64; }
+            if (kind == 1 && seg::bn1x1s_ok(p, d->dtype)) { fam = "bn1x1_stream"; bm = 128; bn = 64; }
+            else if (kind == 1) { fam = "igemm_nt2_bn"; bm = 256; bn = 64; }
             else { fam = "conv_res16c_bn"; bm = 256; bn = 64; }
             break;
         }
@@ -554,6 +555,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
         {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {2, 4, 8}},
         {"nt2bn_bm", &seg::g_nt2bn_bm, 0, 0, 0, {128, 256}},
+        {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},
@@ -776,7 +778,8 @@ static int bwd_data_bn_params(const seg_conv_desc* d, NTParams& p) {
 
 // per-tile (1x1) or per-block (3x3) partial rows + the finish scratch
 static long bwd_data_bn_rows(const seg_conv_desc* d, const NTParams& p, int kind) {
-    return kind == 1 ? seg::nt2_bn_rows(p.M) : seg::res16c_grid(p, seg::device_cus());
+    if (kind == 2) return seg::res16c_grid(p, seg::device_cus());
+    return seg::bn1x1s_ok(p, d->dtype) ? seg::bn1x1s_rows(p, seg::device_cus()) : seg::nt2_bn_rows(p.M);
 }
 
 extern "C" size_t seg_conv_bwd_data_bn_workspace(const seg_conv_desc* d) {
@@ -822,8 +825,14 @@ static int bwd_data_bn_launch(const seg_conv_desc* d, const void* dy, const void
         e.seed = bn->seed;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (kind == 1) seg::launch_nt2_bn(p, d->dtype, s);
-    else seg::launch_res16c_bn(p, seg::device_cus(), s, d->dtype);
+    if (kind == 1 && seg::bn1x1s_ok(p, d->dtype)) {
+        const int st = seg::launch_bn1x1s(p, d->dtype, seg::device_cus(), s);
+        if (st) return st;
+    } else if (kind == 1) {
+        seg::launch_nt2_bn(p, d->dtype, s);
+    } else {
+        seg::launch_res16c_bn(p, seg::device_cus(), s, d->dtype);
+    }
     SEG_CHECK_LAUNCH();
     return SEG_OK;
 }

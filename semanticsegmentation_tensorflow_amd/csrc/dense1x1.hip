@@ -199,6 +199,177 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
     wait_vmcnt<0>();
 }
 
+// ---------------------------------------------------------------------------
+// The bottleneck conv's input gradient through the BN(+ReLU) before it
+// (seg_conv2d_bwd_data_bn, 1x1 form: FC-DenseNet.py:27 backward into the
+// BN of :25-26), streamed: dx[m][c] = BNbwd(sum_k dz[m][k] W[c][k]) over
+// k < 64, accumulated into the concat gradient.  Per pixel it reads 64
+// dz + C x + C old-dx channels and writes C, at 128 MACs per C -- HBM-bound,
+// and the tile-per-block igemm_nt2_bn spent each block in one load latency.
+// Here a block owns one 64-channel chunk of the output for a contiguous range
+// of 128-pixel tiles (blocks of one tile range and different chunks sit on
+// one XCD, so the dz rows they share come from its L2); every wave stages and
+// consumes its own 16 pixel rows (dz, x and old dx of its chunk: 6 LDS-DMA
+// instructions per step) through a 3-deep ring without barriers; the chunk's
+// filter fragments stay in VGPRs; MFMA on D^T = W . dz^T so a lane holds 4
+// consecutive channels of one pixel and finishes them from the staged x / old
+// dx; the BN column sums stay in VGPRs until the block's last tile.
+// ---------------------------------------------------------------------------
+constexpr int B1_TP = 128;       // pixels per tile (8 waves x 16)
+constexpr int B1_NST = 3;        // ring depth (steps)
+constexpr int B1_WST = 3 * 16 * 128;                  // per wave per step: dz, x, old dx rows
+constexpr int B1_ST = 4;         // stores per wave per step
+
+template <typename T>
+__global__ __launch_bounds__(512, 1) void bn1x1_dgrad_stream(NTParams p, int nch, int G, int ntiles) {
+    __shared__ __attribute__((aligned(16))) char ring[B1_NST * 8 * B1_WST];   // 144 KiB
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, fg = lane >> 4, lr = lane >> 3;
+    const EpiParams& e = p.epi;
+    const int b = blockIdx.x;
+    const int chunk = (b >> 3) % nch, bx = ((b >> 3) / nch) * 8 + (b & 7);
+    const int t0 = (int)((long)bx * ntiles / G), t1 = (int)((long)(bx + 1) * ntiles / G);
+    const int S = t1 - t0;
+    const int c0 = chunk * 64;
+    const bool res = e.residual != nullptr;
+    const int ndma = res ? 6 : 4;
+    const T* __restrict__ DZ = reinterpret_cast<const T*>(p.x);
+    const T* __restrict__ BX = reinterpret_cast<const T*>(e.bn_x);
+    const T* __restrict__ RS = reinterpret_cast<const T*>(e.residual);
+    const int hw = p.OH * p.OW;
+
+    // the chunk's filter fragments (A operand: row n = ni*16 + fr, k = ks*32 + 8 fg)
+    uint4 wf[4][2];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int n = c0 + ni * 16 + fr;
+            wf[ni][ks] = n < p.N ? *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p.w) + (long)n * p.w_col +
+                                                                   ks * 32 + fg * 8)
+                                 : uint4{0u, 0u, 0u, 0u};
+        }
+    // BN (scale, shift) of the lane's 16 channels
+    float bsc[4][4], bsh[4][4], sgm[4][4], sbt[4][4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = c0 + ni * 16 + 4 * fg + j;
+            const bool cv = col < e.bn_cv;
+            bsc[ni][j] = cv ? e.bn_gamma[col] * e.bn_inv : 0.f;
+            bsh[ni][j] = cv ? e.bn_beta[col] : 0.f;
+            sgm[ni][j] = sbt[ni][j] = 0.f;
+        }
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)ring;
+    auto issue = [&](int s) {
+        const int t = t0 + s;
+        const unsigned sb = lds0 + ((s % B1_NST) * 8 + w) * B1_WST;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = q * 8 + lr;                   // wave-local pixel row
+            const int c = (lane & 7) ^ ((q * 4 + (lr >> 1)) & 7);
+            const int m = t * B1_TP + w * 16 + row;
+            const bool mok = m < p.M;
+            const int mm = mok ? m : 0;
+            const int img = mm / hw, pix = mm - img * hw;
+            const bool cok = mok && c0 + c * 8 < p.N;
+            const void* zs = (const void*)s1_zero;
+            glds16(mok ? (const void*)(DZ + img * p.x_img + (long)pix * p.ldx + c * 8) : zs, sb + q * 1024);
+            glds16(cok ? (const void*)(BX + img * e.bn_x_img + (long)pix * e.ld_bn_x + c0 + c * 8) : zs,
+                   sb + 2048 + q * 1024);
+            if (res)
+                glds16(cok ? (const void*)(RS + img * e.res_img + (long)pix * e.ld_res + c0 + c * 8) : zs,
+                       sb + 4096 + q * 1024);
+        }
+    };
+    // vector-memory instructions issued after DMA(s) when step s starts: the
+    // stores of steps s-2, s-1 and the DMA of step s+1
+    auto younger = [&](int s) { return B1_ST * min(2, s) + (s + 1 < S ? ndma : 0); };
+    for (int s = 0; s < B1_NST - 1 && s < S; ++s) issue(s);
+
+    const int sw = (fr >> 1) & 7;                        // row swizzle of the lane's pixel row
+    for (int s = 0; s < S; ++s) {
+        wait_vm_rt(younger(s));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own reads of the stage refilled next
+        if (s + B1_NST - 1 < S) issue(s + B1_NST - 1);
+        const char* Ws = ring + ((s % B1_NST) * 8 + w) * B1_WST;
+        f32x4 acc[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const uint4 zb = *reinterpret_cast<const uint4*>(Ws + fr * 128 + 16 * ((ks * 4 + fg) ^ sw));
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) acc[ni] = mfma16x16x32<T>(wf[ni][ks], zb, acc[ni]);   // D^T[n][px]
+        }
+        const int m = (t0 + s) * B1_TP + w * 16 + fr;
+        const bool mok = m < p.M;
+        const int mm = mok ? m : 0;
+        const int img = mm / hw, pix = mm - img * hw;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int col0 = c0 + ni * 16 + 4 * fg;
+            const int off = fr * 128 + 16 * ((2 * ni + (fg >> 1)) ^ sw) + 8 * (fg & 1);
+            const uint2 xr = *reinterpret_cast<const uint2*>(Ws + 2048 + off);
+            const T* xh = reinterpret_cast<const T*>(&xr);
+            uint2 rr = uint2{0u, 0u};
+            if (res) rr = *reinterpret_cast<const uint2*>(Ws + 4096 + off);
+            const T* rh = reinterpret_cast<const T*>(&rr);
+            T o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = col0 + j;
+                const float xv = to_f32(xh[j]);
+                const bool on = col < e.bn_cv && (!e.bn_relu || xv * bsc[ni][j] + bsh[ni][j] > 0.f);
+                const float dz = on ? acc[ni][j] : 0.f;
+                sgm[ni][j] += dz * xv;
+                sbt[ni][j] += dz;
+                float x = dz * bsc[ni][j];
+                if (res) x += to_f32(rh[j]);
+                o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
+            }
+            const bool ok = mok && col0 < p.N;
+            uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + (long)pix * p.ldy + col0)
+                            : s1_trash + (tid & 4095);
+            *dst = *reinterpret_cast<const uint2*>(o);
+        }
+    }
+    wait_vmcnt<0>();
+    // BN column sums: lanes fr share channels -> butterfly, then the 8 waves
+    // meet in LDS; one partial row per tile range (block x), this chunk's columns
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                sgm[ni][j] += __shfl_xor(sgm[ni][j], o);
+                sbt[ni][j] += __shfl_xor(sbt[ni][j], o);
+            }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(ring);     // [8 waves][2 kinds][64 columns]
+    if (fr == 0) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int lc = ni * 16 + 4 * fg + j;
+                red[(w * 2 + 0) * 64 + lc] = sgm[ni][j];
+                red[(w * 2 + 1) * 64 + lc] = sbt[ni][j];
+            }
+    }
+    __syncthreads();
+    if (tid < 128) {
+        const int kind = tid >> 6, lc = tid & 63;
+        float sum = 0.f;
+        for (int w_ = 0; w_ < 8; ++w_) sum += red[(w_ * 2 + kind) * 64 + lc];
+        if (c0 + lc < e.bn_C) e.bn_part[(long)bx * 2 * e.bn_C + kind * e.bn_C + c0 + lc] = sum;
+    }
+}
+
 }  // namespace
 
 // y = epilogue(W . relu(BN(x))): single-tap 1x1 stride-1, N <= 64, C <= 256,
@@ -212,6 +383,49 @@ bool s1x1_ok(const NTParams& p, int dtype, int nphases) {
            p.ldy % 4 == 0 && ((uintptr_t)p.x % 16) == 0 && ((uintptr_t)p.y % 8) == 0 && !p.epi.residual &&
            !p.epi.mask && !p.epi.bn_x && p.M > 0 &&
            (!p.epi.y2 || (p.epi.ld_y2 % 4 == 0 && ((uintptr_t)p.epi.y2 % 8) == 0 && p.epi.y2_img == (long)p.OH * p.OW * p.epi.ld_y2));
+}
+
+// The 1x1 input gradient through the BN backward on bn1x1_dgrad_stream: K = 64
+// (the bottleneck's 4 * growth filters), dense 1x1 stride-1 geometry, 16-bit.
+int g_bn1x1s = 1;
+
+// geometry (from the descriptor alone: it also fixes the partial-row count)
+bool bn1x1s_ok(const NTParams& p, int dtype) {
+    return g_bn1x1s && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.K == 64 && p.C == 64 &&
+           p.taps_w == 1 && p.ish == 1 && p.isw == 1 && p.ioh == 0 && p.iow == 0 && p.osh == 1 && p.osw == 1 &&
+           p.ooh == 0 && p.oow == 0 && p.IH == p.Ha && p.IW == p.Wa && p.OH == p.Ha && p.OW == p.Wa &&
+           p.N % 8 == 0 && p.M > 0 && p.M % (p.OH * p.OW) == 0 && p.ldx % 8 == 0 && p.ldy % 4 == 0 &&
+           p.w_col % 8 == 0 && p.x_img % 8 == 0;
+}
+
+// the launch's operands (16-byte DMA rows, 8-byte stores)
+static bool bn1x1s_args_ok(const NTParams& p) {
+    const EpiParams& e = p.epi;
+    return e.bn_x && e.ld_bn_x % 8 == 0 && e.bn_x_img % 8 == 0 && !e.mask && e.keep_prob >= 1.f &&
+           (!e.residual || (e.ld_res % 8 == 0 && e.res_img % 8 == 0 && ((uintptr_t)e.residual % 16) == 0)) &&
+           ((uintptr_t)p.x % 16) == 0 && ((uintptr_t)e.bn_x % 16) == 0 && ((uintptr_t)p.y % 8) == 0 &&
+           ((uintptr_t)p.w % 16) == 0;
+}
+
+// blocks per 64-channel chunk (= the BN partial rows): a multiple of 8, one
+// block per CU over all chunks
+int bn1x1s_rows(const NTParams& p, int cus) {
+    const int nch = (p.N + 63) / 64;
+    const int ntiles = (p.M + B1_TP - 1) / B1_TP;
+    int G = std::max(8, (cus / nch) & ~7);
+    return std::min(G, std::max(8, (ntiles + 7) & ~7));
+}
+
+int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
+    if (!bn1x1s_args_ok(p)) return SEG_EINVAL;
+    const int nch = (p.N + 63) / 64;
+    const int ntiles = (p.M + B1_TP - 1) / B1_TP;
+    const int G = bn1x1s_rows(p, cus);
+    if (dtype == SEG_F16)
+        hipLaunchKernelGGL(bn1x1_dgrad_stream<f16>, dim3(nch * G), dim3(512), 0, s, p, nch, G, ntiles);
+    else
+        hipLaunchKernelGGL(bn1x1_dgrad_stream<bf16>, dim3(nch * G), dim3(512), 0, s, p, nch, G, ntiles);
+    return SEG_OK;
 }
 
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {

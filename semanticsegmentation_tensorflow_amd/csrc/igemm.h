@@ -166,6 +166,11 @@ void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_
 void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
 extern int g_nt2bn_bm;
 long nt2_bn_rows(int M);
+// dense1x1.hip: the 1x1 BN-backward input gradient streamed (K = 64)
+extern int g_bn1x1s;
+bool bn1x1s_ok(const NTParams& p, int dtype);
+int bn1x1s_rows(const NTParams& p, int cus);
+int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s);
 extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
 extern int g_nt_variant;

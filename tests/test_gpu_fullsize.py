@@ -416,7 +416,7 @@ def _c3_sample(recs):
     """Dense blocks 1 and 6, their transitions, the stem and the head, plus
     the middle block's first layers: every kind of input-gradient launch the
     C3 step runs (plain, in place into a concat gradient, through a folded
-    BatchNorm backward on igemm_nt2_bn and on conv_res16c_bn)."""
+    BatchNorm backward on bn1x1_stream, igemm_nt2_bn and conv_res16c_bn)."""
     keep = ("dense_init", "denseblock1", "transition_layer1", "denseblock6", "transition_layer5",
             "final_conv", "denseblock4bottleneck_layer_0", "denseblock4bottleneck_layer_1")
     return [r for r in recs if r["name"].startswith(keep)]
@@ -435,7 +435,7 @@ def test_c3_layer_local_parity(c3):
     sess, weights = c3["sess"], c3["weights"]
     sample = _c3_sample(sess.capture)
     kinds = {r["bn_bwd"]["kernel"].split("<")[0] for r in sample if r["bn_bwd"] is not None}
-    assert {"igemm_nt2_bn", "conv_res16c_bn"} <= kinds, kinds
+    assert {"bn1x1_stream", "conv_res16c_bn"} <= kinds, kinds
     assert any(r["bn_bwd"] is not None and r["bn_bwd"]["base"] is not None for r in sample)
     assert any(r["bn_bwd"] is not None and r["bn_bwd"]["drop"] is not None for r in sample)
     assert len(sample) >= 40, len(sample)
