@@ -132,8 +132,13 @@ def main():
             apply(o)
             for ci, (d, op, make, nbytes) in enumerate(cases):
                 fn = make()          # per option set: buffers sized for its launch geometry
-                fn()
-                torch.cuda.synchronize()
+                try:
+                    fn()
+                    torch.cuda.synchronize()
+                except RuntimeError as err:
+                    print(f"{a.specs[ci]} [{o}]: {err}", flush=True)
+                    times.setdefault((ci, oi), []).append(float("nan"))
+                    continue
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(a.reps):
@@ -147,6 +152,9 @@ def main():
             apply(o)
             name = ops.conv_kernel_info(d, op)[0]
             t = times[(ci, oi)]
+            if any(v != v for v in t):
+                print(f"{a.specs[ci]:22s} [{o or 'default'}] {name:28s} failed")
+                continue
             med = statistics.median(t)
             print(f"{a.specs[ci]:22s} [{o or 'default'}] {name:28s} med={med:8.1f}us min={min(t):8.1f}us  "
                   f"{nbytes / med / 1e3:7.1f} GB/s of {nbytes / 1e6:.0f} MB", flush=True)
