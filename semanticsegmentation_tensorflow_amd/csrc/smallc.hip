@@ -160,7 +160,7 @@ void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s) {
 // residual, ReluGrad).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int SK_MAXK = 16, SK_MAXN = 1024;
+constexpr int SK_MAXK = 16, SK_MAXN = 1024, SK_UNR = 4;
 
 template <typename T>
 __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
@@ -193,52 +193,74 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
     }
     const int hw = p.OH * p.OW;
     const int step = gridDim.x * PB;
-    int m = blockIdx.x * PB + prow;
-    int img = m / hw, pix = m - img * hw;
-    for (; m < p.M; m += step) {
-        float xv[SK_MAXK];
-        const T* xr = X + img * p.x_img + (long)pix * p.ldx;
+    // SK_UNR pixels per trip (m, m + step, ...): all their loads are issued
+    // before the first is used, so each thread keeps SK_UNR x 2-3 16-byte
+    // requests in flight instead of one
+    int mm[SK_UNR], img[SK_UNR], pix[SK_UNR];
 #pragma unroll
-        for (int q = 0; q < SK_MAXK / 8; ++q) {
-            if (q * 8 < K) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xr + q * 8), xv + q * 8);
-            else {
+    for (int u = 0; u < SK_UNR; ++u) {
+        mm[u] = blockIdx.x * PB + prow + u * step;
+        img[u] = mm[u] / hw;
+        pix[u] = mm[u] - img[u] * hw;
+    }
+    const T* __restrict__ RS = reinterpret_cast<const T*>(e.residual);
+    const T* __restrict__ MK = reinterpret_cast<const T*>(e.mask);
+    for (; mm[0] < p.M;) {
+        uint4 xq[SK_UNR][SK_MAXK / 8], rq[SK_UNR], mq[SK_UNR];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) xv[q * 8 + j] = 0.f;
+        for (int u = 0; u < SK_UNR; ++u) {
+            const bool ok = mm[u] < p.M;
+            const T* xr = X + img[u] * p.x_img + (long)pix[u] * p.ldx;
+#pragma unroll
+            for (int q = 0; q < SK_MAXK / 8; ++q)
+                xq[u][q] = ok && q * 8 < K ? *reinterpret_cast<const uint4*>(xr + q * 8) : uint4{0u, 0u, 0u, 0u};
+            rq[u] = mq[u] = uint4{0u, 0u, 0u, 0u};
+            if (ok && RS) rq[u] = *reinterpret_cast<const uint4*>(RS + img[u] * e.res_img + (long)pix[u] * e.ld_res + col0);
+            if (ok && MK) mq[u] = *reinterpret_cast<const uint4*>(MK + img[u] * e.mask_img + (long)pix[u] * e.ld_mask + col0);
+        }
+#pragma unroll
+        for (int u = 0; u < SK_UNR; ++u) {
+            if (mm[u] >= p.M) break;
+            float xv[SK_MAXK];
+#pragma unroll
+            for (int q = 0; q < SK_MAXK / 8; ++q) Chunk<T>::unpack(xq[u][q], xv + q * 8);
+            float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < SK_MAXK; ++k) {
+                if (k < K) {
+                    const float4 w0 = *reinterpret_cast<const float4*>(wsm + k * NN + col0);
+                    const float4 w1 = *reinterpret_cast<const float4*>(wsm + k * NN + col0 + 4);
+                    const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] += xv[k] * wk[j];
+                }
             }
-        }
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            float res[8], mk[8];
+            Chunk<T>::unpack(rq[u], res);
+            Chunk<T>::unpack(mq[u], mk);
+            const uint64_t gidx = ((uint64_t)mm[u]) * e.n_valid;
 #pragma unroll
-        for (int k = 0; k < SK_MAXK; ++k) {
-            if (k >= K) break;
-            const float4 w0 = *reinterpret_cast<const float4*>(wsm + k * NN + col0);
-            const float4 w1 = *reinterpret_cast<const float4*>(wsm + k * NN + col0 + 4);
-            const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += xv[k] * wk[j];
+            for (int j = 0; j < 8; ++j) {
+                const int col = col0 + j;
+                const bool cv = col < e.n_valid;
+                float x = v[j] * sc[j] + ad[j] + bs[j];
+                if (e.relu) x = fmaxf(x, 0.f);
+                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (RS) x += res[j];
+                if (MK) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                v[j] = cv ? x : 0.f;
+            }
+            *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img[u] * p.y_img + (long)pix[u] * p.ldy + col0) =
+                Chunk<T>::pack(v);
         }
-        float res[8], mk[8];
-        if (e.residual) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
-                            reinterpret_cast<const T*>(e.residual) + img * e.res_img + (long)pix * e.ld_res + col0), res);
-        if (e.mask) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(
-                        reinterpret_cast<const T*>(e.mask) + img * e.mask_img + (long)pix * e.ld_mask + col0), mk);
-        const uint64_t gidx = ((uint64_t)m) * e.n_valid;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int col = col0 + j;
-            const bool cv = col < e.n_valid;
-            float x = v[j] * sc[j] + ad[j] + bs[j];
-            if (e.relu) x = fmaxf(x, 0.f);
-            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
-            if (e.residual) x += res[j];
-            if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
-            v[j] = cv ? x : 0.f;
-        }
-        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img * p.y_img + (long)pix * p.ldy + col0) =
-            Chunk<T>::pack(v);
-        pix += step;
-        while (pix >= hw) {
-            pix -= hw;
-            ++img;
+        for (int u = 0; u < SK_UNR; ++u) {
+            mm[u] += SK_UNR * step;
+            pix[u] += SK_UNR * step;
+            while (pix[u] >= hw) {
+                pix[u] -= hw;
+                ++img[u];
+            }
         }
     }
 }

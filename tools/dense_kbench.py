@@ -17,6 +17,8 @@ Specs (H, W at batch --batch; C = the concat-stack channels):
   grow:H:W      growth conv forward 64 -> 16, dropout (bytes x 64 + y 16)
   smallk:H:W:C  final_conv input gradient 2 -> C with a ReluGrad mask
                 (bytes dy 8 + mask C + dx C)
+A trailing ':nd' runs bn3x3 / fwdbn2 / grow without the dropout (its cost),
+':nm' smallk without the mask; copy:H:W:C times torch's copy of C channels.
 """
 import argparse
 import os
@@ -33,7 +35,8 @@ BF = torch.bfloat16
 
 def setup(spec, N, dev, ws):
     kind, *dims = spec.split(":")
-    dims = [int(v) for v in dims]
+    nodrop = dims[-1] in ("nd", "nm")       # trailing ':nd' / ':nm': without dropout / mask
+    dims = [int(v) for v in dims if v not in ("nd", "nm")]
     H, W = dims[0], dims[1]
     P = N * H * W
     g = torch.Generator(device=dev).manual_seed(1)
@@ -43,7 +46,7 @@ def setup(spec, N, dev, ws):
     if kind == "bn1x1":
         C = dims[2]
         d = ops.conv_desc(N, H, W, C, 64, 1, 1, dtype=ops.BF16)
-        dy, x, dx = rnd(N, H, W, 64), rnd(N, H, W, C), rnd(N, H, W, C)
+        dy, x, dx = rnd(N, H, W, 64), rnd(N, H, W, d.C), rnd(N, H, W, d.C)   # channels padded to 8
         w32 = torch.randn(1, 1, C, 64, device=dev, generator=g) / C ** 0.5
         wh = torch.zeros(ops.packed_shape(1, 1, C, 64, ops.PACK_HWIO, d.C), dtype=BF, device=dev)
         ops.pack_filter(w32, wh, d.C, 64, ops.PACK_HWIO)
@@ -63,7 +66,8 @@ def setup(spec, N, dev, ws):
 
         def run():
             part = torch.empty(ops.conv_bwd_data_bn_part_rows(d) * 2 * 64, device=dev)
-            return lambda: ops.conv2d_bwd_data_bn_part(d, dz, wh, x, gm, bt, dx, part, dropout=(0.2, 7))
+            return lambda: ops.conv2d_bwd_data_bn_part(d, dz, wh, x, gm, bt, dx, part,
+                                                       dropout=None if nodrop else (0.2, 7))
         return d, ops.OP_BWD_DATA_BN, run, P * 2 * (16 + 64 + 64)
     if kind == "fwdbn2":
         C = dims[2]
@@ -75,7 +79,7 @@ def setup(spec, N, dev, ws):
         y, a = torch.empty(N, H, W, 64, dtype=BF, device=dev), torch.empty(N, H, W, 64, dtype=BF, device=dev)
         pro = ops.prologue(torch.ones(C, device=dev), torch.zeros(C, device=dev))
         g2, b2 = torch.ones(64, device=dev), torch.zeros(64, device=dev)
-        epi = ops.epilogue(keep_prob=0.2, seed=3)
+        epi = ops.epilogue(keep_prob=1.0 if nodrop else 0.2, seed=3)
 
         def run():
             return lambda: ops.conv2d_fwd_bn2(d, x, pro, wk, y, a, g2, b2, True, 1e-3, epi, ws)
@@ -87,7 +91,7 @@ def setup(spec, N, dev, ws):
         wk = torch.zeros(ops.packed_shape(3, 3, 64, 16, ops.PACK_KRSC, 64), dtype=BF, device=dev)
         ops.pack_filter(w32, wk, 64, 16, ops.PACK_KRSC)
         y = torch.empty(N, H, W, 16, dtype=BF, device=dev)
-        epi = ops.epilogue(keep_prob=0.2, seed=5)
+        epi = ops.epilogue(keep_prob=1.0 if nodrop else 0.2, seed=5)
 
         def run():
             return lambda: ops.conv2d_fwd(d, x, wk, y, epi, ws)
@@ -102,8 +106,17 @@ def setup(spec, N, dev, ws):
         dx = torch.empty(N, H, W, C, dtype=BF, device=dev)
 
         def run():
-            return lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None, ops.epilogue(relu_mask=mask))
-        return d, ops.OP_BWD_DATA, run, P * 2 * (8 + 2 * C)
+            return lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None,
+                                               None if nodrop else ops.epilogue(relu_mask=mask))
+        return d, ops.OP_BWD_DATA, run, P * 2 * (8 + (1 if nodrop else 2) * C)
+    if kind == "copy":                       # torch's elementwise copy: an HBM reference point
+        C = dims[2]
+        d = ops.conv_desc(N, H, W, C, 2, 1, 1, dtype=ops.BF16)
+        src, dst = rnd(N, H, W, C), torch.empty(N, H, W, C, dtype=BF, device=dev)
+
+        def run():
+            return lambda: dst.copy_(src)
+        return d, ops.OP_BWD_DATA, run, P * 2 * 2 * C
     raise SystemExit(f"unknown spec {spec}")
 
 
