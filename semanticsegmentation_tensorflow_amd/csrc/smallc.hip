@@ -160,16 +160,18 @@ void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s) {
 // residual, ReluGrad).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int SK_MAXK = 16, SK_MAXN = 1024, SK_UNR = 4;
+constexpr int SK_MAXK = 16, SK_MAXN = 1024, SK_UNR = 2;
 
-template <typename T>
+// KK: the reduction rounded up to 2, 4, 8 or 16 (filter zero-padded), so the
+// k loop unrolls without per-k branches
+template <typename T, int KK>
 __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
-    extern __shared__ __attribute__((aligned(16))) float wsm[];   // [K][N]
+    extern __shared__ __attribute__((aligned(16))) float wsm[];   // [KK][N]
     const int K = p.K, NN = p.N;
     const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
-    for (int i = threadIdx.x; i < NN * K; i += 256) {
-        const int n = i / K, k = i - (i / K) * K;
-        wsm[k * NN + n] = to_f32(Wt[(long)n * p.w_col + k]);
+    for (int i = threadIdx.x; i < NN * KK; i += 256) {
+        const int n = i / KK, k = i - (i / KK) * KK;
+        wsm[k * NN + n] = k < K ? to_f32(Wt[(long)n * p.w_col + k]) : 0.f;
     }
     __syncthreads();
     const EpiParams& e = p.epi;
@@ -206,14 +208,15 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
     const T* __restrict__ RS = reinterpret_cast<const T*>(e.residual);
     const T* __restrict__ MK = reinterpret_cast<const T*>(e.mask);
     for (; mm[0] < p.M;) {
-        uint4 xq[SK_UNR][SK_MAXK / 8], rq[SK_UNR], mq[SK_UNR];
+        constexpr int XQ = (KK + 7) / 8;
+        uint4 xq[SK_UNR][XQ], rq[SK_UNR], mq[SK_UNR];
 #pragma unroll
         for (int u = 0; u < SK_UNR; ++u) {
             const bool ok = mm[u] < p.M;
             const T* xr = X + img[u] * p.x_img + (long)pix[u] * p.ldx;
 #pragma unroll
-            for (int q = 0; q < SK_MAXK / 8; ++q)
-                xq[u][q] = ok && q * 8 < K ? *reinterpret_cast<const uint4*>(xr + q * 8) : uint4{0u, 0u, 0u, 0u};
+            for (int q = 0; q < XQ; ++q)
+                xq[u][q] = ok ? *reinterpret_cast<const uint4*>(xr + q * 8) : uint4{0u, 0u, 0u, 0u};
             rq[u] = mq[u] = uint4{0u, 0u, 0u, 0u};
             if (ok && RS) rq[u] = *reinterpret_cast<const uint4*>(RS + img[u] * e.res_img + (long)pix[u] * e.ld_res + col0);
             if (ok && MK) mq[u] = *reinterpret_cast<const uint4*>(MK + img[u] * e.mask_img + (long)pix[u] * e.ld_mask + col0);
@@ -221,19 +224,17 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p) {
 #pragma unroll
         for (int u = 0; u < SK_UNR; ++u) {
             if (mm[u] >= p.M) break;
-            float xv[SK_MAXK];
+            float xv[XQ * 8];
 #pragma unroll
-            for (int q = 0; q < SK_MAXK / 8; ++q) Chunk<T>::unpack(xq[u][q], xv + q * 8);
+            for (int q = 0; q < XQ; ++q) Chunk<T>::unpack(xq[u][q], xv + q * 8);
             float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < SK_MAXK; ++k) {
-                if (k < K) {
-                    const float4 w0 = *reinterpret_cast<const float4*>(wsm + k * NN + col0);
-                    const float4 w1 = *reinterpret_cast<const float4*>(wsm + k * NN + col0 + 4);
-                    const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            for (int k = 0; k < KK; ++k) {
+                const float4 w0 = *reinterpret_cast<const float4*>(wsm + k * NN + col0);
+                const float4 w1 = *reinterpret_cast<const float4*>(wsm + k * NN + col0 + 4);
+                const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] += xv[k] * wk[j];
-                }
+                for (int j = 0; j < 8; ++j) v[j] += xv[k] * wk[j];
             }
             float res[8], mk[8];
             Chunk<T>::unpack(rq[u], res);
@@ -277,12 +278,23 @@ bool smallk_ok(const NTParams& p, int dtype) {
            (!p.epi.residual || p.epi.ld_res % 8 == 0) && (!p.epi.mask || p.epi.ld_mask % 8 == 0);
 }
 
+template <typename T>
+static void launch_smallk_t(NTParams& p, int grid, hipStream_t s) {
+    const int kk = p.K <= 2 ? 2 : p.K <= 4 ? 4 : p.K <= 8 ? 8 : 16;
+    const size_t lds = (size_t)p.N * kk * sizeof(float);
+    switch (kk) {
+        case 2: hipLaunchKernelGGL((smallk_nt_k<T, 2>), dim3(grid), dim3(256), lds, s, p); break;
+        case 4: hipLaunchKernelGGL((smallk_nt_k<T, 4>), dim3(grid), dim3(256), lds, s, p); break;
+        case 8: hipLaunchKernelGGL((smallk_nt_k<T, 8>), dim3(grid), dim3(256), lds, s, p); break;
+        default: hipLaunchKernelGGL((smallk_nt_k<T, 16>), dim3(grid), dim3(256), lds, s, p); break;
+    }
+}
+
 void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s) {
     const int pb = 256 / (p.N / 8);                  // pixels per block pass
     const int grid = (int)std::min<long>((p.M + pb - 1) / pb, (long)cus * 16);
-    const size_t lds = (size_t)p.N * p.K * sizeof(float);
-    if (dtype == SEG_F16) hipLaunchKernelGGL(smallk_nt_k<f16>, dim3(grid), dim3(256), lds, s, p);
-    else hipLaunchKernelGGL(smallk_nt_k<bf16>, dim3(grid), dim3(256), lds, s, p);
+    if (dtype == SEG_F16) launch_smallk_t<f16>(p, grid, s);
+    else launch_smallk_t<bf16>(p, grid, s);
 }
 
 

@@ -1,0 +1,7 @@
+set -o pipefail
+OUT=gpurun_out/r04_j14; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_smallk.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest_new.log 2>&1 || { tail -40 $OUT/pytest_new.log; exit 1; }
+tail -2 $OUT/pytest_new.log
+timeout -k 10 300 python -u tools/dense_kbench.py copy:384:1248:256 smallk:384:1248:256 smallk:384:1248:256:nm wg3x3:384:1248 wg1x1:384:1248:128 wg1x1:192:624:160 > $OUT/dense_kbench.txt 2>&1 || { tail -30 $OUT/dense_kbench.txt; exit 1; }
+grep -v "^round" $OUT/dense_kbench.txt
+echo done

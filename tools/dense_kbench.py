@@ -17,6 +17,8 @@ Specs (H, W at batch --batch; C = the concat-stack channels):
   grow:H:W      growth conv forward 64 -> 16, dropout (bytes x 64 + y 16)
   smallk:H:W:C  final_conv input gradient 2 -> C with a ReluGrad mask
                 (bytes dy 8 + mask C + dx C)
+  wg3x3:H:W     growth conv filter gradient (bytes x 64 + dz 16)
+  wg1x1:H:W:C   bottleneck filter gradient over relu(BN(x)) (bytes x C + dy 64)
 A trailing ':nd' runs bn3x3 / fwdbn2 / grow without the dropout (its cost),
 ':nm' smallk without the mask; copy:H:W:C times torch's copy of C channels.
 """
@@ -109,6 +111,26 @@ def setup(spec, N, dev, ws):
             return lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None,
                                                None if nodrop else ops.epilogue(relu_mask=mask))
         return d, ops.OP_BWD_DATA, run, P * 2 * (8 + (1 if nodrop else 2) * C)
+    if kind == "wg3x3":                      # growth conv filter gradient (64 -> 16, 3x3)
+        d = ops.conv_desc(N, H, W, 64, 16, 3, 3, dtype=ops.BF16)
+        x, dz = rnd(N, H, W, 64), rnd(N, H, W, 16)
+        dw = torch.empty(3, 3, 64, 16, device=dev)
+        ws.get(ops.conv_workspace(d, ops.OP_BWD_FILTER))
+
+        def run():
+            return lambda: ops.conv2d_bwd_filter(d, x, dz, dw, ws)
+        return d, ops.OP_BWD_FILTER, run, P * 2 * (64 + 16)
+    if kind == "wg1x1":                      # bottleneck filter gradient over relu(BN(x)) (C -> 64)
+        C = dims[2]
+        d = ops.conv_desc(N, H, W, C, 64, 1, 1, dtype=ops.BF16)
+        x, dy = rnd(N, H, W, d.C), rnd(N, H, W, 64)
+        dw = torch.empty(1, 1, C, 64, device=dev)
+        pro = ops.prologue(torch.ones(C, device=dev), torch.zeros(C, device=dev))
+        ws.get(ops.conv_workspace(d, ops.OP_BWD_FILTER))
+
+        def run():
+            return lambda: ops.conv2d_bwd_filter_pro(d, x, pro, dy, dw, ws)
+        return d, ops.OP_BWD_FILTER, run, P * 2 * (C + 64)
     if kind == "copy":                       # torch's elementwise copy: an HBM reference point
         C = dims[2]
         d = ops.conv_desc(N, H, W, C, 2, 1, 1, dtype=ops.BF16)
