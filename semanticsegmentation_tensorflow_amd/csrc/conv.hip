@@ -561,6 +561,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"wpad", &g_wpad, 0, 256, 8, {}},
 #ifdef SEG_DIAG
         {"tn3_abl", &seg::g_tn3_abl, 0, 3, 1, {}},
+        {"smallk_abl", &seg::g_smallk_abl, 0, 3, 1, {}},
         {"tn3_adam_abl", &seg::g_tn3_adam_abl, 0, 31, 1, {}},
         {"wgrad_abl", &seg::g_wgrad_abl, 0, 3, 1, {}},
         {"nt2_ablate", &seg::g_nt2_ablate, 0, 9, 1, {}},
