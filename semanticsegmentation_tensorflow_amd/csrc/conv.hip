@@ -133,6 +133,7 @@ static NTParams conv_bwd_data_params(const seg_conv_desc* d) {
     p.w_col = d->K + g_wpad; p.w_tap = (long)d->C * (d->K + g_wpad); p.rstep = 1; p.sstep = 1; p.Sfull = d->S;
     p.y_img = (long)d->H * d->W * d->ldx; p.OH = d->H; p.OW = d->W; p.ldy = d->ldx; p.osh = 1; p.osw = 1;
     p.epi.n_valid = d->C; p.epi.keep_prob = 1.f;
+    p.kv = d->k_valid;
     return p;
 }
 

@@ -99,6 +99,7 @@ struct NTParams {
     // conv2d_transpose phase split: blockIdx.z = ph*st_w + pw
     int phase, st_h, st_w, pad_t, pad_l, Nimg;
     ProParams pro;
+    int kv;        // valid reduction channels per tap (0: all C; the rest are zero padding)
 };
 
 // C[m][n] = sum_p A[p][m] B[p][n].  p -> (img, a, b) on an Ha x Wa grid;

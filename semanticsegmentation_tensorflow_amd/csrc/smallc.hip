@@ -180,7 +180,6 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p, int abl) {
     const int CK = p.N / 8, PB = 256 / CK;
     const int prow = threadIdx.x / CK, ck = threadIdx.x - prow * CK;
     const int col0 = ck * 8;
-    const int hw = p.OH * p.OW;
     const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
     for (int i = threadIdx.x; i < NN * KK; i += 256) {
         const int n = i / KK, k = i - (i / KK) * KK;
@@ -199,26 +198,24 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p, int abl) {
     }
     constexpr int XQ = (KK + 7) / 8;
     const int base = blockIdx.x * (SK_RPT * PB) + prow;
+    T* __restrict__ Y = reinterpret_cast<T*>(p.y);
     for (int r0 = 0; r0 < SK_RPT; r0 += SK_UNR) {
         uint4 xq[SK_UNR][XQ], rq[SK_UNR], mq[SK_UNR];
-        int img[SK_UNR], pix[SK_UNR];
 #pragma unroll
         for (int u = 0; u < SK_UNR; ++u) {
-            const int m = base + (r0 + u) * PB;
+            const long m = base + (r0 + u) * PB;
             const bool ok = m < p.M && !(abl & 1);
-            const int mm = ok ? m : 0;
-            img[u] = mm / hw;
-            pix[u] = mm - img[u] * hw;
-            const T* xr = X + img[u] * p.x_img + (long)pix[u] * p.ldx;
+            const long mm = ok ? m : 0;             // dense pixel rows (smallk_ok)
 #pragma unroll
-            for (int q = 0; q < XQ; ++q) xq[u][q] = ok ? *reinterpret_cast<const uint4*>(xr + q * 8) : uint4{0u, 0u, 0u, 0u};
+            for (int q = 0; q < XQ; ++q)
+                xq[u][q] = ok ? *reinterpret_cast<const uint4*>(X + mm * p.ldx + q * 8) : uint4{0u, 0u, 0u, 0u};
             rq[u] = mq[u] = uint4{0u, 0u, 0u, 0u};
-            if (ok && RS) rq[u] = *reinterpret_cast<const uint4*>(RS + img[u] * e.res_img + (long)pix[u] * e.ld_res + col0);
-            if (ok && MK) mq[u] = *reinterpret_cast<const uint4*>(MK + img[u] * e.mask_img + (long)pix[u] * e.ld_mask + col0);
+            if (ok && RS) rq[u] = *reinterpret_cast<const uint4*>(RS + mm * e.ld_res + col0);
+            if (ok && MK) mq[u] = *reinterpret_cast<const uint4*>(MK + mm * e.ld_mask + col0);
         }
 #pragma unroll
         for (int u = 0; u < SK_UNR; ++u) {
-            const int m = base + (r0 + u) * PB;
+            const long m = base + (r0 + u) * PB;
             if (m >= p.M) break;
             float xv[XQ * 8];
 #pragma unroll
@@ -247,9 +244,7 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p, int abl) {
                 if (MK) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = cv ? x : 0.f;
             }
-            if (!(abl & 2) || v[0] == -1234.5f)
-                *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img[u] * p.y_img + (long)pix[u] * p.ldy + col0) =
-                    Chunk<T>::pack(v);
+            if (!(abl & 2) || v[0] == -1234.5f) *reinterpret_cast<uint4*>(Y + m * p.ldy + col0) = Chunk<T>::pack(v);
         }
     }
 }
@@ -264,12 +259,18 @@ bool smallk_ok(const NTParams& p, int dtype) {
            p.iow == 0 && p.osh == 1 && p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.IH == p.Ha && p.IW == p.Wa &&
            p.OH == p.Ha && p.OW == p.Wa && p.M > 0 && p.M % (p.OH * p.OW) == 0 && p.ldx % 8 == 0 &&
            p.ldy % 8 == 0 && !p.pro.gamma && !p.epi.bn_x && !p.epi.pool_y && !p.epi.y2 &&
+           p.x_img == (long)p.OH * p.OW * p.ldx && p.y_img == (long)p.OH * p.OW * p.ldy &&
+           (!p.epi.residual || p.epi.res_img == (long)p.OH * p.OW * p.epi.ld_res) &&
+           (!p.epi.mask || p.epi.mask_img == (long)p.OH * p.OW * p.epi.ld_mask) &&
            (!p.epi.residual || p.epi.ld_res % 8 == 0) && (!p.epi.mask || p.epi.ld_mask % 8 == 0);
 }
 
 template <typename T>
 static void launch_smallk_t(NTParams& p, int grid, hipStream_t s) {
-    const int kk = p.K <= 2 ? 2 : p.K <= 4 ? 4 : p.K <= 8 ? 8 : 16;
+    // the valid reduction only: the padded channels' products are exact zeros
+    // added to a +0-started sum, so dropping them changes no bit
+    const int kr = p.kv > 0 && p.kv < p.K ? p.kv : p.K;
+    const int kk = kr <= 2 ? 2 : kr <= 4 ? 4 : kr <= 8 ? 8 : 16;
     const size_t lds = (size_t)p.N * kk * sizeof(float);
     switch (kk) {
         case 2: hipLaunchKernelGGL((smallk_nt_k<T, 2>), dim3(grid), dim3(256), lds, s, p, g_smallk_abl); break;
