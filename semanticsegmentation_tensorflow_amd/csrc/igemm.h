@@ -169,6 +169,7 @@ extern int g_nt2bn_bm;
 long nt2_bn_rows(int M);
 // dense1x1.hip: the 1x1 BN-backward input gradient streamed (K = 64)
 extern int g_bn1x1s;
+extern int g_bn1x1s_st;
 bool bn1x1s_ok(const NTParams& p, int dtype);
 int bn1x1s_rows(const NTParams& p, int cus);
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s);

@@ -124,14 +124,18 @@ BNB_CASES = [(2, 9, 11, 48, 64, 1), (1, 12, 10, 136, 64, 1), (1, 33, 41, 200, 13
              (1, 17, 19, 24, 8, 1), (2, 40, 52, 112, 64, 1)]
 
 
-@pytest.fixture(params=[(1, 256), (0, 256), (0, 128)], ids=["stream", "bm256", "bm128"])
+@pytest.fixture(params=[(1, 1, 256), (1, 0, 256), (0, 1, 256), (0, 1, 128)],
+                ids=["stream", "stream8", "bm256", "bm128"])
 def nt2bn_bm(request):
-    """Every 1x1 form: bn1x1_stream (K = 64; option bn1x1s) and igemm_nt2_bn
-    at both M-tile heights (option nt2bn_bm)."""
+    """Every 1x1 form: bn1x1_stream (K = 64; option bn1x1s) with staged
+    16-byte or direct 8-byte dx stores (bn1x1s_st), and igemm_nt2_bn at both
+    M-tile heights (option nt2bn_bm)."""
     ops.set_option("bn1x1s", request.param[0])
-    ops.set_option("nt2bn_bm", request.param[1])
+    ops.set_option("bn1x1s_st", request.param[1])
+    ops.set_option("nt2bn_bm", request.param[2])
     yield request.param
     ops.set_option("bn1x1s", 1)
+    ops.set_option("bn1x1s_st", 1)
     ops.set_option("nt2bn_bm", 256)
 
 
