@@ -35,7 +35,6 @@ constexpr int S1_NST = 6;        // ring stages of S1_TP x 64 channels
 constexpr int S1_MAXC = 256;
 constexpr int S1_NW = 8;
 constexpr int S1_DMA = S1_TP / 8 / S1_NW;   // DMA instructions per wave per step (2)
-constexpr int S1_ST = 4;                    // epilogue stores per wave per tile (one per 16-channel block)
 
 // wait until at most n younger vector-memory instructions are outstanding
 __device__ __forceinline__ void wait_vm_rt(int n) {
@@ -48,8 +47,12 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     }
 }
 
-template <typename T, bool PRO>
+// STAGED: the wave's 16 x 64 output tile (and the BN2 map) leaves through the
+// wave's consumed ring rows as 16-byte stores of whole 128-byte rows (2 per
+// lane per map) instead of 8-byte stores of 32-byte row pieces (4 per lane)
+template <typename T, bool PRO, bool STAGED = false>
 __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles, int kt) {
+    constexpr int S1_ST = STAGED ? 2 : 4;      // epilogue stores per wave per tile and map
     constexpr int STG = S1_TP * 128;
     __shared__ __attribute__((aligned(16))) char ring[S1_NST * STG];            // 96 KiB
     __shared__ __attribute__((aligned(16))) char wsm[64 * S1_MAXC * 2];          // 32 KiB
@@ -161,6 +164,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
             const int t = (int)blockIdx.x + (s / kt) * (int)gridDim.x;
             const long m = (long)t * S1_TP + xrow;
             const uint64_t gidx = (uint64_t)m * e.n_valid;
+            uint2 ob[4], ob2[4];
 #pragma unroll
             for (int nf = 0; nf < 4; ++nf) {
                 const int col0 = nf * 16 + 4 * fg;
@@ -175,9 +179,12 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
                     o[j] = from_f32<T>(col0 + j < e.n_valid ? v : 0.f);
                 }
                 const bool ok = m < p.M && col0 < p.N;
-                uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + m * p.ldy + col0)
-                                : s1_trash + (tid & 4095);
-                *dst = *reinterpret_cast<const uint2*>(o);
+                ob[nf] = *reinterpret_cast<const uint2*>(o);
+                if constexpr (!STAGED) {
+                    uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + m * p.ldy + col0)
+                                    : s1_trash + (tid & 4095);
+                    *dst = ob[nf];
+                }
                 if (e.y2) {      // BN2(+ReLU) of the stored values (seg_bn_relu_fwd's arithmetic)
                     const f32x4 s2 = *reinterpret_cast<const f32x4*>(&etab[2][col0]);
                     const f32x4 t2 = *reinterpret_cast<const f32x4*>(&etab[3][col0]);
@@ -188,11 +195,39 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
                         if (e.bn2_relu) v2 = fmaxf(v2, 0.f);
                         o2[j] = from_f32<T>(v2);
                     }
-                    uint2* dst2 = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(e.y2) + m * e.ld_y2 + col0)
-                                     : s1_trash + (tid & 4095);
-                    *dst2 = *reinterpret_cast<const uint2*>(o2);
+                    ob2[nf] = *reinterpret_cast<const uint2*>(o2);
+                    if constexpr (!STAGED) {
+                        uint2* dst2 = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(e.y2) + m * e.ld_y2 + col0)
+                                         : s1_trash + (tid & 4095);
+                        *dst2 = ob2[nf];
+                    }
                 }
                 acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            if constexpr (STAGED) {
+                // this step's stage rows of the wave (16 x 128 B) are consumed
+                char* Sw = const_cast<char*>(Xs) + w * 2048;
+                const int row = lane >> 2;
+                const long mr = (long)t * S1_TP + w * 16 + row;
+                auto flush = [&](const uint2* v, T* base, int ld) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int nf = 0; nf < 4; ++nf)
+                        *reinterpret_cast<uint2*>(Sw + fr * 128 + 16 * ((2 * nf + (fg >> 1)) ^ ((fr >> 1) & 7)) +
+                                                  8 * (fg & 1)) = v[nf];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int c = (lane & 3) * 2 + h;
+                        const uint4 q = *reinterpret_cast<const uint4*>(Sw + row * 128 + 16 * (c ^ ((row >> 1) & 7)));
+                        const bool ok = mr < p.M && c * 8 < p.N;
+                        uint4* dst = ok ? reinterpret_cast<uint4*>(base + mr * ld + c * 8)
+                                        : reinterpret_cast<uint4*>(s1_trash) + (tid & 2047);
+                        *dst = q;
+                    }
+                };
+                flush(ob, reinterpret_cast<T*>(p.y), p.ldy);
+                if (e.y2) flush(ob2, reinterpret_cast<T*>(e.y2), e.ld_y2);
             }
         }
     }
@@ -448,7 +483,7 @@ int bn1x1s_rows(const NTParams& p, int cus) {
     return std::min(G, std::max(8, (ntiles + 7) & ~7));
 }
 
-int g_bn1x1s_st = 1;   // staged 16-byte dx stores (0: 8-byte stores from the accumulators)
+int g_bn1x1s_st = 0;   // 1: staged 16-byte dx stores (faster alone, slower in the C3 step: 211 vs 212 img/s)
 
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
     if (!bn1x1s_args_ok(p)) return SEG_EINVAL;
@@ -467,17 +502,27 @@ int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
     return SEG_OK;
 }
 
+int g_s1x1_st = 0;   // 1: staged 16-byte output stores when the rows allow them
+
+template <typename T, bool PRO>
+static void launch_s1x1_t(NTParams& p, int grid, int ntiles, int kt, bool st, hipStream_t s) {
+    if (st) hipLaunchKernelGGL((conv1x1_stream<T, PRO, true>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+    else hipLaunchKernelGGL((conv1x1_stream<T, PRO, false>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+}
+
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {
     const int ntiles = (p.M + S1_TP - 1) / S1_TP;
     const int kt = (p.K + 63) / 64;
     const int grid = std::min(ntiles, cus);
     const bool pro = p.pro.gamma != nullptr;
+    const bool st = g_s1x1_st && p.N % 8 == 0 && p.ldy % 8 == 0 && ((uintptr_t)p.y % 16) == 0 &&
+                    (!p.epi.y2 || (p.epi.ld_y2 % 8 == 0 && ((uintptr_t)p.epi.y2 % 16) == 0));
     if (dtype == SEG_F16) {
-        if (pro) hipLaunchKernelGGL((conv1x1_stream<f16, true>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
-        else hipLaunchKernelGGL((conv1x1_stream<f16, false>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+        if (pro) launch_s1x1_t<f16, true>(p, grid, ntiles, kt, st, s);
+        else launch_s1x1_t<f16, false>(p, grid, ntiles, kt, st, s);
     } else {
-        if (pro) hipLaunchKernelGGL((conv1x1_stream<bf16, true>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
-        else hipLaunchKernelGGL((conv1x1_stream<bf16, false>), dim3(grid), dim3(512), 0, s, p, ntiles, kt);
+        if (pro) launch_s1x1_t<bf16, true>(p, grid, ntiles, kt, st, s);
+        else launch_s1x1_t<bf16, false>(p, grid, ntiles, kt, st, s);
     }
 }
 

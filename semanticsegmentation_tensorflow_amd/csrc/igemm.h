@@ -170,6 +170,7 @@ long nt2_bn_rows(int M);
 // dense1x1.hip: the 1x1 BN-backward input gradient streamed (K = 64)
 extern int g_bn1x1s;
 extern int g_bn1x1s_st;
+extern int g_s1x1_st;
 bool bn1x1s_ok(const NTParams& p, int dtype);
 int bn1x1s_rows(const NTParams& p, int cus);
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s);

@@ -22,9 +22,10 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("st", [0, 1], ids=["st8", "st16"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES)
-def test_conv_bn2_equals_conv_then_bn_relu(dev, case, dtype):
+def test_conv_bn2_equals_conv_then_bn_relu(dev, case, dtype, st):
     N, H, W, C, K, with_pro, fam, kp = case
     dt = ops.BF16 if dtype == torch.bfloat16 else ops.F16
     d = ops.conv_desc(N, H, W, C, K, 1, 1, dtype=dt)
@@ -45,6 +46,7 @@ def test_conv_bn2_equals_conv_then_bn_relu(dev, case, dtype):
     pro = ops.prologue(g1, b1) if with_pro else None
     epi = ops.epilogue(keep_prob=kp, seed=99)
     ws = ops.Workspace(dev)
+    ops.set_option("s1x1_st", st)       # conv1x1_stream's staged 16-byte stores (both launches)
     # the pair
     y_ref = torch.full((N, H, W, K), float("nan"), dtype=dtype, device=dev)
     if with_pro:
@@ -58,6 +60,7 @@ def test_conv_bn2_equals_conv_then_bn_relu(dev, case, dtype):
     a = torch.full_like(y_ref, float("nan"))
     ops.conv2d_fwd_bn2(d, x, pro, wk, y, a, g2, b2, True, 1e-3, epi, ws)
     torch.cuda.synchronize()
+    ops.set_option("s1x1_st", 0)
     assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
     assert torch.equal(a.view(torch.int16), a_ref.view(torch.int16))
     zero = (a == 0).float().mean().item()

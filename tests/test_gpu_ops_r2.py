@@ -135,7 +135,7 @@ def nt2bn_bm(request):
     ops.set_option("nt2bn_bm", request.param[2])
     yield request.param
     ops.set_option("bn1x1s", 1)
-    ops.set_option("bn1x1s_st", 1)
+    ops.set_option("bn1x1s_st", 0)
     ops.set_option("nt2bn_bm", 256)
 
 
@@ -243,10 +243,18 @@ def _np_uniform_vec(seed, idx):
     return ((x >> np.uint64(8)).astype(np.float64) / 16777216.0).astype(np.float32)
 
 
+@pytest.fixture(params=[0, 1], ids=["st8", "st16"])
+def s1x1_st(request):
+    """conv1x1_stream's direct 8-byte and staged 16-byte stores (option s1x1_st)."""
+    ops.set_option("s1x1_st", request.param)
+    yield request.param
+    ops.set_option("s1x1_st", 0)
+
+
 @pytest.mark.parametrize("kp", [1.0, 0.2], ids=["no-dropout", "dropout"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", S1_CASES)
-def test_conv1x1_stream_bn_relu_dropout(dev, case, dtype, kp):
+def test_conv1x1_stream_bn_relu_dropout(dev, case, dtype, kp, s1x1_st):
     from tests.test_gpu_ops import _np_uniform
     N, H, W, C, K = case
     x, w, gamma, beta, xr, wr, a = _pro_case((N, H, W, C, K, 1), dtype, dev)
