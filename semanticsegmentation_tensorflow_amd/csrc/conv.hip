@@ -558,7 +558,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"nt2bn_bm", &seg::g_nt2bn_bm, 0, 0, 0, {128, 256}},
         {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
         {"bn1x1s_st", &seg::g_bn1x1s_st, 0, 1, 1, {}},
-        {"s1x1_st", &seg::g_s1x1_st, 0, 1, 1, {}},
+        {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},

@@ -502,7 +502,10 @@ int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
     return SEG_OK;
 }
 
-int g_s1x1_st = 0;   // 1: staged 16-byte output stores when the rows allow them
+// staged 16-byte output stores: 0 never, 1 for single-k-tile launches (C <= 64:
+// write-dominated, 393 vs 475 us at 384x1248x8, C = 48; C3 212 -> 213.5 img/s),
+// 2 always (C = 128 / 144: 1-4 % slower)
+int g_s1x1_st = 1;
 
 template <typename T, bool PRO>
 static void launch_s1x1_t(NTParams& p, int grid, int ntiles, int kt, bool st, hipStream_t s) {
@@ -515,7 +518,8 @@ void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {
     const int kt = (p.K + 63) / 64;
     const int grid = std::min(ntiles, cus);
     const bool pro = p.pro.gamma != nullptr;
-    const bool st = g_s1x1_st && p.N % 8 == 0 && p.ldy % 8 == 0 && ((uintptr_t)p.y % 16) == 0 &&
+    const bool st = (g_s1x1_st == 2 || (g_s1x1_st == 1 && kt == 1)) && p.N % 8 == 0 && p.ldy % 8 == 0 &&
+                    ((uintptr_t)p.y % 16) == 0 &&
                     (!p.epi.y2 || (p.epi.ld_y2 % 8 == 0 && ((uintptr_t)p.epi.y2 % 16) == 0));
     if (dtype == SEG_F16) {
         if (pro) launch_s1x1_t<f16, true>(p, grid, ntiles, kt, st, s);

@@ -243,12 +243,12 @@ def _np_uniform_vec(seed, idx):
     return ((x >> np.uint64(8)).astype(np.float64) / 16777216.0).astype(np.float32)
 
 
-@pytest.fixture(params=[0, 1], ids=["st8", "st16"])
+@pytest.fixture(params=[0, 2], ids=["st8", "st16"])
 def s1x1_st(request):
     """conv1x1_stream's direct 8-byte and staged 16-byte stores (option s1x1_st)."""
     ops.set_option("s1x1_st", request.param)
     yield request.param
-    ops.set_option("s1x1_st", 0)
+    ops.set_option("s1x1_st", 1)
 
 
 @pytest.mark.parametrize("kp", [1.0, 0.2], ids=["no-dropout", "dropout"])
