@@ -85,3 +85,28 @@ def test_product_library_has_no_ablation_knobs():
     assert lib.seg_set_option(b"tn_reduce_sl", 3) == EINVAL
     assert lib.seg_set_option(b"tn_reduce_sl", 16) == 0
     assert lib.seg_set_option(b"wpad", 12) == EINVAL
+
+
+def test_bn_part_launch_refuses_a_foreign_row_count():
+    """seg_conv2d_bwd_data_bn_part writes exactly seg_conv_bwd_data_bn_part_rows
+    partial rows -- the count a batched finish plan was made for; any other
+    part_rows (a buffer sized under another kernel option) is refused with
+    SEG_EWORKSPACE on the host (fake pointers, never touched).  The row count
+    follows the launch geometry: bn1x1_stream blocks per 64-channel chunk, or
+    igemm_nt2_bn M tiles."""
+    import ctypes
+    lib = _lib.load()
+    d = _lib.SegConvDesc()
+    assert lib.seg_conv_desc_init(ctypes.byref(d), 8, 384, 1248, 128, 64, 1, 1, 1, 1, 0, 1) == 0
+    rows = lib.seg_conv_bwd_data_bn_part_rows(ctypes.byref(d))
+    assert rows > 0
+    assert lib.seg_set_option(b"bn1x1s", 0) == 0
+    try:
+        rows_nt2 = lib.seg_conv_bwd_data_bn_part_rows(ctypes.byref(d))
+    finally:
+        assert lib.seg_set_option(b"bn1x1s", 1) == 0
+    assert rows_nt2 == (8 * 384 * 1248 + 255) // 256 and rows_nt2 != rows
+    fake = ctypes.c_void_p(1 << 20)
+    bn = _lib.SegBnBwd(1 << 20, 128, 1 << 20, 1 << 20, 1e-3, 1, 1, None, None, 1.0, 0)
+    st = lib.seg_conv2d_bwd_data_bn_part(ctypes.byref(d), fake, fake, ctypes.byref(bn), fake, fake, rows_nt2, None)
+    assert st == 4, st                  # SEG_EWORKSPACE
