@@ -1558,7 +1558,10 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
 // holds the kernel at 160 VGPRs, three waves per SIMD: 8-row tiles (8-wave
 // blocks) fit one block per CU, 4-row tiles (4-wave blocks) three, and the
 // blocks' epilogues, MFMAs and loads then overlap.
-template <typename T = bf16, bool BNB = false, int BH = 8>
+// ST: the wave's 64 px x 32 ch output tile goes through a per-wave LDS
+// buffer and leaves as 16-byte stores of 64-byte row halves (4 per lane per
+// tile) instead of 8-byte stores of 32-byte pieces (8 per lane)
+template <typename T = bf16, bool BNB = false, int BH = 8, bool ST = false>
 __global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res16c(NTParams p, int tiles_x, int tiles_y,
                                                                                   int ntiles) {
     static_assert(BH == 8 || BH == 4 || BH == 2, "tile rows");
@@ -1569,6 +1572,7 @@ __global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res
     constexpr int BS = KS * 64 * 64;
     constexpr int HS = HROWS * 32 > NW * 2 * 32 * 4 ? HROWS * 32 : NW * 2 * 32 * 4;
     __shared__ __attribute__((aligned(16))) char smem[BS + HS];
+    __shared__ __attribute__((aligned(16))) char stg[ST ? NW * 4096 : 16];
     char* Bs = smem;
     char* Hs = smem + BS;
 
@@ -1772,8 +1776,29 @@ __global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
                         }
                     }
-                    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
-                        *reinterpret_cast<const uint2*>(o);
+                    if constexpr (ST) {
+                        const int r = mi * 16 + fr;
+                        *reinterpret_cast<uint2*>(stg + w * 4096 + r * 64 + 16 * ((ni * 2 + (fg >> 1)) ^ ((r >> 2) & 3)) +
+                                                  8 * (fg & 1)) = *reinterpret_cast<const uint2*>(o);
+                    } else {
+                        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
+                            *reinterpret_cast<const uint2*>(o);
+                    }
+                }
+            }
+            if constexpr (ST) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const int c = lane & 3;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = q * 16 + (lane >> 2);
+                    const uint4 v = *reinterpret_cast<const uint4*>(stg + w * 4096 + r * 64 + 16 * (c ^ ((r >> 2) & 3)));
+                    const int ml = wm * WTM + r;
+                    const int oy = oy0 + ml / R64_BW, ox = ox0 + ml % R64_BW;
+                    const int col = wn * WTN + c * 8;
+                    if (oy < p.OH && ox < p.OW && col < p.N)
+                        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + img * p.y_img +
+                                                  ((long)oy * p.OW + ox) * p.ldy + col) = v;
                 }
             }
         }
@@ -1967,11 +1992,15 @@ int res16c_grid(const NTParams& p, int cus) {
     return std::min((p.M / (p.OH * p.OW)) * tx * ty, (bh == 8 ? 2 : 6) * cus);
 }
 
+int g_res16c_st = 0;   // 1: staged 16-byte dx stores in the BN-backward form
+
 template <typename T, int BH>
 static void launch_res16c_bn_t(NTParams& p, int grid, hipStream_t s) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + BH - 1) / BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
-    hipLaunchKernelGGL((conv_res16c<T, true, BH>), dim3(grid), dim3(BH * 64), 0, s, p, tx, ty, ntiles);
+    const bool st = g_res16c_st && p.ldy % 8 == 0 && p.y_img % 8 == 0 && ((uintptr_t)p.y % 16) == 0;
+    if (st) hipLaunchKernelGGL((conv_res16c<T, true, BH, true>), dim3(grid), dim3(BH * 64), 0, s, p, tx, ty, ntiles);
+    else hipLaunchKernelGGL((conv_res16c<T, true, BH>), dim3(grid), dim3(BH * 64), 0, s, p, tx, ty, ntiles);
 }
 
 void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype) {

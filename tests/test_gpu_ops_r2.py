@@ -180,11 +180,15 @@ def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate, nt2bn_bm)
 BNB3_CASES = [(2, 21, 67, 64, 16), (1, 30, 70, 64, 16), (2, 9, 11, 32, 16)]
 
 
-@pytest.fixture(params=[4, 8, 2], ids=["bh4", "bh8", "bh2"])
+@pytest.fixture(params=[(4, 0), (8, 0), (2, 0), (4, 1), (8, 1)], ids=["bh4", "bh8", "bh2", "bh4st", "bh8st"])
 def res16c_bh(request):
-    ops.set_option("res16c_bh", request.param)
+    """Tile heights (option res16c_bh) and the staged 16-byte dx stores
+    (option res16c_st)."""
+    ops.set_option("res16c_bh", request.param[0])
+    ops.set_option("res16c_st", request.param[1])
     yield request.param
     ops.set_option("res16c_bh", 4)
+    ops.set_option("res16c_st", 0)
 
 
 @pytest.mark.parametrize("kp", [1.0, 0.6], ids=["no-dropout", "dropout"])
