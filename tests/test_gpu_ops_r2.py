@@ -188,7 +188,7 @@ def res16c_bh(request):
     ops.set_option("res16c_st", request.param[1])
     yield request.param
     ops.set_option("res16c_bh", 4)
-    ops.set_option("res16c_st", 0)
+    ops.set_option("res16c_st", 1)
 
 
 @pytest.mark.parametrize("kp", [1.0, 0.6], ids=["no-dropout", "dropout"])
