@@ -560,6 +560,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"bn1x1s_st", &seg::g_bn1x1s_st, 0, 1, 1, {}},
         {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
         {"res16c_st", &seg::g_res16c_st, 0, 1, 1, {}},
+        {"dropout_flat", &seg::g_dropout_flat, 0, 1, 1, {}},
         {"smallc", &seg::g_smallc, 0, 1, 1, {}},
         {"smallk", &seg::g_smallk, 0, 1, 1, {}},
         {"wpad", &g_wpad, 0, 256, 8, {}},

@@ -382,6 +382,29 @@ __global__ __launch_bounds__(256) void dropout_ch_k(const T* __restrict__ dy, in
     }
 }
 
+// The same re-draw with one 8-channel chunk per thread over a grid of all
+// (pixel, chunk) pairs: no grid-stride loop, the chunk's loads issued at once
+// (the loop form above ran FC-DenseNet's 16-channel growth outputs at ~1.5-2
+// TB/s, instruction-bound like smallk_nt's first forms)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_ch_flat_k(const T* __restrict__ dy, int ldy, T* __restrict__ dz, int ldz,
+                                                         int P, int CK, int cv, float kp, uint64_t seed) {
+    constexpr int EPC = dt_traits<T>::EPC;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= P * CK) return;
+    const int pix = q / CK, cc = q - pix * CK;
+    const float rkp = 1.f / kp;
+    const uint64_t base = (uint64_t)pix * cv;
+    float v[EPC];
+    Chunk<T>::unpack(ldc(dy + (long)pix * ldy + cc * EPC), v);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+        const int c = cc * EPC + e;
+        v[e] = c < cv ? (v[e] * rkp) * floorf(kp + seg_uniform(seed, base + c)) : 0.f;
+    }
+    stc(dz + (long)pix * ldz + cc * EPC, Chunk<T>::pack(v));
+}
+
 template <typename T>
 __global__ void fill_k(T* y, long n, float v) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -1107,11 +1130,24 @@ extern "C" int seg_dropout_bwd(const void* dy, void* dx, long n, float kp, uint6
     return seg_dropout_fwd(dy, dx, n, kp, seed, dtype, stream);
 }
 
+namespace seg {
+int g_dropout_flat = 1;   // dropout re-draw: one chunk per thread (0: the grid-stride loop)
+}
+
 extern "C" int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C, int cv, float kp,
                                   uint64_t seed, int dtype, void* stream) {
     if (!dy || !dz || !(kp > 0.f) || kp > 1.f || (C & 7) || cv > C || ldy < C || ldz < C) return SEG_EINVAL;
     if (C > 4096) return SEG_EINVAL;
     const RedGeom g = red_geom(C, epc_of(dtype));
+    const long chunks = P * (long)g.CK;
+    if (seg::g_dropout_flat && chunks < (1L << 31) - 256) {
+        const int CK = g.CK;
+        DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_flat_k<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                                             (hipStream_t)stream, (const T*)dy, ldy, (T*)dz, ldz, (int)P, CK, cv, kp,
+                                             seed));
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     const long blocks = std::max<long>(1, std::min<long>((P + g.rows - 1) / g.rows, 16384));
     DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_k<T>, dim3((unsigned)blocks), dim3(256), 0,
                                          (hipStream_t)stream, (const T*)dy, ldy, (T*)dz, ldz, P, C, cv, kp, seed));

@@ -172,6 +172,7 @@ extern int g_bn1x1s;
 extern int g_bn1x1s_st;
 extern int g_s1x1_st;
 extern int g_res16c_st;
+extern int g_dropout_flat;
 bool bn1x1s_ok(const NTParams& p, int dtype);
 int bn1x1s_rows(const NTParams& p, int cus);
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s);
