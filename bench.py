@@ -23,17 +23,10 @@ import re
 import sys
 import time
 
-# Hardware queues per process, before the HIP runtime starts: HIP's default of 4
-# is taken by torch's stream, RCCL's streams and the Session's side stream, so
-# under data parallelism the side stream (filter gradients beside the
-# input-gradient chain) shared a queue with the compute stream and ran serially
-# (world-1 DP step 8.40 -> 7.69 ms with 8 queues; N=1 unchanged).  Unset or
-# HIP's default 4 (the GPU box exports 4) -> 8; any other value the user set is
-# kept.  The requested and effective values are recorded in the result line.
-_HWQ_USER = os.environ.get("GPU_MAX_HW_QUEUES")
-if _HWQ_USER is None or _HWQ_USER.strip() == "4":
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
+# HIP hardware queues per process: left as the environment sets them (the GPU
+# box exports GPU_MAX_HW_QUEUES=4, HIP's own default); the value in effect is
+# recorded in the result line.  The Session's stream layout is sized for 4
+# (DESIGN.md section 6).
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -89,6 +82,9 @@ def parse():
     ap.add_argument("--no-dp-probe", action="store_true",
                     help="N=1: skip the side line that re-times the step through a world-1 RCCL data-parallel Session")
     ap.add_argument("--no-inference", action="store_true", help="skip the inference-latency line")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank path (no GPU): --gpus N starts N rank processes over "
+                         "gloo, each times K trivial steps, rank 0 prints the line with n_gpus = the world size")
     ap.add_argument("--overlap-optimizer", action="store_true",
                     help="per-layer Adam on a side stream as gradients become final (measured slower: the "
                          "HBM-bound update steals CUs from the MFMA-bound backward)")
@@ -316,8 +312,13 @@ def kernel_symbol(name):
         return rf"igemm_tn2(<{bm}, {bn},|I\w*Li{bm}ELi{bn}E)"
     if fam == "wgrad_halo":
         return rf"wgrad_halo(<\d+, {bn},|ILi\d+ELi{bn}E)"
+    # family names whose kernel symbol differs from the family name
     return {"conv_res64": r"conv_res64[<I]", "conv_c8": r"conv_c8_fwd", "wgrad_c8": r"wgrad_c8",
-            "igemm_nt": r"igemm_ntI", "igemm_tn": r"igemm_tnI"}.get(fam, re.escape(fam))
+            "igemm_nt": r"igemm_ntI", "igemm_tn": r"igemm_tnI",
+            "bn1x1_stream": r"bn1x1_dgrad_stream", "conv1x1_stream": r"conv1x1_stream",
+            "conv_res16c_bn": r"conv_res16cIDF16[b_]Lb1E", "smallk_nt": r"smallk_nt_k",
+            "igemm_nt2_pro": r"igemm_nt2I\w*Lb1ELb0EEEv", "igemm_tn2_pro": r"igemm_tn2I\w*Lb1EEEv",
+            }.get(fam, re.escape(fam))
 
 
 def pmc_traffic(argv, symbol, out_dir):
@@ -611,12 +612,106 @@ def dp_probe(args, B, H, W, kp, device):
                     "skips them and runs the single-process plan)"}
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without torchrun: start N rank
+    processes of this script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE =
+    N, rendezvous on 127.0.0.1), and exit with the worst rank's status.  The
+    parent never initialises the GPU (torch.cuda.device_count() does not on
+    this image) and prints nothing on stdout: rank 0 prints the line.  N above
+    the visible device count is an error.  If a rank fails, the others are
+    terminated (by PID) rather than left waiting in a collective."""
+    import signal
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        vis = torch.cuda.device_count()
+        if n > vis:
+            print(f"bench.py: --gpus {n} but {vis} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            if p.poll() is None:
+                continue
+            live.remove(p)
+            rc = max(rc, abs(p.returncode))
+            if p.returncode != 0:
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+    return rc
+
+
+def dry_run(args):
+    """The multi-rank reporting path without a GPU: gloo process group, W + K
+    steps of a small all-reduce (the step's gradient exchange stand-in),
+    barrier-bracketed timing, MAX over ranks, rank 0 prints the line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    g = torch.ones(1 << 16)
+
+    def step():
+        if world > 1:
+            dist.all_reduce(g)
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    B = args.batch or DEFAULTS[args.model][2]
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"metric": METRIC, "value": round(B * world * args.steps / elapsed, 3), "unit": "images/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "synthetic",
+                          "dry_run": True, "config": {"workload": "dry run (gloo, no GPU)", "global_batch": B * world,
+                                                      "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        sys.exit(dry_run(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -626,6 +721,7 @@ def main():
         init_rccl(device)
         from semanticsegmentation_tensorflow_amd.dp import DataParallel
         dp = DataParallel(bucket_mb=args.bucket_mb, shard_optimizer=args.dp_mode == "zero")
+        world = dist.get_world_size()     # what RCCL saw
 
     from semanticsegmentation_tensorflow_amd import ops
     for kv in args.option:
@@ -682,7 +778,7 @@ def main():
         "conv_gflop_per_step_measured": round(m["conv_gflop_per_step"], 2),
         "loss_after": round(m["loss"], 5),
         "miou_parity": m.get("miou"),
-        "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "GPU_MAX_HW_QUEUES_requested": _HWQ_USER},
+        "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")},
     }
     if "loss_scaling" in m:
         result["loss_scaling"] = m["loss_scaling"]

@@ -85,11 +85,24 @@ class Saver:
             return int(round(float(sess.variable_value(global_step.var_name).reshape(-1)[0])))
         return int(global_step)
 
-    def save(self, sess, save_path, global_step=None):
+    def save(self, sess, save_path, global_step=None, write=None):
+        """Write `save_path[-global_step]` and TF's `checkpoint` state file.
+
+        Under data parallelism EVERY rank calls save: gathering the ZeRO-1
+        Adam slots is a collective (`Session.sync_optimizer_slots`), so a
+        rank-0-only call would hang the job.  Only one rank writes and prunes
+        the files: `write=None` means rank 0 of the Session's data-parallel
+        group (every process when there is none); the other ranks return the
+        same path without touching the file system."""
         store = sess._ensure_store()
-        sess.sync_optimizer_slots()        # ZeRO-1 data parallelism: Adam slots gathered first
+        sess.sync_optimizer_slots()        # ZeRO-1 data parallelism: Adam slots gathered first (collective)
         gs = self._global_step_value(sess, global_step)
         path = save_path if gs is None else f"{save_path}-{gs}"
+        if write is None:
+            dp = getattr(sess, "dp", None)
+            write = dp is None or getattr(dp, "rank", 0) == 0
+        if not write:
+            return path
         out = {}
         for v in self._vars(sess):
             name = v.var_name

@@ -327,6 +327,7 @@ class Session:
             ops.axpy(g.view(-1), store.aux[acc.var_name].view(-1), 1.0)
             names.append(var.var_name)
         self._repack(None)
+        self.sync_optimizer_slots()      # after ZeRO-1 steps: whole m / v before a whole-variable Adam
         store.step += 1
         ops.adam_tf1_pack(store.params, store.grads, store.m, store.v, self._adam_plan(names), opt.lr,
                           store.step, opt.beta1, opt.beta2, opt.epsilon, grad_scale=1.0,
@@ -1266,6 +1267,10 @@ class Session:
                     and not p.train.accum)
             if dpa is not None:
                 dpa.mode = "zero" if zero else "allreduce"
+                if opt is not None and not zero and dpa.slots_stale:
+                    # a whole-variable Adam after ZeRO-1 steps: gather the m / v
+                    # slices of the other ranks first, or the replicas diverge
+                    self.sync_optimizer_slots()
             self._red = None
             if self.defer_wgrad_reduce and self.device.type == "cuda":
                 # (with the overlapped optimizer the reductions and each layer's
