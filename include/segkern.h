@@ -482,21 +482,6 @@ int seg_adam_tf1_pack(float* p, const float* g, float* m, float* v, const seg_ad
                       int nsegs, int total_tiles, float lr, float beta1, float beta2, float eps, int t,
                       float grad_scale, int dtype, void* stream);
 
-/* TF1 Adam (seg_adam_tf1_step's arithmetic) over n fp32 elements (n % 4 == 0)
- * that runs BESIDE MFMA-bound conv kernels on another stream instead of taking
- * CUs from them: no LDS, at most 32 VGPRs (one wave per SIMD fits next to the
- * 256x256-tile conv kernels), a persistent grid of `blocks` 256-thread blocks
- * (one per CU).  copy16 (may be NULL): the new values as an unpadded bf16 /
- * fp16 (dtype) copy, i.e. a weight's HWIO compute copy when its C and K need
- * no padding (FCN conv6). */
-int seg_adam_tf1_shadow(float* p, const float* g, float* m, float* v, void* copy16, long n, float lr, float beta1,
-                        float beta2, float eps, int t, float grad_scale, int dtype, int blocks, void* stream);
-
-/* The KRSC compute copy [K][R][S][tr_ap] of a filter from its HWIO copy
- * [R][S][rows_ap][rows_bp] (16-bit: a bit-pattern transpose; no LDS). */
-int seg_hwio_to_krsc(const void* rows, void* tr, int R, int S, int C, int K, int rows_ap, int rows_bp, int tr_ap,
-                     int dtype, void* stream);
-
 /* The packed compute copies of seg_adam_tf1_pack's segments rewritten from p
  * alone (no update): the repack after a data-parallel step whose Adam ran on
  * each rank's shard and whose parameters were then all-gathered (ZeRO-1).

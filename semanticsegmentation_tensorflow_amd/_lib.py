@@ -210,8 +210,6 @@ SIGNATURES = {
     "seg_concat_bwd": (_I, [_P, _I, _P, _I, _L, _I, _P]),
     "seg_adam_tf1_pack": (_I, [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _I, _F, _I, _P]),
     "seg_pack_segments": (_I, [_P, _P, _I, _I, _I, _P]),
-    "seg_adam_tf1_shadow": (_I, [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _I, _F, _I, _I, _P]),
-    "seg_hwio_to_krsc": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "seg_fill": (_I, [_P, _L, _F, _I, _P]),
     "seg_cast": (_I, [_P, _I, _P, _I, _L, _P]),
     "seg_axpy": (_I, [_P, _P, _F, _L, _P]),

@@ -554,10 +554,8 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res64", &seg::g_res64, 0, 1, 1, {}},
         {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
-        {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {2, 4, 8}},
-        {"nt2bn_bm", &seg::g_nt2bn_bm, 0, 0, 0, {128, 256}},
+        {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {4, 8}},
         {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
-        {"bn1x1s_st", &seg::g_bn1x1s_st, 0, 1, 1, {}},
         {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
         {"res16c_st", &seg::g_res16c_st, 0, 1, 1, {}},
         {"dropout_flat", &seg::g_dropout_flat, 0, 1, 1, {}},
@@ -983,22 +981,6 @@ __global__ __launch_bounds__(256) void rows_to_tr_k(const bf16* __restrict__ row
                 if (c0 + i < C) d16[i] = (unsigned short)(o[i >> 1] >> (16 * (i & 1)));
         }
     }
-}
-
-extern "C" int seg_hwio_to_krsc(const void* rows, void* tr, int R, int S, int C, int K, int rows_ap, int rows_bp,
-                                int tr_ap, int dtype, void* stream) {
-    if (!rows || !tr || R <= 0 || S <= 0 || C <= 0 || K <= 0 || rows_ap < C || rows_bp < K || tr_ap < C ||
-        (rows_bp & 7) || (tr_ap & 7) || (dtype != SEG_BF16 && dtype != SEG_F16))
-        return SEG_EINVAL;
-    if (((uintptr_t)rows | (uintptr_t)tr) & 15) return SEG_EALIGN;
-    const int RS = R * S;
-    const int ctiles = (C + 63) / 64, ntiles = (K + 63) / 64;
-    const int tiles = ctiles * ntiles;
-    // a bit-pattern transpose: the bf16 kernel moves fp16 copies unchanged
-    hipLaunchKernelGGL(rows_to_tr_k, dim3((tiles + 3) / 4, RS), dim3(256), 0, (hipStream_t)stream, (const bf16*)rows,
-                       (bf16*)tr, RS, C, K, rows_ap, rows_bp, tr_ap, ctiles, tiles);
-    SEG_CHECK_LAUNCH();
-    return SEG_OK;
 }
 
 extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x, const void* dy, float* dw,

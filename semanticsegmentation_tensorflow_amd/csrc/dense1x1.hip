@@ -253,12 +253,9 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
 constexpr int B1_TP = 128;       // pixels per tile (8 waves x 16)
 constexpr int B1_NST = 3;        // ring depth (steps)
 constexpr int B1_WST = 3 * 16 * 128;                  // per wave per step: dz, x, old dx rows
-// STG: the wave's 16 x 64 dx tile goes back through its (consumed) x rows in
-// LDS and leaves as 16-byte stores of whole 128-byte row chunks (2 per lane)
-// instead of 8-byte stores of 32-byte row pieces (4 per lane)
-template <typename T, bool STG>
+template <typename T>
 __global__ __launch_bounds__(512, 1) void bn1x1_dgrad_stream(NTParams p, int nch, int G, int ntiles) {
-    constexpr int B1_ST = STG ? 2 : 4;      // stores per wave per step
+    constexpr int B1_ST = 4;      // 8-byte dx stores per wave per step
     __shared__ __attribute__((aligned(16))) char ring[B1_NST * 8 * B1_WST];   // 144 KiB
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -346,7 +343,6 @@ __global__ __launch_bounds__(512, 1) void bn1x1_dgrad_stream(NTParams p, int nch
         const bool mok = m < p.M;
         const int mm = mok ? m : 0;
         const int img = mm / hw, pix = mm - img * hw;
-        uint2 ob[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
             const int col0 = c0 + ni * 16 + 4 * fg;
@@ -369,39 +365,11 @@ __global__ __launch_bounds__(512, 1) void bn1x1_dgrad_stream(NTParams p, int nch
                 if (res) x += to_f32(rh[j]);
                 o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
             }
-            ob[ni] = *reinterpret_cast<const uint2*>(o);
-            if constexpr (!STG) {
-                const bool ok = mok && col0 < p.N;
-                uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img +
-                                                           (long)pix * p.ldy + col0)
-                                : s1_trash + (tid & 4095);
-                *dst = ob[ni];
-            }
-        }
-        if constexpr (STG) {
-            // the x rows of this stage are consumed: stage the tile there
-            // (same swizzled offsets), read back row chunks, store 16 B each
-            char* Xw = const_cast<char*>(Ws) + 2048;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-                *reinterpret_cast<uint2*>(Xw + fr * 128 + 16 * ((2 * ni + (fg >> 1)) ^ sw) + 8 * (fg & 1)) = ob[ni];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const int row = lane >> 2;
-            const int mr = (t0 + s) * B1_TP + w * 16 + row;
-            const bool rok = mr < p.M;
-            const int mrr = rok ? mr : 0;
-            const int rimg = mrr / hw, rpix = mrr - rimg * hw;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = (lane & 3) * 2 + h;
-                const uint4 v = *reinterpret_cast<const uint4*>(Xw + row * 128 + 16 * (c ^ ((row >> 1) & 7)));
-                const bool ok = rok && c0 + c * 8 < p.N;
-                uint4* dst = ok ? reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + rimg * p.y_img +
-                                                           (long)rpix * p.ldy + c0 + c * 8)
-                                : reinterpret_cast<uint4*>(s1_trash) + (tid & 2047);
-                *dst = v;
-            }
+            const bool ok = mok && col0 < p.N;
+            uint2* dst = ok ? reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img +
+                                                       (long)pix * p.ldy + col0)
+                            : s1_trash + (tid & 4095);
+            *dst = *reinterpret_cast<const uint2*>(o);
         }
     }
     wait_vmcnt<0>();
@@ -483,22 +451,15 @@ int bn1x1s_rows(const NTParams& p, int cus) {
     return std::min(G, std::max(8, (ntiles + 7) & ~7));
 }
 
-int g_bn1x1s_st = 0;   // 1: staged 16-byte dx stores (faster alone, slower in the C3 step: 211 vs 212 img/s)
 
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
     if (!bn1x1s_args_ok(p)) return SEG_EINVAL;
-    const bool st = g_bn1x1s_st && p.ldy % 8 == 0 && p.y_img % 8 == 0 && ((uintptr_t)p.y % 16) == 0;
     const int nch = (p.N + 63) / 64;
     const int ntiles = (p.M + B1_TP - 1) / B1_TP;
     const int G = bn1x1s_rows(p, cus);
     const dim3 grid(nch * G);
-    if (dtype == SEG_F16) {
-        if (st) hipLaunchKernelGGL((bn1x1_dgrad_stream<f16, true>), grid, dim3(512), 0, s, p, nch, G, ntiles);
-        else hipLaunchKernelGGL((bn1x1_dgrad_stream<f16, false>), grid, dim3(512), 0, s, p, nch, G, ntiles);
-    } else {
-        if (st) hipLaunchKernelGGL((bn1x1_dgrad_stream<bf16, true>), grid, dim3(512), 0, s, p, nch, G, ntiles);
-        else hipLaunchKernelGGL((bn1x1_dgrad_stream<bf16, false>), grid, dim3(512), 0, s, p, nch, G, ntiles);
-    }
+    if (dtype == SEG_F16) hipLaunchKernelGGL((bn1x1_dgrad_stream<f16>), grid, dim3(512), 0, s, p, nch, G, ntiles);
+    else hipLaunchKernelGGL((bn1x1_dgrad_stream<bf16>), grid, dim3(512), 0, s, p, nch, G, ntiles);
     return SEG_OK;
 }
 

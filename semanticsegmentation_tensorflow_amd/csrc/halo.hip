@@ -43,7 +43,7 @@ int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 // and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
 int g_res64_pp = 1;
 int g_res16_dma = 1;
-int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8, 4 or 2)   // 16-wide conv_res64: halo by LDS DMA (two blocks / CU) or VGPR staging
+int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8 or 4)
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
@@ -1985,7 +1985,7 @@ void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype) {
 }
 
 // grid of the BN-backward form (= its bn_part rows): tiles of g_res16c_bh rows,
-// two rounds of the resident blocks (8 rows: one per CU, 4 or 2 rows: three)
+// two rounds of the resident blocks (8 rows: one per CU, 4 rows: three)
 int res16c_grid(const NTParams& p, int cus) {
     const int bh = g_res16c_bh;
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + bh - 1) / bh;
@@ -2010,7 +2010,6 @@ void launch_res16c_bn(NTParams& p, int cus, hipStream_t s, int dtype) {
     const bool h = dtype == SEG_F16;
     switch (g_res16c_bh) {
         case 8: h ? launch_res16c_bn_t<f16, 8>(p, grid, s) : launch_res16c_bn_t<bf16, 8>(p, grid, s); break;
-        case 2: h ? launch_res16c_bn_t<f16, 2>(p, grid, s) : launch_res16c_bn_t<bf16, 2>(p, grid, s); break;
         default: h ? launch_res16c_bn_t<f16, 4>(p, grid, s) : launch_res16c_bn_t<bf16, 4>(p, grid, s); break;
     }
 }

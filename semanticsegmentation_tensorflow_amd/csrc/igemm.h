@@ -165,11 +165,9 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
 void tn_info(int M, int N, int P, int dtype, int* bm, int* bn, int* splits);
 void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_t s);
 void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
-extern int g_nt2bn_bm;
 long nt2_bn_rows(int M);
 // dense1x1.hip: the 1x1 BN-backward input gradient streamed (K = 64)
 extern int g_bn1x1s;
-extern int g_bn1x1s_st;
 extern int g_s1x1_st;
 extern int g_res16c_st;
 extern int g_dropout_flat;

@@ -706,22 +706,11 @@ bool nt2_short(const NTParams& p, int dtype) {
     return dtype == SEG_BF16 && !p.partial && p.K <= 64 * g_nt2_short && g_nt2_ablate == 0;
 }
 
-// input gradient + folded BN backward (EpiParams.bn_*): short-K 2-stage form
-// BN-backward 1x1 input gradient: 256-row tiles of 8 waves (two blocks per
-// CU) or 128-row tiles of 4 waves (three per CU); one bn_part row per M tile
-int g_nt2bn_bm = 256;
-
-long nt2_bn_rows(int M) { return (M + g_nt2bn_bm - 1) / g_nt2bn_bm; }
+// input gradient + folded BN backward (EpiParams.bn_*): short-K 2-stage form,
+// 256-row tiles of 8 waves (two blocks per CU); one bn_part row per M tile
+long nt2_bn_rows(int M) { return (M + 255) / 256; }
 
 void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s) {
-    if (g_nt2bn_bm == 128) {
-        const int tiles = ((p.M + 127) / 128) * ((p.N + 63) / 64);
-        if (dtype == SEG_F16)
-            hipLaunchKernelGGL((igemm_nt2<f16, 128, 64, 2, 2, 0, 2, false, true>), dim3(tiles), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((igemm_nt2<bf16, 128, 64, 2, 2, 0, 2, false, true>), dim3(tiles), dim3(256), 0, s, p);
-        return;
-    }
     const int tiles = ((p.M + 255) / 256) * ((p.N + 63) / 64);
     if (dtype == SEG_F16)
         hipLaunchKernelGGL((igemm_nt2<f16, 256, 64, 4, 2, 0, 2, false, true>), dim3(tiles), dim3(512), 0, s, p);

@@ -164,90 +164,8 @@ __global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const 
     }
 }
 
-// TF1 Adam over a flat fp32 range (+ an optional unpadded 16-bit copy of the
-// new values), built to run BESIDE the MFMA-bound conv kernels instead of
-// taking CUs from them: no LDS and at most 32 VGPRs, so one wave per SIMD fits
-// next to conv_halo2 (228 VGPRs x 2 waves per SIMD, 160 KiB LDS) or
-// wgrad_halo (240 x 2, 128 KiB); a persistent grid of one 256-thread block per
-// CU walks the range.  Elementwise arithmetic is adam_pack_tile's.
-template <typename T>
-__global__ __launch_bounds__(256) void adam_shadow_k(float* P, const float* G, float* Mm, float* Vv, T* copy,
-                                                     unsigned n2, float lr_t, float b1, float b2, float eps,
-                                                     float gs) {
-    // buffer resources: one 32-bit lane offset addresses all five arrays (no
-    // 64-bit address pairs), 8-byte pairs per lane, and the next pair's four
-    // loads in flight while this one updates (two register sets) -- the
-    // register budget is the point of this kernel.  Offsets past the range
-    // read zeros / drop stores (buffer bounds), so the pipeline needs no
-    // branch around a memory instruction.
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const int bytes = (int)(n2 * 8u);
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, bytes,
-                                                                        0x00020000);
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(Mm, (short)0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(Vv, (short)0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(copy, (short)0, copy ? bytes / 2 : 0,
-                                                                        0x00020000);
-    const unsigned stride = gridDim.x * 256u;
-    unsigned i = blockIdx.x * 256u + threadIdx.x;
-    const unsigned first = i;
-    if (first >= n2) return;
-    unsigned o = i * 8u;
-    f32x2 pp = __builtin_amdgcn_raw_buffer_load_b64(rp, o, 0, 0);
-    f32x2 gg = __builtin_amdgcn_raw_buffer_load_b64(rg, o, 0, 0);
-    f32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(rm, o, 0, 0);
-    f32x2 vv = __builtin_amdgcn_raw_buffer_load_b64(rv, o, 0, 0);
-    for (; i < n2; i += stride) {
-        const unsigned on = (i + stride) * 8u;      // out of range past the end: zeros
-        const f32x2 pn = __builtin_amdgcn_raw_buffer_load_b64(rp, on, 0, 0);
-        const f32x2 gn = __builtin_amdgcn_raw_buffer_load_b64(rg, on, 0, 0);
-        const f32x2 mn = __builtin_amdgcn_raw_buffer_load_b64(rm, on, 0, 0);
-        const f32x2 vn = __builtin_amdgcn_raw_buffer_load_b64(rv, on, 0, 0);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const float gc = gg[c] * gs;
-            mm[c] = b1 * mm[c] + (1.f - b1) * gc;
-            vv[c] = b2 * vv[c] + (1.f - b2) * gc * gc;
-            pp[c] = pp[c] - lr_t * mm[c] / (sqrtf(vv[c]) + eps);
-        }
-        o = i * 8u;
-        __builtin_amdgcn_raw_buffer_store_b64(pp, rp, o, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(mm, rm, o, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(vv, rv, o, 0, 0);
-        if (copy) {
-            const T h[2] = {(T)pp[0], (T)pp[1]};
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const unsigned*>(h), rc, i * 4u, 0, 0);
-        }
-        pp = pn; gg = gn; mm = mn; vv = vn;
-    }
-}
-
 }  // namespace
 
-extern "C" int seg_adam_tf1_shadow(float* p, const float* g, float* m, float* v, void* copy16, long n, float lr,
-                                   float b1, float b2, float eps, int t, float gs, int dtype, int blocks,
-                                   void* stream) {
-    if (!p || !g || !m || !v || t < 1 || n <= 0 || (n & 3) || blocks < 1) return SEG_EINVAL;
-    if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)copy16) & 15) return SEG_EALIGN;
-    const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
-    if (dtype != SEG_F16 && dtype != SEG_BF16) return SEG_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    // buffer resources hold < 2^31 bytes: 2^28-element chunks (1 GiB of fp32)
-    constexpr long CH = 1L << 28;
-    for (long o = 0; o < n; o += CH) {
-        const unsigned n4 = (unsigned)(std::min(CH, n - o) / 2);   // element pairs
-        void* c16 = copy16 ? (void*)((char*)copy16 + 2 * o) : nullptr;
-        if (dtype == SEG_F16)
-            hipLaunchKernelGGL(adam_shadow_k<f16>, dim3(blocks), dim3(256), 0, st, p + o, g + o, m + o, v + o,
-                               (f16*)c16, n4, (float)lr_t, b1, b2, eps, gs);
-        else
-            hipLaunchKernelGGL(adam_shadow_k<bf16>, dim3(blocks), dim3(256), 0, st, p + o, g + o, m + o, v + o,
-                               (bf16*)c16, n4, (float)lr_t, b1, b2, eps, gs);
-        SEG_CHECK_LAUNCH();
-    }
-    return SEG_OK;
-}
 
 int g_adam_blocks = 0;    // seg_set_option("adam_blocks"): grid cap of seg_adam_tf1_pack (0 = one block per tile)
 

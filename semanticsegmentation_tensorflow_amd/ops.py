@@ -755,25 +755,6 @@ def adam_tf1_pack(p, g, m, v, plan, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, gra
                                        int(t), float(grad_scale), int(dtype), stream_ptr(stream)), "adam_pack")
 
 
-def adam_tf1_shadow(p, g, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0, copy16=None,
-                    dtype=BF16, blocks=None, stream=None):
-    """TF1 Adam on flat fp32 p / g / m / v built to co-reside with MFMA-bound
-    conv kernels (no LDS, <= 32 VGPRs, one block per CU); copy16: an unpadded
-    16-bit copy of the new values (or None)."""
-    if blocks is None:
-        blocks = torch.cuda.get_device_properties(p.device).multi_processor_count
-    check(_lib.lib().seg_adam_tf1_shadow(ptr(p), ptr(g), ptr(m), ptr(v), None if copy16 is None else ptr(copy16),
-                                         p.numel(), float(lr), float(beta1), float(beta2), float(eps), int(t),
-                                         float(grad_scale), int(dtype), int(blocks), stream_ptr(stream)),
-          "adam_shadow")
-
-
-def hwio_to_krsc(rows, tr, R, S, C, K, stream=None):
-    """KRSC compute copy (rows = (tensor, a_pad, b_pad) HWIO, tr = (tensor, a_pad, _))."""
-    check(_lib.lib().seg_hwio_to_krsc(ptr(rows[0]), ptr(tr[0]), R, S, C, K, rows[1], rows[2], tr[1],
-                                      seg_dtype(rows[0]), stream_ptr(stream)), "hwio_to_krsc")
-
-
 def pack_segments(p, plan, dtype=BF16, stream=None):
     """Rewrite every planned variable's packed compute copies from p (no update)."""
     check(_lib.lib().seg_pack_segments(ptr(p), ptr(plan.table), plan.nsegs, plan.total_tiles, int(dtype),

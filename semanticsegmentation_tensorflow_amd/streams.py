@@ -1,0 +1,114 @@
+"""Stream scheduling of a Session step (mixin): the side stream that runs the
+filter gradients and their split-K reductions beside the input-gradient chain,
+the deferred fused filter-gradient + Adam launches, per-launch HIP-event
+timing, and the overlapped per-layer optimizer.  Split out of session.py;
+`Session` inherits these methods unchanged."""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from . import ops
+
+
+class _AdamOverlap:
+    """Per-step driver of the overlapped optimizer: each variable group's fused
+    Adam + pack launch runs on a side stream after an event on the compute
+    stream (or, with data parallelism, after the bucket's all-reduce), so the
+    HBM-bound update of layer L hides under the MFMA-bound backward of layers
+    < L.  Nothing later in the step reads L's parameters or packed copies
+    (its input gradient is enqueued before its filter gradient).  finish()
+    updates the remaining variables and makes the compute stream wait."""
+
+    def __init__(self, sess, opt, gs, var_set):
+        self.s = sess
+        self.opt = opt
+        self.gs = gs
+        self.var_set = var_set
+        if sess._side is None:
+            sess._side = torch.cuda.Stream(device=sess.device)
+        self.side = sess._side
+        self.main = torch.cuda.current_stream(sess.device)
+        self.done = set()
+
+    def _adam(self, names):
+        st = self.s.store
+        o = self.opt
+        names = [nm for nm in names if nm in self.var_set]
+        if not names:
+            return
+        ops.adam_tf1_pack(st.params, st.grads, st.m, st.v, self.s._adam_plan(names), o.lr, st.step, o.beta1,
+                          o.beta2, o.epsilon, grad_scale=self.gs, dtype=self.s._pack_dtype(), stream=self.side)
+        self.done.update(names)
+
+    def launch(self, names):
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        self._adam(names)
+
+    def after_work(self, works, names):
+        if works:
+            with torch.cuda.stream(self.side):
+                for w in works:
+                    w.wait()
+        else:
+            ev = torch.cuda.Event()
+            ev.record(self.main)
+            self.side.wait_event(ev)
+        self._adam(names)
+
+    def finish(self):
+        rest = [v.var_name for v in self.s.store.order if v.var_name in self.var_set and v.var_name not in self.done]
+        if rest:
+            self.launch(rest)
+        self.main.wait_stream(self.side)
+
+
+class StreamMixin:
+    @contextlib.contextmanager
+    def _beside(self, side):
+        """Run the enclosed launches on `side` (the filter-gradient stream),
+        ordered after everything enqueued so far on the compute stream; a no-op
+        context when side is None (no side stream: CPU plans, disabled)."""
+        if side is None:
+            yield None
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._red[1])
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            yield side
+
+    def _wgrad_side(self, p, n, level=1):
+        """The side stream for node n's filter gradient, or None."""
+        return self._red[0] if (self._red is not None and self.side_wgrad >= level) else None
+
+    def _tick_fused(self, flush=False):
+        keep = []
+        for item in self._pending_fused:
+            item[0] -= 1
+            if flush or item[0] <= 0:
+                item[1]()
+            else:
+                keep.append(item)
+        self._pending_fused = keep
+
+    def _node_ws(self, p, n):
+        """The conv's own filter-gradient workspace (p.wg_ws) as an ops.Workspace,
+        for launches on the side stream (the shared one belongs to the compute stream)."""
+        w = ops.Workspace(self.device)
+        w.buf = p.wg_ws[id(n)]
+        return w
+
+    def _timed(self, desc, op, fn, *args):
+        if self.timer is None:
+            return fn(*args)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn(*args)
+        e.record()
+        self.timer.append((desc, op, s, e))
+        return r

@@ -85,6 +85,12 @@ def test_product_library_has_no_ablation_knobs():
     assert lib.seg_set_option(b"tn_reduce_sl", 3) == EINVAL
     assert lib.seg_set_option(b"tn_reduce_sl", 16) == 0
     assert lib.seg_set_option(b"wpad", 12) == EINVAL
+    # variants measured slower and deleted: no knob selects them
+    for knob in (b"bn1x1s_st", b"nt2bn_bm"):
+        assert lib.seg_set_option(knob, 1) == EINVAL, knob
+    assert lib.seg_set_option(b"nt2bn_bm", 128) == EINVAL
+    assert lib.seg_set_option(b"res16c_bh", 2) == EINVAL
+    assert lib.seg_set_option(b"res16c_bh", 4) == 0
 
 
 def test_bn_part_launch_refuses_a_foreign_row_count():

@@ -6,7 +6,7 @@ sharded Adam + all-gather, and the all-reduce path, issued from the Session's
 side stream beside the side-stream filter gradients and their deferred split-K
 reductions -- a stream-ordering mistake there would corrupt C4's gradients.
 Every Session schedule attribute value (side_wgrad 0 / 1 / 2, main_wgrad 0 /
-1 / 2 / 3, fused_delay 0 / 6, fuse_pool, fuse_grad_sum, shadow_update) runs, single-process
+1 / 2 / 3, fused_delay 0 / 6, fuse_pool, fuse_grad_sum) runs, single-process
 and data-parallel, and each step's gradients, parameters and Adam m / v are
 checked against the default single-process step (which fuses the conv6 /
 conv7 update into their filter-gradient epilogues):

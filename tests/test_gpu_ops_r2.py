@@ -124,19 +124,13 @@ BNB_CASES = [(2, 9, 11, 48, 64, 1), (1, 12, 10, 136, 64, 1), (1, 33, 41, 200, 13
              (1, 17, 19, 24, 8, 1), (2, 40, 52, 112, 64, 1)]
 
 
-@pytest.fixture(params=[(1, 1, 256), (1, 0, 256), (0, 1, 256), (0, 1, 128)],
-                ids=["stream", "stream8", "bm256", "bm128"])
+@pytest.fixture(params=[1, 0], ids=["stream", "bm256"])
 def nt2bn_bm(request):
-    """Every 1x1 form: bn1x1_stream (K = 64; option bn1x1s) with staged
-    16-byte or direct 8-byte dx stores (bn1x1s_st), and igemm_nt2_bn at both
-    M-tile heights (option nt2bn_bm)."""
-    ops.set_option("bn1x1s", request.param[0])
-    ops.set_option("bn1x1s_st", request.param[1])
-    ops.set_option("nt2bn_bm", request.param[2])
+    """Both 1x1 forms: bn1x1_stream (K = 64; option bn1x1s) and igemm_nt2_bn
+    (256-row tiles)."""
+    ops.set_option("bn1x1s", request.param)
     yield request.param
     ops.set_option("bn1x1s", 1)
-    ops.set_option("bn1x1s_st", 0)
-    ops.set_option("nt2bn_bm", 256)
 
 
 @pytest.mark.parametrize("accumulate", [False, True], ids=["write", "accumulate"])
@@ -176,11 +170,11 @@ def test_conv2d_bwd_data_through_bn_relu(dev, case, dtype, accumulate, nt2bn_bm)
 # the 3x3 form (FC-DenseNet growth conv, 64 -> 16): the input gradient runs on
 # conv_res16c and continues through the BN(+ReLU) that produced the conv's
 # input and, with keep_prob < 1, the dropout of the conv before that BN; every
-# tile height of the kernel (option res16c_bh: 8, 4 = the default, 2)
+# tile height of the kernel (option res16c_bh: 8, 4 = the default)
 BNB3_CASES = [(2, 21, 67, 64, 16), (1, 30, 70, 64, 16), (2, 9, 11, 32, 16)]
 
 
-@pytest.fixture(params=[(4, 0), (8, 0), (2, 0), (4, 1), (8, 1)], ids=["bh4", "bh8", "bh2", "bh4st", "bh8st"])
+@pytest.fixture(params=[(4, 0), (8, 0), (4, 1), (8, 1)], ids=["bh4", "bh8", "bh4st", "bh8st"])
 def res16c_bh(request):
     """Tile heights (option res16c_bh) and the staged 16-byte dx stores
     (option res16c_st)."""

@@ -4,7 +4,7 @@ each one's algorithmic HBM bytes / time (Network/model/FCDenseNet.py:23-34:
 BN -> ReLU -> 1x1 conv -> dropout -> BN -> ReLU -> 3x3 conv -> dropout).
 
     python tools/dense_kbench.py bn1x1:384:1248:128 bn3x3:384:1248 fwdbn2:384:1248:128 \
-        grow:384:1248 smallk:384:1248:256 [--opts 'nt2bn_bm=256'] [--opts 'nt2bn_bm=128']
+        grow:384:1248 smallk:384:1248:256
 
 Specs (H, W at batch --batch; C = the concat-stack channels):
   bn1x1:H:W:C   input gradient of the bottleneck 1x1 conv (64 -> C) through
