@@ -524,6 +524,29 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
         sess.timer = None
         sess.side_wgrad = side_mode
     dname, (dn, dflops, dms, dbytes) = max(per.items(), key=lambda kv: kv[1][2])
+    # the dominant family re-timed in-step with events around ITS launches
+    # only (every other launch un-instrumented, as in the timed steps): the
+    # figure the line reports, comparable with the kernel durations of the
+    # timed steps in a rocprofv3 kernel trace (tools/timed_stats.py)
+    all_ev_ms = dms / dn
+    reps = max(1, min(steps, 5))
+    sess.timer = []
+    seen = {}
+
+    def is_dominant(d, o):
+        k = (id(d), o)
+        if k not in seen:
+            seen[k] = ops.conv_kernel_info(d, o)[0] == dname
+        return seen[k]
+    sess.timer_match = is_dominant
+    torch.cuda._sleep(int(4e8))
+    for _ in range(reps):
+        sess.run(train_step, feed_dict=feed)
+    torch.cuda.synchronize()
+    ev = [s_ev.elapsed_time(e_ev) for _, _, s_ev, e_ev in sess.timer]
+    sess.timer, sess.timer_match = None, None
+    if len(ev) == dn * reps:
+        dms = sum(ev) / reps
     achieved = (dflops / dn) / (dms / dn * 1e-3)
     peak = PEAK[dtype]
     # roofline bound of the dominant kernel group from its arithmetic intensity
@@ -539,6 +562,10 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
                 "peak": round(peak / 1e12, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": None, "launches_per_step": dn, "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
                 "algorithmic_bytes_per_launch": round(dbytes / dn), "avg_launch_ms": round(dms / dn, 4)}
+    roof["all_events_avg_launch_ms"] = round(all_ev_ms, 4)
+    roof["timing"] = (f"HIP events on the launch stream around the {dn} launches per step of this family only, "
+                      f"{reps} train steps after the timed ones; all_events_avg_launch_ms: the same with every "
+                      f"conv launch of the step bracketed")
     if dname in alone and alone[dname][1] > 0:
         an, ams = alone[dname]
         if hbm_bound:

@@ -530,6 +530,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"nt_halo", &seg::g_nt_halo, 0, 1, 1, {}},
         {"halo_wide", &seg::g_halo_wide, 0, 1, 1, {}},
         {"halo_min_splits", &seg::g_halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
+        {"halo2_1p", &seg::g_halo2_1p, 0, 1, 1, {}},
         {"adam_tr_fused", &g_adam_tr_fused, 0, 1, 1, {}},
         {"nt2_short", &seg::g_nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
         {"tn_fill", &seg::g_tn_fill, 1, 64, 1, {}},                   // filter-gradient split-K target, blocks/CU
@@ -545,6 +546,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"tn3", &seg::g_tn3, 0, 1, 1, {}},
         {"nt3", &seg::g_nt3, 0, 1, 1, {}},
         {"wgrad_fill", &seg::g_wgrad_fill, 1, 800, 1, {}},            // filter-gradient split-K, % of the CUs
+        {"wgrad_fill16", &seg::g_wgrad_fill16, 1, 800, 1, {}},        // ... for <= 32 output channels
         {"wgrad_nt32", &seg::g_wgrad_nt32, 0, 1, 1, {}},
         {"wgrad_nbias", &seg::g_wgrad_nbias, 1, 4, 1, {}},
         {"wgrad_nt", &seg::g_wgrad_nt, 0, 0, 0, {64, 128}},

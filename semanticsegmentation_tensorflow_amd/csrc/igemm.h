@@ -282,6 +282,7 @@ extern int g_res16;
 extern int g_res64_pp;
 extern int g_res16_dma;
 extern int g_res16c_bh;
+extern int g_halo2_1p;
 extern int g_smallk_abl;
 // the launch plan for p writes EpiParams.y2 (seg_conv2d_fwd_bn2)
 bool nt_bn2_ok(const NTParams& p, int dtype);
@@ -317,6 +318,7 @@ extern int g_wgrad_abl;
 extern int g_wgrad_nbias;
 extern int g_wgrad_nt32;
 extern int g_wgrad_fill;
+extern int g_wgrad_fill16;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);

@@ -177,6 +177,7 @@ class Session(PlanMixin, StreamMixin):
         self._ready_filter = None
         self.capture = None    # tests: list -> per-conv buffer records of the last backward
         self.timer = None      # list -> (desc, op, start_event, end_event) per conv launch
+        self.timer_match = None   # (desc, op) -> bool: which launches self.timer records (None: all)
 
     # ------------------------------------------------------------------ vars
     def _ensure_store(self):

@@ -103,7 +103,10 @@ class StreamMixin:
         return w
 
     def _timed(self, desc, op, fn, *args):
-        if self.timer is None:
+        """fn(*args), bracketed by HIP events on the launch stream when
+        self.timer is a list (and self.timer_match, if set, accepts the
+        launch: bench.py times only the dominant kernel's launches)."""
+        if self.timer is None or (self.timer_match is not None and not self.timer_match(desc, op)):
             return fn(*args)
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
