@@ -532,6 +532,22 @@ int seg_cast(const void* x, int xdtype, void* y, int ydtype, long n, void* strea
  * code for tf.train.Saver's tensor-bundle checkpoints (per-tensor checksums
  * in the .index file, SSTable block trailers). */
 uint32_t seg_crc32c(const void* data, size_t n, uint32_t crc);
+/* Timing events (Session.timer / bench.py per-launch roofline timing): HIP
+ * events created with hipEventDisableSystemFence, so recording one does not
+ * write back and invalidate the caches.  A plain timing event adds that
+ * system-scope release to the interval it closes: +23 us (+15 %) per
+ * conv_halo2 launch in the C2 step against a kernel trace of the same steps.
+ * elapsed waits for `end`.  Not a TF interface: measurement support. */
+int seg_timing_event_create(void** ev);
+int seg_timing_event_record(void* ev, void* stream);
+int seg_timing_event_elapsed_ms(float* ms, void* start, void* end);
+int seg_timing_event_destroy(void* ev);
+/* A HIP stream restricted to the CUs set in mask (nwords 32-bit words, bit i
+ * = CU i): the Session runs the HBM-bound fused conv6 / conv7 filter-gradient
+ * + Adam launches there (FCN.py:78, :338-340) so they leave CUs to the
+ * input-gradient chain.  Not a TF interface: scheduling support. */
+int seg_stream_create_cu_mask(void** stream, const unsigned* mask, int nwords);
+int seg_stream_destroy(void* stream);
 const char* seg_status_string(int status);
 int seg_version(void);
 

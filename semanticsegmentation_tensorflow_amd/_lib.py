@@ -23,7 +23,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
 # SEG_DIAG_LIB=1 loads it instead of the product library
 DIAG_LIB_PATH = os.path.join(PKG_DIR, "build_diag", "libsegkern_diag.so")
 SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
-HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]   # host-only C++ (g++), linked into the same library
+HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]
+HIP_HOST_SOURCES = ["timing.cpp"]   # host code against the HIP runtime API (hipcc, no kernels)
 HOST_LIBS = ["-lz"]
 # per-source extra compiler flags
 EXTRA_FLAGS = {}
@@ -68,7 +69,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
         return o
 
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        objs = list(ex.map(compile_one, SOURCES + HOST_SOURCES))
+        objs = list(ex.map(compile_one, SOURCES + HIP_HOST_SOURCES + HOST_SOURCES))
     if force or not os.path.exists(lib_path) or any(
             os.path.getmtime(o) > os.path.getmtime(lib_path) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, *HOST_LIBS]
@@ -167,6 +168,12 @@ SIGNATURES = {
     "seg_softmax": (_I, [_P, _I, _I, _L, _P, _I, _I, _P]),
     "seg_conv2d_bwd_filter_adam": (_I, [_DP, _P, _P, _P, _P, ctypes.POINTER(SegAdamFused), _P, _Z, _P]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),
+    "seg_timing_event_create": (_I, [ctypes.POINTER(ctypes.c_void_p)]),
+    "seg_timing_event_record": (_I, [_P, _P]),
+    "seg_timing_event_elapsed_ms": (_I, [ctypes.POINTER(ctypes.c_float), _P, _P]),
+    "seg_timing_event_destroy": (_I, [_P]),
+    "seg_stream_create_cu_mask": (_I, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint), _I]),
+    "seg_stream_destroy": (_I, [_P]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
                                   ctypes.POINTER(ctypes.c_double)]),
     "seg_pack_filter": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

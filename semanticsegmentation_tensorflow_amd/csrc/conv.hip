@@ -530,7 +530,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"nt_halo", &seg::g_nt_halo, 0, 1, 1, {}},
         {"halo_wide", &seg::g_halo_wide, 0, 1, 1, {}},
         {"halo_min_splits", &seg::g_halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
-        {"halo2_1p", &seg::g_halo2_1p, 0, 1, 1, {}},
         {"adam_tr_fused", &g_adam_tr_fused, 0, 1, 1, {}},
         {"nt2_short", &seg::g_nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
         {"tn_fill", &seg::g_tn_fill, 1, 64, 1, {}},                   // filter-gradient split-K target, blocks/CU

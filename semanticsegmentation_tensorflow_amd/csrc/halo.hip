@@ -47,7 +47,6 @@ int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8 or 4)
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
 int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
 int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
-int g_halo2_1p = 0;          // 256x256 tiles on conv_halo2s (one MFMA phase per iteration and wave group)
 
 struct HaloGeom {
     int taps_h, tiles_x, tiles_y, nimg;
@@ -936,278 +935,6 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
 }
 
 
-
-// ---------------------------------------------------------------------------
-// conv_halo2 with ONE MFMA phase per (chunk, tap) iteration and wave group
-// (option halo2_1p): each group reads all of its A (both M halves) and B
-// fragments of the iteration in one LDS phase, then issues its 64 MFMAs in
-// one 1024-cycle segment, while the other group (one barrier behind) reads.
-// Two barriers per iteration instead of four, so the per-barrier skew is paid
-// half as often per MFMA; +32 fragment VGPRs (A for both halves at once),
-// paid for by 32-bit DMA offsets.  The filter slice ring is filled half by
-// each group in its read phase: group 0 issues its half of slice it+1 (the
-// buffer group 1 finished reading one interval ago), group 1 its half of
-// slice it+2 after its own reads of slice it have completed; every wave
-// drains its DMAs (vmcnt(0)) at the end of its MFMA phase, one interval
-// before anyone reads them.  Accumulation order per accumulator is
-// conv_halo2's, so the results are bit-identical to it.
-template <int BW, typename T = bf16>
-__global__ __launch_bounds__(512) void conv_halo2s(NTParams p, HaloGeom g) {
-    constexpr int NW = 8, BM = 256, BN = 256, BH = BM / BW, HI = 6;
-    constexpr int WTN = BN / 4, NFH = WTN / 32;
-    constexpr int HBUF = HI * NW * 1024;
-    constexpr int BBUF = BN * 128;
-    constexpr int SMEM = 2 * HBUF + 2 * BBUF;
-    constexpr int B_INS = BN / 8 / NW;   // 4 slice pieces per wave (its group's half)
-    static_assert(BW % 16 == 0 && BM % BW == 0, "fragments are 16 px of one tile row");
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int wg = xcd_remap2(blockIdx.x, gridDim.x);
-    const int tsp = wg / tiles_n, tn = wg - (wg / tiles_n) * tiles_n;
-    const int tpi = g.tiles_x * g.tiles_y;
-    const int img = tsp / tpi;
-    if (img >= g.nimg) return;
-    const int trem = tsp - img * tpi;
-    const int ty = trem / g.tiles_x, tx = trem - (trem / g.tiles_x) * g.tiles_x;
-    const int oy0 = ty * BH, ox0 = tx * BW, n0 = tn * BN;
-    int kc_begin = 0, kc_end = g.nchunks;
-    if (p.partial) {
-        kc_begin = blockIdx.z * g.kc_per_split;
-        kc_end = min(g.nchunks, kc_begin + g.kc_per_split);
-    }
-    const int ntaps = g.taps_h * p.taps_w;
-    const int iters = (kc_end - kc_begin) * ntaps;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w >> 2, wn = w & 3;
-    const int lr = lane >> 3;
-    const int c = (lane & 7) ^ (lr & 6);
-
-    const T* __restrict__ X = reinterpret_cast<const T*>(p.x) + (long)img * p.x_img;
-    const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w);
-    const void* zero = (const void*)halo_zero_page;
-
-    // 32-bit element offsets (the planner admits images of < 2^31 elements)
-    int h_off[HI];
-#pragma unroll
-    for (int h = 0; h < HI; ++h) {
-        const int hr = (h * NW + w) * 8 + lr;
-        const int hy = hr / g.hwd, hx = hr - (hr / g.hwd) * g.hwd;
-        const int ih = oy0 + p.ioh + g.hy0 + hy, iw = ox0 + p.iow + g.hx0 + hx;
-        const bool ok = hr < g.hrows && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-        h_off[h] = ok ? (ih * p.IW + iw) * p.ldx + c * 8 : -1;
-    }
-    const int h_n = g.hrows > w * 8 ? min(HI, (g.hrows - w * 8 + NW * 8 - 1) / (NW * 8)) : 0;
-    int b_off[B_INS];
-#pragma unroll
-    for (int i = 0; i < B_INS; ++i) {
-        const int n = n0 + (i * NW + w) * 8 + lr;
-        b_off[i] = n < p.N ? n * p.w_col + c * 8 : -1;
-    }
-    const unsigned lds0 = (unsigned)(uintptr_t)(SEG_LDS char*)smem;
-    const unsigned ldsB = lds0 + 2 * HBUF;
-
-    auto load_halo = [&](int h, int kc, int buf) {
-        const void* src = h_off[h] >= 0 ? (const void*)(X + h_off[h] + kc * 64) : zero;
-        glds16(src, __builtin_amdgcn_readfirstlane(lds0 + buf * HBUF + (h * NW + w) * 1024));
-    };
-    // this wave's pieces of filter slice `it` (iteration order: chunk, tap row, tap col)
-    auto issue_b = [&](int it, int buf) {
-        const int kcs = kc_begin + it / ntaps, tp = it - (it / ntaps) * ntaps;
-        const int tj = tp / p.taps_w, ti = tp - (tp / p.taps_w) * p.taps_w;
-        const long wtap = (long)((p.rb + p.rstep * tj) * p.Sfull + (p.sb + p.sstep * ti)) * p.w_tap + kcs * 64;
-#pragma unroll
-        for (int i = 0; i < B_INS; ++i) {
-            const void* src = b_off[i] >= 0 ? (const void*)(Wt + wtap + b_off[i]) : zero;
-            glds16(src, __builtin_amdgcn_readfirstlane(ldsB + buf * BBUF + (i * NW + w) * 1024));
-        }
-    };
-
-    f32x4 acc[8][2 * NFH];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 2 * NFH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    if (iters > 0) {
-        for (int h = 0; h < h_n; ++h) load_halo(h, kc_begin, 0);
-        issue_b(0, 0);
-        if (iters > 1) issue_b(1, 1);
-    }
-    wait_vmcnt<0>();
-    lds_barrier();
-    if (wm == 1) __builtin_amdgcn_s_barrier();
-
-    const int fr = lane & 15, fg = lane >> 4;
-    const int rb0 = ((wm * 128) / BW) * g.hwd + ((wm * 128) % BW) + fr;
-    int kc = kc_begin, hbuf = 0, tap = 0;
-    for (int it = 0; it < iters; ++it) {
-        const char* Hs = smem + hbuf * HBUF;
-        const char* Bs = smem + 2 * HBUF + (it & 1) * BBUF;
-        const int t_j = tap / p.taps_w, t_i = tap - (tap / p.taps_w) * p.taps_w;
-        const int toff = (t_j * p.tsh - g.hy0) * g.hwd + t_i * p.tsw - g.hx0;
-        uint4 af[2][2][4], bq[2][2][NFH];   // A [mh][ks][mi]; B [nh][ks][ni]
-        // ---- read phase: every fragment of the iteration
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int ml = mh * 64 + mi * 16;   // within the wave's 128 rows
-                const int row = rb0 + (ml / BW) * g.hwd + (ml % BW) + toff;
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-                    af[mh][ks][mi] = *reinterpret_cast<const uint4*>(Hs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
-            }
-#pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int ni = 0; ni < NFH; ++ni) {
-                    const int row = wn * WTN + nh * (WTN / 2) + ni * 16 + fr;
-                    bq[nh][ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ (row & 6)));
-                }
-        if (wm == 0 && it + 1 >= 2 && it + 1 < iters) issue_b(it + 1, (it + 1) & 1);
-        if (tap < h_n && kc + 1 < kc_end) load_halo(tap, kc + 1, hbuf ^ 1);
-        if (wm == 1 && it + 2 < iters) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own reads of slice it retired
-            issue_b(it + 2, it & 1);
-        }
-        lds_barrier();
-        // ---- MFMA phase (conv_halo2's per-accumulator order)
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int mh = q >> 1, nh = (q == 1 || q == 2) ? 1 : 0;   // (0,0) (0,1) (1,1) (1,0)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < NFH; ++ni)
-                        acc[mh * 4 + mi][nh * NFH + ni] =
-                            mfma16x16x32<T>(af[mh][ks][mi], bq[nh][ks][ni], acc[mh * 4 + mi][nh * NFH + ni]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        if (++tap == ntaps) {
-            tap = 0;
-            ++kc;
-            hbuf ^= 1;
-        }
-    }
-    if (wm == 0) __builtin_amdgcn_s_barrier();
-
-    if (p.partial) {
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int ml = wm * 128 + mi * 16 + fg * 4 + r;
-                const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-                if (oy >= p.Ha || ox >= p.Wa) continue;
-                const long m = ((long)img * p.Ha + oy) * p.Wa + ox;
-                float* prow = p.partial + ((long)blockIdx.z * p.M + m) * p.N;
-#pragma unroll
-                for (int ni = 0; ni < 2 * NFH; ++ni) {
-                    const int col = n0 + wn * WTN + ni * 16 + fr;
-                    if (col < p.N) prow[col] = acc[mi][ni][r];
-                }
-            }
-        return;
-    }
-    // ---- epilogue in two 64-row halves per wave (LDS holds 8 x 64 x WTN fp32)
-    constexpr int SROW = WTN * 4 + 16;
-    constexpr int CPR = WTN / 8, RPP = 64 / CPR;
-    static_assert(NW * 64 * SROW <= SMEM, "epilogue staging must fit");
-    const int cch = lane % CPR, rsub = lane / CPR;
-    const int col0 = n0 + wn * WTN + cch * 8;
-    const EpiParams& e = p.epi;
-    float bias[8], scl[8], shf[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int col = col0 + j;
-        const bool cv = col < e.n_valid;
-        bias[j] = (e.bias && cv) ? e.bias[col] : 0.f;
-        scl[j] = (e.scale && cv) ? e.scale[col] : 1.f;
-        shf[j] = (e.shift && cv) ? e.shift[col] : 0.f;
-    }
-    char* wbuf = smem + w * 64 * SROW;
-    // ReluGrad mask rows: the first half's requested before its staging, the
-    // second half's row by row as the first half's are consumed
-    constexpr int NRR = 64 / RPP;
-    uint4 mkv[NRR];
-    auto load_mask = [&](int mh, int k) {
-        const int ml = wm * 128 + mh * 64 + rsub + k * RPP;
-        const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-        mkv[k] = uint4{0u, 0u, 0u, 0u};
-        if (oy < p.Ha && ox < p.Wa && col0 < p.N)
-            mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
-                                                     halo_opix(p, oy, ox) * e.ld_mask + col0);
-    };
-    if (e.mask) {
-#pragma unroll
-        for (int k = 0; k < NRR; ++k) load_mask(0, k);
-    }
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh) {
-        lds_barrier();
-        {
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int ni = 0; ni < 2 * NFH; ++ni)
-                        *reinterpret_cast<float*>(wbuf + (mi * 16 + fg * 4 + r) * SROW + (ni * 16 + fr) * 4) =
-                            acc[mh * 4 + mi][ni][r];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (CPR == 8) {
-            if (e.pool_y) {              // MaxPool fused: pooled map + switches only
-                pool_epi_rows<T, BW, 64>(p, wbuf + cch * 32, SROW, wm * 128 + mh * 64, oy0, ox0, img, col0, lane,
-                                         bias, scl, shf);
-                continue;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NRR; ++k) {
-            const int rr = rsub + k * RPP;
-            const int ml = wm * 128 + mh * 64 + rr;
-            const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
-            float mk[8];
-            if (e.mask) {
-                Chunk<T>::unpack(mkv[k], mk);
-                if (mh == 0) load_mask(1, k);
-            }
-            if (oy >= p.Ha || ox >= p.Wa || col0 >= p.N) continue;
-            const long pix = halo_opix(p, oy, ox);
-            float v[8];
-            splitk_lds8(wbuf + rr * SROW + cch * 32, v);
-            float res[8];
-            if (e.residual) {
-                const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
-                Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
-            }
-            const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int col = col0 + j;
-                float x = v[j] * scl[j] + shf[j] + bias[j];
-                if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
-                if (e.residual) x += res[j];
-                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
-                v[j] = col < e.n_valid ? x : 0.f;
-            }
-            T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
-            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Persistent variant for a single 64-channel chunk with N <= 64 (conv1_2 fwd
@@ -2169,7 +1896,7 @@ bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* 
                 hp->geom[4] = hwd; hp->geom[5] = hwd * hht;
             }
         }
-        if (best2 >= 0 && (long)p.IH * p.IW * p.ldx < (1L << 31)) hp->bn = 256;
+        if (best2 >= 0) hp->bn = 256;
     }
     const int nchunks = p.C / 64;
     const long tiles = (long)hp->geom[1] * hp->geom[2] * nimg * ((p.N + hp->bn - 1) / hp->bn);
@@ -2351,16 +2078,6 @@ int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int 
             }
         }
 #endif
-        if (g_halo2_1p) {
-            if (dtype == SEG_F16) {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2s<16, f16>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2s<32, f16>), grid, dim3(512), 0, s, p, g);
-            } else {
-                if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2s<16>), grid, dim3(512), 0, s, p, g);
-                else hipLaunchKernelGGL((conv_halo2s<32>), grid, dim3(512), 0, s, p, g);
-            }
-            return SEG_OK;
-        }
         if (dtype == SEG_F16) {
             if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, 0, f16>), grid, dim3(512), 0, s, p, g);
             else hipLaunchKernelGGL((conv_halo2<32, 0, f16>), grid, dim3(512), 0, s, p, g);

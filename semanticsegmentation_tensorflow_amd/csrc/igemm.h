@@ -282,7 +282,6 @@ extern int g_res16;
 extern int g_res64_pp;
 extern int g_res16_dma;
 extern int g_res16c_bh;
-extern int g_halo2_1p;
 extern int g_smallk_abl;
 // the launch plan for p writes EpiParams.y2 (seg_conv2d_fwd_bn2)
 bool nt_bn2_ok(const NTParams& p, int dtype);

@@ -76,6 +76,46 @@ class Workspace:
 # ---------------------------------------------------------------------------
 # descriptors
 # ---------------------------------------------------------------------------
+class TimingEvent:
+    """A HIP event for kernel timing without the system-scope cache flush
+    (seg_timing_event_*); torch.cuda.Event's record / elapsed_time API."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(_lib.lib().seg_timing_event_create(ctypes.byref(h)), "timing_event")
+        self._h = h
+
+    def record(self, stream=None):
+        check(_lib.lib().seg_timing_event_record(self._h, stream_ptr(stream)), "timing_event")
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        check(_lib.lib().seg_timing_event_elapsed_ms(ctypes.byref(ms), self._h, end._h), "timing_event")
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.lib().seg_timing_event_destroy(self._h)
+            self._h = None
+
+
+def cu_masked_stream(device, pct, contiguous=False):
+    """A torch.cuda.ExternalStream whose kernels run on `pct` % of the
+    device's CUs (seg_stream_create_cu_mask): evenly spread over the CU
+    indices, or the first ones (contiguous).  The stream is never destroyed
+    (Sessions keep theirs for the process lifetime)."""
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    keep = [(i * pct) // 100 != ((i + 1) * pct) // 100 for i in range(n)] if not contiguous else \
+        [i < n * pct // 100 for i in range(n)]
+    words = (ctypes.c_uint * ((n + 31) // 32))()
+    for i, k in enumerate(keep):
+        if k:
+            words[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    check(_lib.lib().seg_stream_create_cu_mask(ctypes.byref(h), words, len(words)), "cu_masked_stream")
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
 def conv_desc(N, H, W, C, K, R, S, stride=1, dilation=1, padding="SAME", dtype=BF16):
     d = SegConvDesc()
     check(_lib.lib().seg_conv_desc_init(ctypes.byref(d), N, H, W, C, K, R, S, stride, dilation,

@@ -108,10 +108,10 @@ class StreamMixin:
         launch: bench.py times only the dominant kernel's launches)."""
         if self.timer is None or (self.timer_match is not None and not self.timer_match(desc, op)):
             return fn(*args)
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
+        s, e = ops.TimingEvent(), ops.TimingEvent()    # no cache flush in the interval
+        stream = torch.cuda.current_stream(self.device)
+        s.record(stream)
         r = fn(*args)
-        e.record()
+        e.record(stream)
         self.timer.append((desc, op, s, e))
         return r
