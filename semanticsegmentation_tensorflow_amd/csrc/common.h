@@ -125,14 +125,18 @@ template <> struct Chunk<f16> {
     }
 };
 
-// Counter-based uniform in [0,1) for TF1 dropout: the top 24 bits of a
-// lowbias32-style finalizer (xorshift-multiply, 32-bit multiplies: quarter
-// rate on CDNA, ~2.5x cheaper than a 64-bit splitmix in the fused conv
-// epilogues) of the counter (high word folded in first), with the seed key --
-// itself fully avalanched, a loop invariant -- XORed in after the first
-// multiply.  Mixing the key non-additively keeps the streams of different
-// seeds (layers, steps, data-parallel ranks) from being shifted copies of one
-// another, which F(idx + key) would make them.  Restated in numpy by the tests.
+// Counter-based uniform in [0,1) for TF1 dropout, in groups of 8 counters:
+// counter idx = 8 q + j.  The group hash of q is a lowbias32-style finalizer
+// (xorshift-multiply, 32-bit multiplies: quarter rate on CDNA) of q (high word
+// folded in first) with the seed key -- itself fully avalanched, a loop
+// invariant -- XORed in after the first multiply; mixing the key
+// non-additively keeps the streams of different seeds (layers, steps,
+// data-parallel ranks) from being shifted copies of one another.  Each element
+// then takes one more xorshift-multiply-xorshift of (group hash + j * golden
+// ratio), so a lane that owns 4 or 8 consecutive counters (the conv
+// epilogues' column chunks) pays ONE multiply per element plus the group hash
+// once (SegDropRun), instead of the three multiplies per element of a
+// per-counter finalizer.  Restated in numpy by the tests.
 __host__ __device__ __forceinline__ uint32_t seg_avalanche32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7FEB352Du;
@@ -142,16 +146,31 @@ __host__ __device__ __forceinline__ uint32_t seg_avalanche32(uint32_t x) {
     return x;
 }
 
-__host__ __device__ __forceinline__ float seg_uniform(uint64_t seed, uint64_t idx) {
-    const uint32_t key = seg_avalanche32((uint32_t)(seed ^ (seed >> 32)) ^ 0x632BE59Bu);
-    uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x85EBCA6Bu);
+__host__ __device__ __forceinline__ uint32_t seg_drop_key(uint64_t seed) {
+    return seg_avalanche32((uint32_t)(seed ^ (seed >> 32)) ^ 0x632BE59Bu);
+}
+
+__host__ __device__ __forceinline__ uint32_t seg_grp_hash(uint32_t key, uint64_t q) {
+    uint32_t x = (uint32_t)q ^ ((uint32_t)(q >> 32) * 0x85EBCA6Bu);
     x ^= x >> 16;
     x *= 0x7FEB352Du;
     x ^= key;
     x ^= x >> 15;
     x *= 0x846CA68Bu;
     x ^= x >> 16;
+    return x;
+}
+
+__host__ __device__ __forceinline__ float seg_grp_uniform(uint32_t h, uint32_t j) {
+    uint32_t x = h + j * 0x9E3779B9u;
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
     return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+__host__ __device__ __forceinline__ float seg_uniform(uint64_t seed, uint64_t idx) {
+    return seg_grp_uniform(seg_grp_hash(seg_drop_key(seed), idx >> 3), (uint32_t)idx & 7u);
 }
 
 // TF1 dropout of one element, x / kp * floor(kp + U(seed, idx)), with the
@@ -160,6 +179,28 @@ __host__ __device__ __forceinline__ float seg_uniform(uint64_t seed, uint64_t id
 __host__ __device__ __forceinline__ float seg_dropout(float x, float kp, uint64_t seed, uint64_t idx) {
     return (x * (1.f / kp)) * floorf(kp + seg_uniform(seed, idx));
 }
+
+// Dropout of N <= 8 consecutive counters base .. base + N - 1 (one lane's
+// column chunk): the one or two group hashes they touch computed once.
+// Same values as seg_dropout element by element.
+template <int N>
+struct SegDropRun {
+    static_assert(N >= 1 && N <= 8, "at most one group boundary");
+    uint32_t h0, h1, off;
+    // on == false (keep_prob 1): no hashing; operator() must not be called
+    __host__ __device__ __forceinline__ SegDropRun(uint64_t seed, uint64_t base, bool on = true) {
+        h0 = h1 = off = 0u;
+        if (!on) return;
+        const uint32_t key = seg_drop_key(seed);
+        off = (uint32_t)base & 7u;
+        h0 = seg_grp_hash(key, base >> 3);
+        h1 = off + N > 8 ? seg_grp_hash(key, (base >> 3) + 1) : h0;
+    }
+    __host__ __device__ __forceinline__ float operator()(float x, float kp, int j) const {
+        const uint32_t jj = off + (uint32_t)j;
+        return (x * (1.f / kp)) * floorf(kp + seg_grp_uniform(jj < 8u ? h0 : h1, jj & 7u));
+    }
+};
 
 #define SEG_CHECK_LAUNCH()                                     \
     do {                                                       \

@@ -557,6 +557,9 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
         {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {4, 8}},
         {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
+        {"bn1x1s_fill", &seg::g_bn1x1s_fill, 1, 8, 1, {}},
+        {"s1x1_fill", &seg::g_s1x1_fill, 1, 8, 1, {}},
+        {"res64_fill", &seg::g_res64_fill, 1, 8, 1, {}},
         {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
         {"res16c_st", &seg::g_res16c_st, 0, 1, 1, {}},
         {"dropout_flat", &seg::g_dropout_flat, 0, 1, 1, {}},

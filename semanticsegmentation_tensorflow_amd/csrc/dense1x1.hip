@@ -171,11 +171,12 @@ __global__ __launch_bounds__(512, 1) void conv1x1_stream(NTParams p, int ntiles,
                 const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
                 const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
                 T o[4];
+                const SegDropRun<4> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float v = acc[nf][j] * sc4[j] + ad4[j];
                     if (e.relu) v = fmaxf(v, 0.f);
-                    if (e.keep_prob < 1.f) v = seg_dropout(v, e.keep_prob, e.seed, gidx + col0 + j);
+                    if (e.keep_prob < 1.f) v = drop(v, e.keep_prob, j);
                     o[j] = from_f32<T>(col0 + j < e.n_valid ? v : 0.f);
                 }
                 const bool ok = m < p.M && col0 < p.N;
@@ -444,10 +445,16 @@ static bool bn1x1s_args_ok(const NTParams& p) {
 
 // blocks per 64-channel chunk (= the BN partial rows): a multiple of 8, one
 // block per CU over all chunks
+// persistent grids in blocks per CU (1: one round; more: shorter tile ranges,
+// so a kernel sharing the chip with the side stream's blocks is not held to
+// its last-started CU's whole range)
+int g_bn1x1s_fill = 1;
+int g_s1x1_fill = 1;
+
 int bn1x1s_rows(const NTParams& p, int cus) {
     const int nch = (p.N + 63) / 64;
     const int ntiles = (p.M + B1_TP - 1) / B1_TP;
-    int G = std::max(8, (cus / nch) & ~7);
+    int G = std::max(8, (cus * g_bn1x1s_fill / nch) & ~7);
     return std::min(G, std::max(8, (ntiles + 7) & ~7));
 }
 
@@ -477,7 +484,7 @@ static void launch_s1x1_t(NTParams& p, int grid, int ntiles, int kt, bool st, hi
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {
     const int ntiles = (p.M + S1_TP - 1) / S1_TP;
     const int kt = (p.K + 63) / 64;
-    const int grid = std::min(ntiles, cus);
+    const int grid = std::min(ntiles, cus * g_s1x1_fill);
     const bool pro = p.pro.gamma != nullptr;
     const bool st = (g_s1x1_st == 2 || (g_s1x1_st == 1 && kt == 1)) && p.N % 8 == 0 && p.ldy % 8 == 0 &&
                     ((uintptr_t)p.y % 16) == 0 &&

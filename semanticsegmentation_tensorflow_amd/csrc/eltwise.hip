@@ -361,7 +361,6 @@ __global__ __launch_bounds__(256) void dropout_ch_k(const T* __restrict__ dy, in
     const int t = threadIdx.x;
     const int c8 = t % g.LPP, prow = t / g.LPP;
     if (prow >= g.rows) return;
-    const float rkp = 1.f / kp;
     const long step = (long)gridDim.x * g.rows;
     for (long pix = (long)blockIdx.x * g.rows + prow; pix < P; pix += step) {
         const uint64_t base = (uint64_t)pix * cv;
@@ -372,10 +371,11 @@ __global__ __launch_bounds__(256) void dropout_ch_k(const T* __restrict__ dy, in
             if (cc >= g.CK) break;
             float v[EPC];
             Chunk<T>::unpack(ldc(dy + pix * ldy + cc * EPC), v);
+            const SegDropRun<EPC> drop(seed, base + cc * EPC);
 #pragma unroll
             for (int e = 0; e < EPC; ++e) {
                 const int c = cc * EPC + e;
-                v[e] = c < cv ? (v[e] * rkp) * floorf(kp + seg_uniform(seed, base + c)) : 0.f;
+                v[e] = c < cv ? drop(v[e], kp, e) : 0.f;
             }
             stc(dz + pix * ldz + cc * EPC, Chunk<T>::pack(v));
         }
@@ -393,14 +393,14 @@ __global__ __launch_bounds__(256) void dropout_ch_flat_k(const T* __restrict__ d
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q >= P * CK) return;
     const int pix = q / CK, cc = q - pix * CK;
-    const float rkp = 1.f / kp;
     const uint64_t base = (uint64_t)pix * cv;
     float v[EPC];
     Chunk<T>::unpack(ldc(dy + (long)pix * ldy + cc * EPC), v);
+    const SegDropRun<EPC> drop(seed, base + cc * EPC);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
         const int c = cc * EPC + e;
-        v[e] = c < cv ? (v[e] * rkp) * floorf(kp + seg_uniform(seed, base + c)) : 0.f;
+        v[e] = c < cv ? drop(v[e], kp, e) : 0.f;
     }
     stc(dz + (long)pix * ldz + cc * EPC, Chunk<T>::pack(v));
 }
@@ -663,7 +663,6 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
             sc[j][e] = ok ? gamma[c] * inv : 0.f;
             sh[j][e] = ok && remask ? beta[c] : 0.f;
         }
-    const float rdkp = dkp < 1.f ? 1.f / dkp : 1.f;
     if (active) {
         for (long pix = p0 + prow; pix < p1; pix += g.rows) {
             const uint64_t dbase = (uint64_t)pix * dcv;
@@ -677,6 +676,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                 if (relu && !remask) Chunk<T>::unpack(ldc(y + pix * ldy + cc * EPC), yv);
                 Chunk<T>::unpack(ldc(dy + pix * lddy + cc * EPC), d);
                 if (acc) Chunk<T>::unpack(ldc(dx + pix * lddx + cc * EPC), old);
+                const SegDropRun<EPC> drop(dseed, dbase + cc * EPC, dkp < 1.f);
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) {
                     const int c = cc * EPC + e;
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_k(const T* __restrict__ x, in
                     if (acc) d[e] += old[e];
                     // dropout of the conv epilogue that produced x (no ReLU
                     // between): its gradient, same counter as the forward draw
-                    if (dkp < 1.f) d[e] = c < dcv ? (d[e] * rdkp) * floorf(dkp + seg_uniform(dseed, dbase + c)) : 0.f;
+                    if (dkp < 1.f) d[e] = c < dcv ? drop(d[e], dkp, e) : 0.f;
                 }
                 stc(dx + pix * lddx + cc * EPC, Chunk<T>::pack(d));
             }

@@ -42,6 +42,7 @@ int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 // pooled forward and the ReluGrad-masked input gradient (conv1_2: 191 vs 192
 // and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
 int g_res64_pp = 1;
+int g_res64_fill = 1;   // persistent grid rounds of conv_res64 / conv_res64pp (blocks per resident slot)
 int g_res16_dma = 1;
 int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8 or 4)
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
@@ -369,12 +370,13 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
             Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
         }
         const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+        const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int col = col0 + j;
             float x = v[j] * scl[j] + shf[j] + bias[j];
             if (e.relu) x = fmaxf(x, 0.f);
-            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+            if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
             if (e.residual) x += res[j];
             if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
             v[j] = col < e.n_valid ? x : 0.f;
@@ -595,6 +597,7 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             }
             const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
@@ -602,7 +605,7 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                 const float sc = (e.scale && cv) ? e.scale[col] : 1.f, sh = (e.shift && cv) ? e.shift[col] : 0.f;
                 float x = v[j] * sc + sh + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (e.residual) x += res[j];
                 if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
@@ -918,12 +921,13 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             }
             const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
                 float x = v[j] * scl[j] + shf[j] + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (e.residual) x += res[j];
                 if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
@@ -1237,12 +1241,13 @@ __global__ __launch_bounds__(512, NB == 16 ? (DMA ? 4 : 2) : 1) void conv_res64(
                     T o[4];
                     const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
                     const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
+                    const SegDropRun<4> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int col = col0 + j;
                         float x = acc[mi][ni][j] * sc4[j] + ad4[j];
                         if (e.relu) x = fmaxf(x, 0.f);
-                        if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                        if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                         x += res[j];
                         if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                         o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
@@ -1519,12 +1524,13 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
                         T o[4];
                         const f32x4 sc4 = *reinterpret_cast<const f32x4*>(etab + col0);
                         const f32x4 ad4 = *reinterpret_cast<const f32x4*>(etab + NB + col0);
+                        const SegDropRun<4> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int col = col0 + j;
                             float x = acc[mi][ni][j] * sc4[j] + ad4[j];
                             if (e.relu) x = fmaxf(x, 0.f);
-                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                             x += res[j];
                             if (e.mask) x = (mbits >> ((mi * TN + ni) * 4 + j)) & 1 ? x * e.mask_scale : 0.f;
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
@@ -1751,6 +1757,7 @@ __global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res
                         const T* xh = reinterpret_cast<const T*>(&xr);
                         const f32x4 bs4 = *reinterpret_cast<const f32x4*>(&etab[2][col0]);
                         const f32x4 bb4 = *reinterpret_cast<const f32x4*>(&etab[3][col0]);
+                        const SegDropRun<4> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int col = col0 + j;
@@ -1760,18 +1767,19 @@ __global__ __launch_bounds__(BH * 64, BNB ? (BH == 8 ? 2 : 3) : 4) void conv_res
                             sgm[ni][j] += dz * xv;
                             sbt[ni][j] += dz;
                             float x = dz * bs4[j];
-                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
                         }
                     } else {
                         const f32x4 sc4 = *reinterpret_cast<const f32x4*>(&etab[0][col0]);
                         const f32x4 ad4 = *reinterpret_cast<const f32x4*>(&etab[1][col0]);
+                        const SegDropRun<4> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int col = col0 + j;
                             float x = acc[mi][ni][j] * sc4[j] + ad4[j];
                             if (e.relu) x = fmaxf(x, 0.f);
-                            if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                            if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                             x += res[j];
                             if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
@@ -2028,7 +2036,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     if (p.N <= 16 && g_res16) {
         if (p.epi.pool_y) return SEG_EINVAL;  // no pooled epilogue in the 16-wide form
-        const int grid = std::min(ntiles, 2 * cus);
+        const int grid = std::min(ntiles, 2 * cus * g_res64_fill);
         if (g_res16_dma) {                    // two blocks per CU (launch bounds: 4 waves / SIMD)
             if (dtype == SEG_F16)
                 hipLaunchKernelGGL((conv_res64<0, f16, 16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
@@ -2041,7 +2049,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
         }
         return SEG_OK;
     }
-    const int grid = std::min(ntiles, cus);
+    const int grid = std::min(ntiles, cus * g_res64_fill);
     if (g_res64_pp == 2 || (g_res64_pp == 1 && (p.epi.pool_y || p.epi.mask))) {
         if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64pp<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         else hipLaunchKernelGGL((conv_res64pp<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);

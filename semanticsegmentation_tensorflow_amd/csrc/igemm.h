@@ -318,6 +318,9 @@ extern int g_wgrad_nbias;
 extern int g_wgrad_nt32;
 extern int g_wgrad_fill;
 extern int g_wgrad_fill16;
+extern int g_bn1x1s_fill;
+extern int g_res64_fill;
+extern int g_s1x1_fill;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);

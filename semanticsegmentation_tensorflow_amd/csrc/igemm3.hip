@@ -301,12 +301,13 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             }
             const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
+            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
                 float x = v[j] * scl[j] + shf[j] + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (e.residual) x += res[j];
                 if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;

@@ -233,13 +233,14 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p, int abl) {
             Chunk<T>::unpack(rq[u], res);
             Chunk<T>::unpack(mq[u], mk);
             const uint64_t gidx = ((uint64_t)m) * e.n_valid;
+            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
                 const bool cv = col < e.n_valid;
                 float x = v[j] * sc[j] + ad[j] + bs[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = seg_dropout(x, e.keep_prob, e.seed, gidx + col);
+                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (RS) x += res[j];
                 if (MK) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = cv ? x : 0.f;

@@ -474,18 +474,38 @@ def _np_avalanche32(x):
 
 
 def _np_uniform(seed, idx):
-    """seg_uniform (csrc/common.h): counter finalizer with the avalanched seed
-    key XORed in after the first multiply."""
+    """seg_uniform (csrc/common.h): counters in groups of 8, idx = 8 q + j; the
+    group hash of q is a counter finalizer with the avalanched seed key XORed
+    in after the first multiply, then one xorshift-multiply-xorshift of
+    (group hash + j * golden ratio) per element."""
     M = 0xFFFFFFFF
     key = _np_avalanche32(((seed ^ (seed >> 32)) & M) ^ 0x632BE59B)
-    x = ((idx & M) ^ (((idx >> 32) * 0x85EBCA6B) & M)) & M
+    q, j = idx >> 3, idx & 7
+    x = ((q & M) ^ (((q >> 32) * 0x85EBCA6B) & M)) & M
     x ^= x >> 16
     x = (x * 0x7FEB352D) & M
     x ^= key
     x ^= x >> 15
     x = (x * 0x846CA68B) & M
     x ^= x >> 16
+    x = (x + j * 0x9E3779B9) & M
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M
+    x ^= x >> 15
     return (x >> 8) / 16777216.0
+
+
+def test_uniform_grouped_counters_are_independent():
+    """Counters in groups of 8 share a group hash: the Bernoulli(0.2) keep
+    masks of neighbours within a group, and of the same slot in adjacent
+    groups, stay uncorrelated, and every slot keeps its rate."""
+    from tests.test_gpu_ops_r2 import _np_uniform_vec
+    u = _np_uniform_vec(1234, np.arange(1 << 18, dtype=np.uint64)).reshape(-1, 8)
+    k = (u < 0.2).astype(np.float64)
+    assert np.all(np.abs(k.mean(0) - 0.2) < 0.01)
+    for a, b in ((k[:, :-1], k[:, 1:]), (k[:-1], k[1:]), (k[:, :4], k[:, 4:])):
+        c = np.corrcoef(a.ravel(), b.ravel())[0, 1]
+        assert abs(c) < 0.01, c
 
 
 def test_uniform_streams_of_different_seeds_are_not_shifts():

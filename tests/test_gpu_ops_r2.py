@@ -231,13 +231,19 @@ def _np_uniform_vec(seed, idx):
     from tests.test_gpu_ops import _np_avalanche32
     M = np.uint64(0xFFFFFFFF)
     key = np.uint64(_np_avalanche32(((seed ^ (seed >> 32)) & 0xFFFFFFFF) ^ 0x632BE59B))
-    x = ((idx & M) ^ (((idx >> np.uint64(32)) * np.uint64(0x85EBCA6B)) & M)) & M
+    idx = np.asarray(idx, dtype=np.uint64)
+    q, j = idx >> np.uint64(3), idx & np.uint64(7)
+    x = ((q & M) ^ (((q >> np.uint64(32)) * np.uint64(0x85EBCA6B)) & M)) & M
     x ^= x >> np.uint64(16)
     x = (x * np.uint64(0x7FEB352D)) & M
     x ^= key
     x ^= x >> np.uint64(15)
     x = (x * np.uint64(0x846CA68B)) & M
     x ^= x >> np.uint64(16)
+    x = (x + j * np.uint64(0x9E3779B9)) & M
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & M
+    x ^= x >> np.uint64(15)
     return ((x >> np.uint64(8)).astype(np.float64) / 16777216.0).astype(np.float32)
 
 
