@@ -610,6 +610,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_tn(TNParams p, int splits, 
         for (int r = m; r < r_end; ++r) {
             const float* src = p.partial + (long)r * p.N + n0;
             int z = sl;
+            for (; z + 7 * SL < splits; z += 8 * SL) {  // 8 independent slab loads in flight
+                float4 a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a[u] = *reinterpret_cast<const float4*>(src + (z + u * SL) * slab);
+                s.x += ((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x));
+                s.y += ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y));
+                s.z += ((a[0].z + a[1].z) + (a[2].z + a[3].z)) + ((a[4].z + a[5].z) + (a[6].z + a[7].z));
+                s.w += ((a[0].w + a[1].w) + (a[2].w + a[3].w)) + ((a[4].w + a[5].w) + (a[6].w + a[7].w));
+            }
             for (; z + 3 * SL < splits; z += 4 * SL) {  // 4 independent slab loads in flight
                 const float4 a = *reinterpret_cast<const float4*>(src + z * slab);
                 const float4 b = *reinterpret_cast<const float4*>(src + (z + SL) * slab);

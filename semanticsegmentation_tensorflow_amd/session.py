@@ -176,6 +176,11 @@ class Session(PlanMixin, StreamMixin):
         # CUs): the HBM-bound update otherwise holds every CU for ~0.9 ms while
         # the input-gradient chain's 160 KiB-LDS conv tiles wait for one
         self.fused_cu_pct = 0
+        # data-parallel all-reduce steps: the Adam update of every variable of
+        # >= overlap_big_mb MB (FCN conv6 / conv7) as soon as its buckets'
+        # collectives complete, on the CU-masked stream (fused_cu_pct) or the
+        # side stream, beside the rest of backward (0: all at the end)
+        self.overlap_big_mb = 0
         self.fused_cu_contig = 0
         self._fused_stream = None
         self._fused_used = False
@@ -777,6 +782,10 @@ class Session(PlanMixin, StreamMixin):
                 self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set)
                 if dpa is not None:
                     dpa.on_launch = self._adam_ctx.after_work
+            elif (opt is not None and dpa is not None and not zero and self.overlap_big_mb and not scaled
+                  and not p.train.accum and self.device.type == "cuda"):
+                self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set, big_only=True)
+                dpa.on_launch = self._adam_ctx.after_work
             if dpa is not None and p.never_ready:
                 dpa.ready(p.never_ready)
             self._ready_filter = p.var_set

@@ -6,6 +6,7 @@ timing, and the overlapped per-layer optimizer.  Split out of session.py;
 from __future__ import annotations
 
 import contextlib
+import math
 
 import torch
 
@@ -21,7 +22,7 @@ class _AdamOverlap:
     (its input gradient is enqueued before its filter gradient).  finish()
     updates the remaining variables and makes the compute stream wait."""
 
-    def __init__(self, sess, opt, gs, var_set):
+    def __init__(self, sess, opt, gs, var_set, big_only=False):
         self.s = sess
         self.opt = opt
         self.gs = gs
@@ -31,15 +32,31 @@ class _AdamOverlap:
         self.side = sess._side
         self.main = torch.cuda.current_stream(sess.device)
         self.done = set()
+        # big_only (data-parallel all-reduce steps, Session.overlap_big_mb):
+        # only variables of >= overlap_big_mb MB overlap (FCN: conv6, conv7 --
+        # the 2.9 GB of Adam traffic the single-process step fuses into their
+        # filter gradients), on the CU-masked stream when fused_cu_pct is set;
+        # finish() updates the rest in one launch on the compute stream
+        self.big = None
+        if big_only:
+            st = sess.store
+            lim = sess.overlap_big_mb * (1 << 20) / 4
+            self.big = {nm for nm in var_set if nm in st.by_name and math.prod(st.by_name[nm].shape) >= lim}
+            if sess.fused_cu_pct:
+                if sess._fused_stream is None:
+                    sess._fused_stream = ops.cu_masked_stream(sess.device, sess.fused_cu_pct,
+                                                              bool(sess.fused_cu_contig))
+                self.side = sess._fused_stream
 
-    def _adam(self, names):
+    def _adam(self, names, stream=None):
         st = self.s.store
         o = self.opt
         names = [nm for nm in names if nm in self.var_set]
         if not names:
             return
         ops.adam_tf1_pack(st.params, st.grads, st.m, st.v, self.s._adam_plan(names), o.lr, st.step, o.beta1,
-                          o.beta2, o.epsilon, grad_scale=self.gs, dtype=self.s._pack_dtype(), stream=self.side)
+                          o.beta2, o.epsilon, grad_scale=self.gs, dtype=self.s._pack_dtype(),
+                          stream=self.side if stream is None else stream)
         self.done.update(names)
 
     def launch(self, names):
@@ -49,6 +66,10 @@ class _AdamOverlap:
         self._adam(names)
 
     def after_work(self, works, names):
+        if self.big is not None:
+            names = [nm for nm in names if nm in self.big]
+            if not names:
+                return
         if works:
             with torch.cuda.stream(self.side):
                 for w in works:
@@ -61,6 +82,11 @@ class _AdamOverlap:
 
     def finish(self):
         rest = [v.var_name for v in self.s.store.order if v.var_name in self.var_set and v.var_name not in self.done]
+        if self.big is not None:           # the small variables: one launch on the compute stream
+            self.main.wait_stream(self.side)
+            if rest:
+                self._adam(rest, stream=self.main)
+            return
         if rest:
             self.launch(rest)
         self.main.wait_stream(self.side)

@@ -43,6 +43,8 @@ CASES = [
     ("dp_bf16_zero", "bf16", "zero", {}),
     ("dp_bf16_zero_serial", "bf16", "zero", {"side_wgrad": 0, "main_wgrad": 0}),
     ("dp_bf16_allreduce", "bf16", "allreduce", {"side_wgrad": 1}),
+    ("dp_bf16_allreduce_big", "bf16", "allreduce", {"overlap_big_mb": 4, "fused_cu_pct": 50}),
+    ("dp_f32_allreduce_big", "f32", "allreduce", {"overlap_big_mb": 1}),
 ]
 
 
