@@ -523,7 +523,9 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
             a[1] += s_ev.elapsed_time(e_ev)
         sess.timer = None
         sess.side_wgrad = side_mode
-    dname, (dn, dflops, dms, dbytes) = max(per.items(), key=lambda kv: kv[1][2])
+    # the dominant family: the most algorithmic work per step (its in-step time
+    # decides nothing: two families of similar time would swap between runs)
+    dname, (dn, dflops, dms, dbytes) = max(per.items(), key=lambda kv: kv[1][1])
     # the dominant family re-timed in-step with events around ITS launches
     # only (every other launch un-instrumented, as in the timed steps): the
     # figure the line reports, comparable with the kernel durations of the
