@@ -542,12 +542,6 @@ int seg_timing_event_create(void** ev);
 int seg_timing_event_record(void* ev, void* stream);
 int seg_timing_event_elapsed_ms(float* ms, void* start, void* end);
 int seg_timing_event_destroy(void* ev);
-/* A HIP stream restricted to the CUs set in mask (nwords 32-bit words, bit i
- * = CU i): the Session runs the HBM-bound fused conv6 / conv7 filter-gradient
- * + Adam launches there (FCN.py:78, :338-340) so they leave CUs to the
- * input-gradient chain.  Not a TF interface: scheduling support. */
-int seg_stream_create_cu_mask(void** stream, const unsigned* mask, int nwords);
-int seg_stream_destroy(void* stream);
 const char* seg_status_string(int status);
 int seg_version(void);
 

@@ -172,8 +172,6 @@ SIGNATURES = {
     "seg_timing_event_record": (_I, [_P, _P]),
     "seg_timing_event_elapsed_ms": (_I, [ctypes.POINTER(ctypes.c_float), _P, _P]),
     "seg_timing_event_destroy": (_I, [_P]),
-    "seg_stream_create_cu_mask": (_I, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint), _I]),
-    "seg_stream_destroy": (_I, [_P]),
     "seg_conv_kernel_info": (_I, [_DP, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I),
                                   ctypes.POINTER(ctypes.c_double)]),
     "seg_pack_filter": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -545,7 +545,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"tn3", &seg::g_tn3, 0, 1, 1, {}},
         {"nt3", &seg::g_nt3, 0, 1, 1, {}},
         {"wgrad_fill", &seg::g_wgrad_fill, 1, 800, 1, {}},            // filter-gradient split-K, % of the CUs
-        {"wgrad_fill16", &seg::g_wgrad_fill16, 1, 800, 1, {}},        // ... for <= 32 output channels
         {"wgrad_nt32", &seg::g_wgrad_nt32, 0, 1, 1, {}},
         {"wgrad_nbias", &seg::g_wgrad_nbias, 1, 4, 1, {}},
         {"wgrad_nt", &seg::g_wgrad_nt, 0, 0, 0, {64, 128}},
@@ -557,9 +556,6 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
         {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {4, 8}},
         {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
-        {"bn1x1s_fill", &seg::g_bn1x1s_fill, 1, 8, 1, {}},
-        {"s1x1_fill", &seg::g_s1x1_fill, 1, 8, 1, {}},
-        {"res64_fill", &seg::g_res64_fill, 1, 8, 1, {}},
         {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
         {"res16c_st", &seg::g_res16c_st, 0, 1, 1, {}},
         {"dropout_flat", &seg::g_dropout_flat, 0, 1, 1, {}},

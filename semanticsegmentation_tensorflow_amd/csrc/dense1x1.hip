@@ -445,16 +445,10 @@ static bool bn1x1s_args_ok(const NTParams& p) {
 
 // blocks per 64-channel chunk (= the BN partial rows): a multiple of 8, one
 // block per CU over all chunks
-// persistent grids in blocks per CU (1: one round; more: shorter tile ranges,
-// so a kernel sharing the chip with the side stream's blocks is not held to
-// its last-started CU's whole range)
-int g_bn1x1s_fill = 1;
-int g_s1x1_fill = 1;
-
 int bn1x1s_rows(const NTParams& p, int cus) {
     const int nch = (p.N + 63) / 64;
     const int ntiles = (p.M + B1_TP - 1) / B1_TP;
-    int G = std::max(8, (cus * g_bn1x1s_fill / nch) & ~7);
+    int G = std::max(8, (cus / nch) & ~7);
     return std::min(G, std::max(8, (ntiles + 7) & ~7));
 }
 
@@ -484,7 +478,7 @@ static void launch_s1x1_t(NTParams& p, int grid, int ntiles, int kt, bool st, hi
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s) {
     const int ntiles = (p.M + S1_TP - 1) / S1_TP;
     const int kt = (p.K + 63) / 64;
-    const int grid = std::min(ntiles, cus * g_s1x1_fill);
+    const int grid = std::min(ntiles, cus);
     const bool pro = p.pro.gamma != nullptr;
     const bool st = (g_s1x1_st == 2 || (g_s1x1_st == 1 && kt == 1)) && p.N % 8 == 0 && p.ldy % 8 == 0 &&
                     ((uintptr_t)p.y % 16) == 0 &&

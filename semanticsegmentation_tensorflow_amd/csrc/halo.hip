@@ -42,7 +42,6 @@ int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 // pooled forward and the ReluGrad-masked input gradient (conv1_2: 191 vs 192
 // and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
 int g_res64_pp = 1;
-int g_res64_fill = 1;   // persistent grid rounds of conv_res64 / conv_res64pp (blocks per resident slot)
 int g_res16_dma = 1;
 int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8 or 4)
 int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
@@ -2036,7 +2035,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     if (p.N <= 16 && g_res16) {
         if (p.epi.pool_y) return SEG_EINVAL;  // no pooled epilogue in the 16-wide form
-        const int grid = std::min(ntiles, 2 * cus * g_res64_fill);
+        const int grid = std::min(ntiles, 2 * cus);
         if (g_res16_dma) {                    // two blocks per CU (launch bounds: 4 waves / SIMD)
             if (dtype == SEG_F16)
                 hipLaunchKernelGGL((conv_res64<0, f16, 16, true>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
@@ -2049,7 +2048,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
         }
         return SEG_OK;
     }
-    const int grid = std::min(ntiles, cus * g_res64_fill);
+    const int grid = std::min(ntiles, cus);
     if (g_res64_pp == 2 || (g_res64_pp == 1 && (p.epi.pool_y || p.epi.mask))) {
         if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64pp<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         else hipLaunchKernelGGL((conv_res64pp<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);

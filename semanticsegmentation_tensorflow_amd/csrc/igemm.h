@@ -116,6 +116,37 @@ __device__ __forceinline__ void splitk_lds8(const char* src, float v[8]) {
 }
 
 
+// Pixel cursor (img, row a, col b) over the N x Ha x Wa GEMM-k grid of a TN
+// (filter-gradient) kernel, advanced by a fixed step per k tile.  The step is
+// split once per kernel into q rows + r columns (0 <= r < Wa), so an advance
+// is two adds and at most one carry into the row and one into the image --
+// instead of a divergent `while (b >= Wa)` loop (~35 VALU / SALU per DMA piece
+// on conv6's 39-wide rows, ~40 % of the filter-gradient main loop's VALU).
+// Exact when q + 1 <= Ha (the step spans less than an image); otherwise
+// (images of fewer pixels than the step) the general loop runs.
+struct PixStep {
+    int q, r, fast;
+    __device__ __forceinline__ PixStep(int step, int Ha, int Wa) {
+        q = step / Wa;
+        r = step - q * Wa;
+        fast = q + 1 <= Ha;
+    }
+    __device__ __forceinline__ void advance(int step, int Ha, int Wa, int& img, int& a, int& b) const {
+        if (fast) {
+            b += r;
+            a += q;
+            if (b >= Wa) { b -= Wa; ++a; }
+            if (a >= Ha) { a -= Ha; ++img; }
+        } else {
+            b += step;
+            while (b >= Wa) {
+                b -= Wa;
+                if (++a == Ha) { a = 0; ++img; }
+            }
+        }
+    }
+};
+
 struct TNParams {
     int M, N, P;
     const void* x;
@@ -317,10 +348,6 @@ extern int g_wgrad_abl;
 extern int g_wgrad_nbias;
 extern int g_wgrad_nt32;
 extern int g_wgrad_fill;
-extern int g_wgrad_fill16;
-extern int g_bn1x1s_fill;
-extern int g_res64_fill;
-extern int g_s1x1_fill;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);

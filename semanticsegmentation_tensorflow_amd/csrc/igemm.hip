@@ -418,6 +418,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
     // ---- A pixel rows: incremental (img, a, b) ----
     int pimg[A_CH], pa[A_CH], pb[A_CH], pp[A_CH];
     const int hw = p.Ha * p.Wa;
+    const PixStep pstep(BKP, p.Ha, p.Wa);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
         const int pix = kt_begin * BKP + tid / A_CPR + A_RPP * i;
@@ -445,11 +446,7 @@ __global__ __launch_bounds__(256) void igemm_tn(TNParams p) {
             ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
             // advance by one k tile
             pp[i] += BKP;
-            pb[i] += BKP;
-            while (pb[i] >= p.Wa) {
-                pb[i] -= p.Wa;
-                if (++pa[i] == p.Ha) { pa[i] = 0; ++pimg[i]; }
-            }
+            pstep.advance(BKP, p.Ha, p.Wa, pimg[i], pa[i], pb[i]);
         }
 #pragma unroll
         for (int i = 0; i < B_CH; ++i) {

@@ -520,6 +520,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
     const int hoff = atj * p.tsh + p.ioh, woff = ati * p.tsw + p.iow;
     int pimg[A_INS], pa[A_INS], pb[A_INS], pp[A_INS];
     const int hw = p.Ha * p.Wa;
+    const PixStep pstep(BKP, p.Ha, p.Wa);
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
         const int pix = kt_begin * BKP + (i * NW) * A_RPI + a_row0;
@@ -548,11 +549,7 @@ __global__ __launch_bounds__(WM* WN * 64) void igemm_tn2(TNParams p, int tiles_m
             const void* src = ok ? (const void*)(X + (long)pimg[i] * p.x_img + ((long)ih * p.IW + iw) * p.ldx + ac) : zero;
             glds16(src, sb_ + (i * NW + w) * 1024);
             pp[i] += BKP;
-            pb[i] += BKP;
-            while (pb[i] >= p.Wa) {
-                pb[i] -= p.Wa;
-                if (++pa[i] == p.Ha) { pa[i] = 0; ++pimg[i]; }
-            }
+            pstep.advance(BKP, p.Ha, p.Wa, pimg[i], pa[i], pb[i]);
         }
 #pragma unroll
         for (int i = 0; i < B_INS; ++i) {

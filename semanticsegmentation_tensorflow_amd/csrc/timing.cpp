@@ -1,5 +1,3 @@
-// Host-side HIP runtime helpers (no kernels).
-//
 // Timing events for per-launch kernel timing (Session.timer, bench.py's
 // roofline): HIP events created with hipEventDisableSystemFence.  A plain
 // timing event (hipEventDefault, torch.cuda.Event(enable_timing=True)) ends
@@ -9,7 +7,6 @@
 // kernel durations of a rocprofv3 trace of the same steps.  Host code (HIP
 // runtime API only, no kernels).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 
 #include "../../include/segkern.h"
 
@@ -36,22 +33,4 @@ extern "C" int seg_timing_event_elapsed_ms(float* ms, void* start, void* end) {
 extern "C" int seg_timing_event_destroy(void* ev) {
     if (!ev) return SEG_OK;
     return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? SEG_OK : SEG_ELAUNCH;
-}
-
-// A stream whose kernels run only on the CUs set in `mask` (nwords 32-bit
-// words, bit i = CU i in the runtime's order): the Session's stream for the
-// fused conv6 / conv7 filter-gradient + Adam launches, so that HBM-bound
-// update cannot hold every CU while the input-gradient chain waits (its
-// 256 x 256 conv tiles need a whole CU's LDS).
-extern "C" int seg_stream_create_cu_mask(void** stream, const unsigned* mask, int nwords) {
-    if (!stream || !mask || nwords <= 0) return SEG_EINVAL;
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask) != hipSuccess) return SEG_ELAUNCH;
-    *stream = (void*)s;
-    return SEG_OK;
-}
-
-extern "C" int seg_stream_destroy(void* stream) {
-    if (!stream) return SEG_OK;
-    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? SEG_OK : SEG_ELAUNCH;
 }

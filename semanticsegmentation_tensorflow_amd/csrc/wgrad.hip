@@ -35,7 +35,6 @@ int g_wgrad_nt = 128;
 int g_wgrad_abl = 0;
 int g_wgrad_nt32 = 1;     // 32-wide dy tiles for N <= 32
 int g_wgrad_fill = 100;   // split-K target: blocks = this percentage of the CUs
-int g_wgrad_fill16 = 100; // ... for <= 32 output channels (FC-DenseNet growth convs: 36 KB outputs, 256 slabs)
 int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
 
 struct WGGeom {
@@ -340,7 +339,7 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     const int nct = p.Cg / 64, nnt = (p.N + wp->nt - 1) / wp->nt;
     const int nout = nct * nnt;
     const int ptiles = nimg * wp->g[0] * wp->g[1];
-    const int tcus = std::max(1, cus * (p.N <= 32 ? g_wgrad_fill16 : g_wgrad_fill) / 100);
+    const int tcus = std::max(1, cus * g_wgrad_fill / 100);
     int splits = std::max(1, std::min(ptiles, (tcus + nout - 1) / nout));
     const int tps = (ptiles + splits - 1) / splits;
     splits = (ptiles + tps - 1) / tps;

@@ -99,23 +99,6 @@ class TimingEvent:
             self._h = None
 
 
-def cu_masked_stream(device, pct, contiguous=False):
-    """A torch.cuda.ExternalStream whose kernels run on `pct` % of the
-    device's CUs (seg_stream_create_cu_mask): evenly spread over the CU
-    indices, or the first ones (contiguous).  The stream is never destroyed
-    (Sessions keep theirs for the process lifetime)."""
-    n = torch.cuda.get_device_properties(device).multi_processor_count
-    keep = [(i * pct) // 100 != ((i + 1) * pct) // 100 for i in range(n)] if not contiguous else \
-        [i < n * pct // 100 for i in range(n)]
-    words = (ctypes.c_uint * ((n + 31) // 32))()
-    for i, k in enumerate(keep):
-        if k:
-            words[i // 32] |= 1 << (i % 32)
-    h = ctypes.c_void_p()
-    check(_lib.lib().seg_stream_create_cu_mask(ctypes.byref(h), words, len(words)), "cu_masked_stream")
-    return torch.cuda.ExternalStream(h.value, device=device)
-
-
 def conv_desc(N, H, W, C, K, R, S, stride=1, dilation=1, padding="SAME", dtype=BF16):
     d = SegConvDesc()
     check(_lib.lib().seg_conv_desc_init(ctypes.byref(d), N, H, W, C, K, R, S, stride, dilation,

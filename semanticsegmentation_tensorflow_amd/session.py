@@ -171,19 +171,6 @@ class Session(PlanMixin, StreamMixin):
         # has no input gradient left to run then, beside the side stream's
         # remaining filter gradients instead of after them
         self.main_wgrad = 2
-        # the fused conv6 / conv7 filter-gradient + Adam launches on a stream
-        # restricted to this percentage of the CUs (0: on the side stream, all
-        # CUs): the HBM-bound update otherwise holds every CU for ~0.9 ms while
-        # the input-gradient chain's 160 KiB-LDS conv tiles wait for one
-        self.fused_cu_pct = 0
-        # data-parallel all-reduce steps: the Adam update of every variable of
-        # >= overlap_big_mb MB (FCN conv6 / conv7) as soon as its buckets'
-        # collectives complete, on the CU-masked stream (fused_cu_pct) or the
-        # side stream, beside the rest of backward (0: all at the end)
-        self.overlap_big_mb = 0
-        self.fused_cu_contig = 0
-        self._fused_stream = None
-        self._fused_used = False
 
         self._side = None
         self._adam_ctx = None
@@ -805,9 +792,6 @@ class Session(PlanMixin, StreamMixin):
                     self._adam_ctx = None
                 if self._red is not None:        # pending filter-gradient reductions done before Adam
                     self._red[1].wait_stream(self._red[0])
-                    if self._fused_used:
-                        self._red[1].wait_stream(self._fused_stream)
-                        self._fused_used = False
                     self._red = None
                 if dpa is not None:
                     if ok:
@@ -1190,12 +1174,6 @@ class Session(PlanMixin, StreamMixin):
                     opt, gs, fdone = self._fused
                     wn = n.w.var_name
                     side = self._wgrad_side(p, n, level=2)
-                    if side is not None and self.fused_cu_pct:
-                        if self._fused_stream is None:
-                            self._fused_stream = ops.cu_masked_stream(self.device, self.fused_cu_pct,
-                                                                      bool(self.fused_cu_contig))
-                        side = self._fused_stream
-                        self._fused_used = True
 
                     def launch_fused(n=n, x=x, dz=dz, wn=wn, fused_db=fused_db, side=side, opt=opt, gs=gs):
                         # on the side stream too: its input gradient (the only reader of the

@@ -35,18 +35,13 @@ class _AdamOverlap:
         # big_only (data-parallel all-reduce steps, Session.overlap_big_mb):
         # only variables of >= overlap_big_mb MB overlap (FCN: conv6, conv7 --
         # the 2.9 GB of Adam traffic the single-process step fuses into their
-        # filter gradients), on the CU-masked stream when fused_cu_pct is set;
-        # finish() updates the rest in one launch on the compute stream
+        # filter gradients); finish() updates the rest in one launch on the
+        # compute stream
         self.big = None
         if big_only:
             st = sess.store
             lim = sess.overlap_big_mb * (1 << 20) / 4
             self.big = {nm for nm in var_set if nm in st.by_name and math.prod(st.by_name[nm].shape) >= lim}
-            if sess.fused_cu_pct:
-                if sess._fused_stream is None:
-                    sess._fused_stream = ops.cu_masked_stream(sess.device, sess.fused_cu_pct,
-                                                              bool(sess.fused_cu_contig))
-                self.side = sess._fused_stream
 
     def _adam(self, names, stream=None):
         st = self.s.store

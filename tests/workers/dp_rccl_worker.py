@@ -38,12 +38,10 @@ CASES = [
     ("sp_bf16_serial", "bf16", None, {"side_wgrad": 0, "main_wgrad": 0, "fused_delay": 0}),
     ("sp_bf16_side1", "bf16", None, {"side_wgrad": 1, "main_wgrad": 1}),
     ("sp_bf16_nofuse", "bf16", None, {"fuse_pool": False, "fuse_grad_sum": False}),
-    ("sp_bf16_fusedcu", "bf16", None, {"fused_cu_pct": 50}),
-    ("sp_bf16_fusedcu_c", "bf16", None, {"fused_cu_pct": 25, "fused_cu_contig": 1, "fused_delay": 0}),
     ("dp_bf16_zero", "bf16", "zero", {}),
     ("dp_bf16_zero_serial", "bf16", "zero", {"side_wgrad": 0, "main_wgrad": 0}),
     ("dp_bf16_allreduce", "bf16", "allreduce", {"side_wgrad": 1}),
-    ("dp_bf16_allreduce_big", "bf16", "allreduce", {"overlap_big_mb": 4, "fused_cu_pct": 50}),
+    ("dp_bf16_allreduce_big", "bf16", "allreduce", {"overlap_big_mb": 4}),
     ("dp_f32_allreduce_big", "f32", "allreduce", {"overlap_big_mb": 1}),
 ]
 
