@@ -171,6 +171,11 @@ class Session(PlanMixin, StreamMixin):
         # has no input gradient left to run then, beside the side stream's
         # remaining filter gradients instead of after them
         self.main_wgrad = 2
+        # data-parallel all-reduce steps: the Adam update of every variable of
+        # >= overlap_big_mb MB (FCN conv6 / conv7) as soon as its buckets'
+        # collectives complete, on the side stream beside the rest of backward
+        # (0: all at the end)
+        self.overlap_big_mb = 0
 
         self._side = None
         self._adam_ctx = None
