@@ -523,9 +523,12 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
             a[1] += s_ev.elapsed_time(e_ev)
         sess.timer = None
         sess.side_wgrad = side_mode
-    # the dominant family: the most algorithmic work per step (its in-step time
-    # decides nothing: two families of similar time would swap between runs)
-    dname, (dn, dflops, dms, dbytes) = max(per.items(), key=lambda kv: kv[1][1])
+    # the dominant family: the most time in the serialized step (each kernel
+    # alone on the chip; in the overlapped step two families of similar time
+    # swap between runs), or in the step itself when no side stream exists
+    rank_by = {k: v for k, v in alone.items() if k in per} or {k: (v[0], v[2]) for k, v in per.items()}
+    dname = max(rank_by.items(), key=lambda kv: kv[1][1])[0]
+    dn, dflops, dms, dbytes = per[dname]
     # the dominant family re-timed in-step with events around ITS launches
     # only (every other launch un-instrumented, as in the timed steps): the
     # figure the line reports, comparable with the kernel durations of the
@@ -565,9 +568,9 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
                 "traffic": None, "launches_per_step": dn, "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
                 "algorithmic_bytes_per_launch": round(dbytes / dn), "avg_launch_ms": round(dms / dn, 4)}
     roof["all_events_avg_launch_ms"] = round(all_ev_ms, 4)
-    roof["timing"] = (f"HIP events on the launch stream around the {dn} launches per step of this family only, "
-                      f"{reps} train steps after the timed ones; all_events_avg_launch_ms: the same with every "
-                      f"conv launch of the step bracketed")
+    roof["timing"] = (f"HIP events (hipEventDisableSystemFence: no cache flush in the interval) on the launch "
+                      f"stream around the {dn} launches per step of this family only, {reps} train steps after the "
+                      f"timed ones; all_events_avg_launch_ms: the same with every conv launch of the step bracketed")
     if dname in alone and alone[dname][1] > 0:
         an, ams = alone[dname]
         if hbm_bound:
