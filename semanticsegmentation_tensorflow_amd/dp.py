@@ -12,7 +12,7 @@ of per-shard means == the global-batch mean for equal shards).
 
 Two exchange modes per step:
 
-* "zero" (ZeRO-1, the default for an Adam step at world > 1): each bucket is
+* "zero" (ZeRO-1, `shard_optimizer=True`; an Adam step at world > 1): each bucket is
   reduce-SCATTERED -- rank r receives the summed slice r of every bucket --
   TF1 Adam runs on those slices only (1/world of the parameters: per-rank
   Adam HBM traffic 28 B/param / world), and the updated fp32 slices are
@@ -20,9 +20,15 @@ Two exchange modes per step:
   rewritten from the full parameters (Session._zero_update).  Wire bytes equal
   an all-reduce's (a reduce-scatter + an all-gather); the m / v slots outside
   a rank's slices are stale until `gather_slots` (checkpoints).
-* "allreduce": every bucket all-reduced, Adam everywhere (the accumulate
-  template's steps, which read the whole gradient, and the overlapped
-  per-layer optimizer).
+* "allreduce" (the default, as in bench.py): every bucket all-reduced, Adam
+  everywhere (also the accumulate template's steps, which read the whole
+  gradient, and the overlapped per-layer optimizer).
+
+ZeRO-1 at world > 1 is UNVERIFIED on hardware: the RCCL test forces the
+collectives at world 1 (a rank's slice is the whole bucket) and the gloo
+world-2 tests stand in an all-reduce for the reduce-scatter; the library
+default stays "allreduce" until an 8-GPU run compares one step's parameters
+and m / v against it.
 
 At world 1 every collective is the identity and none is issued (`active`
 False) -- the Session then runs its single-process plan, fused conv6 / conv7
@@ -36,7 +42,7 @@ import torch.distributed as dist
 
 
 class DataParallel:
-    def __init__(self, bucket_mb: float = 64.0, group=None, shard_optimizer: bool = True,
+    def __init__(self, bucket_mb: float = 64.0, group=None, shard_optimizer: bool = False,
                  force_collectives: bool = False):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed must be initialised (one process per GPU)")
