@@ -276,6 +276,23 @@ void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s)
 void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype);
 
 inline bool nt3_applies(int N, int dtype) { return g_nt3 && (dtype == SEG_BF16 || dtype == SEG_F16) && N > 128; }
+// Split-K count for `tiles` output tiles of a one-block-per-CU kernel: the
+// s <= min(smax, ceil(cus / tiles)) minimising rounds / s, rounds =
+// ceil(tiles * s / cus) (the smaller s on ties).  The plain ceil(cus / tiles)
+// overshoots the CU count by a few blocks for many tile counts (C3's
+// transposed-conv gradients: 20 x 13 = 260, 54 x 5 = 270, 30 x 9 = 270 blocks
+// on 256 CUs), and the second round of 4-14 blocks doubles the launch.
+inline int one_round_splits(long tiles, int cus, int smax) {
+    if (tiles <= 0 || tiles >= cus || smax <= 1) return 1;
+    const int hi = (int)std::min<long>(smax, (cus + tiles - 1) / tiles);
+    int best = 1;
+    double best_t = 1e30;
+    for (int s = 1; s <= hi; ++s) {
+        const double t = (double)((tiles * s + cus - 1) / cus) / s;
+        if (t < best_t * 0.999) { best_t = t; best = s; }
+    }
+    return best;
+}
 void nt3_info(int M, int N, int K, int cus, int* splits);
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype);
 extern int g_tn3;

@@ -318,18 +318,12 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
     }
 }
 
-// 256 x 256 tiles, one block per CU: split K until the grid covers the CUs
-// (keeping >= 6 K tiles per split), never past 64 slabs.
+// 256 x 256 tiles, one block per CU: split K until the grid covers the CUs in
+// one round (keeping >= 6 K tiles per split), never past 64 slabs.
 void nt3_info(int M, int N, int K, int cus, int* splits) {
     const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
     const int kt = (K + 63) / 64;
-    int s = 1;
-    if (tiles < cus) {
-        s = (int)((cus + tiles - 1) / tiles);
-        s = std::min(s, std::max(1, kt / 6));
-        s = std::min(s, 64);
-    }
-    *splits = s;
+    *splits = one_round_splits(tiles, cus, std::min(64, std::max(1, kt / 6)));
 }
 
 bool nt3_ok(const NTParams& p, int dtype) {
@@ -850,13 +844,7 @@ bool tn3_ok(const TNParams& p, int dtype) { return tn3_applies(p.M, p.N, dtype);
 void tn3_info(int M, int N, int P, int cus, int* splits) {
     const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
     const int kt = (P + 63) / 64;
-    int s = 1;
-    if (tiles < cus) {
-        s = (int)((cus + tiles - 1) / tiles);
-        s = std::min(s, std::max(1, kt / 6));
-        s = std::min(s, 64);
-    }
-    *splits = s;
+    *splits = one_round_splits(tiles, cus, std::min(64, std::max(1, kt / 6)));
 }
 
 void launch_tn3(TNParams& p, int splits, hipStream_t s, int dtype) {

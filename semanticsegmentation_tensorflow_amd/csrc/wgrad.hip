@@ -340,7 +340,7 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     const int nout = nct * nnt;
     const int ptiles = nimg * wp->g[0] * wp->g[1];
     const int tcus = std::max(1, cus * g_wgrad_fill / 100);
-    int splits = std::max(1, std::min(ptiles, (tcus + nout - 1) / nout));
+    int splits = std::max(1, std::min(ptiles, one_round_splits(nout, tcus, ptiles)));
     const int tps = (ptiles + splits - 1) / splits;
     splits = (ptiles + tps - 1) / tps;
     wp->g[5] = nct; wp->g[6] = nnt; wp->g[7] = splits; wp->g[8] = tps; wp->g[9] = ptiles;

@@ -403,6 +403,24 @@ def test_bias_relu_bwd(dev, dtype, K):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("K,P,kv", [(4096, 4 * 12 * 39, 4096), (512, 1000, 500), (1024, 7, 1024), (256, 333, 256)])
+def test_bias_grad_wide_colsum(dev, dtype, K, P, kv):
+    """BiasAddGrad alone (no ReLU, dz = dy) of a wide dy: col_sum_k + reduce_rows_k
+    (C2's conv6 / conv7 bias gradients, P = 4 x 12 x 39), ragged row ranges,
+    fewer rows than row lanes, and a partial last chunk group (K = 4096 / 8 = 512
+    chunks = 8 groups; fp32: 1024 chunks)."""
+    g = torch.Generator().manual_seed(21)
+    dy = rnd(torch.randn(1, 1, P, K, generator=g, dtype=torch.float64), dtype)
+    dyd = to_dev(dy, dtype, dev)
+    dbd = torch.full((kv,), 7.0, dtype=torch.float32, device=dev)
+    ops.bias_relu_bwd(dyd, None, dyd, dbd, kv, relu=False)
+    torch.cuda.synchronize()
+    assert torch.equal(from_dev(dyd), dy)          # dy untouched
+    db = dy[..., :kv].sum(dim=(0, 1, 2))
+    assert_close(dbd.double().cpu(), db, torch.float32, "dbias", 1e-5)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("labels_kind", ["index", "onehot"])
 def test_softmax_xent(dev, dtype, labels_kind):
     N, H, W, C = 2, 12, 16, 2
