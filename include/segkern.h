@@ -115,6 +115,23 @@ int seg_conv2d_fwd_pool(const seg_conv_desc* d, const void* x, const void* w_krs
                         void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropInput.  w_hwio: packed filter [R][S][C][K] in `dtype`
  * (seg_pack_filter mode 1).  dx may be a channel-slice view (ldx). */
+/* Conv2DBackpropInput + MaxPoolGrad in one launch, for the conv that
+ * consumes a 2x2 / 2 MaxPool's output (Network/model/FCN.py:63-69 conv2_1 /
+ * conv3_1 after pool1 / pool2, with :158-160): the pooled input gradient is
+ * never written; dx_full [N][2H][2W] (row stride ld_full, H x W = d's input)
+ * gets it routed by idx (seg_maxpool2x2_fwd_argmax switches, row stride
+ * ld_idx bytes; zero where relu != 0 and the switch's bit 2 is clear: the
+ * ReluGrad of the post-ReLU pool input) and zeros at the other three window
+ * elements -- bit for bit seg_conv2d_bwd_data + seg_maxpool2x2_bwd_argmax.
+ * epi: NULL, or a residual only (the pooled gradient of the pool's other
+ * consumers, added before routing).  16-bit dtypes, stride 1, a launch whose
+ * kernel has the epilogue: seg_conv2d_bwd_data_unpool_ok(d) == 1, SEG_EINVAL
+ * otherwise.  Replaces the pair nn_ops MaxPoolGrad + Conv2DBackpropInput of
+ * tf.train.AdamOptimizer.minimize (Network/model/FCN.py:338-340). */
+int seg_conv2d_bwd_data_unpool_ok(const seg_conv_desc* d);
+int seg_conv2d_bwd_data_unpool(const seg_conv_desc* d, const void* dy, const void* w_hwio,
+                               const seg_epilogue* epi, const void* idx, int ld_idx, int relu,
+                               void* dx_full, int ld_full, void* ws, size_t ws_bytes, void* stream);
 /* A-operand prologue: the conv reads relu(x * gamma / sqrt(1 + eps) + beta)
  * in place of x (frozen-statistics tf.layers.batch_normalization + ReLU
  * feeding the conv, Network/model/FCDenseNet.py:25-28 and :39-41,

@@ -764,6 +764,40 @@ extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Conv2DBackpropInput + MaxPoolGrad (+ the ReluGrad of the pool's post-ReLU
+// input) in one launch: the MaxPoolGrad epilogue of the halo kernels
+// (EpiParams::unpool_y), no split-K.
+extern "C" int seg_conv2d_bwd_data_unpool_ok(const seg_conv_desc* d) {
+    if (!d || check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return 0;
+    if (d->stride_h != 1 || d->stride_w != 1 || (d->C & 7) || (d->ldx & 7)) return 0;
+    return seg::nt_unpool_ok(conv_bwd_data_params(d), d->dtype) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_bwd_data_unpool(const seg_conv_desc* d, const void* dy, const void* w,
+                                          const seg_epilogue* epi, const void* idx, int ld_idx, int relu,
+                                          void* dx_full, int ld_full, void* ws, size_t ws_bytes, void* stream) {
+    if (!d || !dy || !w || !idx || !dx_full || ld_full < d->C || (ld_full & 7) || ld_idx < d->C || (ld_idx & 7))
+        return SEG_EINVAL;
+    if (((uintptr_t)dx_full & 15) || ((uintptr_t)idx & 7)) return SEG_EALIGN;
+    if (!seg_conv2d_bwd_data_unpool_ok(d)) return SEG_EINVAL;
+    if (epi && (epi->bias || epi->scale || epi->shift || epi->relu || epi->relu_mask ||
+                (epi->keep_prob > 0.f && epi->keep_prob < 1.f)))
+        return SEG_EINVAL;
+    NTParams p = conv_bwd_data_params(d);
+    p.x = dy; p.w = w; p.y = nullptr;
+    if (epi && epi->residual) {     // the pooled gradient of the pool's other consumers, added first
+        const int ldr = epi->ld_residual ? epi->ld_residual : d->ldx;
+        p.epi = make_epi(epi, d->C, (long)d->H * d->W * ldr, (long)d->H * d->W, d->ldx);
+        p.epi.ld_res = ldr;
+    }
+    p.epi.unpool_y = dx_full;
+    p.epi.unpool_idx = reinterpret_cast<const unsigned char*>(idx);
+    p.epi.ld_unpool = ld_full;
+    p.epi.ld_uidx = ld_idx;
+    p.epi.unpool_relu = relu != 0;
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
 // Conv2DBackpropInput of a 1x1 conv whose input is relu(BN(x)) with the BN
 // folded into its operand prologue, continued through the BatchNorm(+ReLU)
 // backward in the GEMM epilogue: dx = dL/dx of the BN input (optionally

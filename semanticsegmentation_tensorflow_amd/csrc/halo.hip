@@ -397,7 +397,10 @@ __global__ __launch_bounds__(512) void conv_halo(NTParams p, HaloGeom g) {
 // FCN (C = 64 / 128: one or two chunks per tile, 1872 tiles) conv_halo left
 // each block ~80 % of its time waiting on a single in-order pipeline.
 // No split-K (the host uses it only for splits == 1).
-template <int BW, int HI, int BN, typename T = bf16>
+// UNP: the MaxPoolGrad epilogue (EpiParams::unpool_y), no ReluGrad mask /
+// dropout paths (its own instantiation: the 128-VGPR budget of two blocks
+// per CU has no room for both).
+template <int BW, int HI, int BN, typename T = bf16, bool UNP = false>
 __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) {
     constexpr int NW = 8, WM = 4, WN = 2, BM = 256, BH = BM / BW;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
         uint4 mkv[NRH];          // ReluGrad mask rows of this half, requested before the staging
-        if (e.mask) {
+        if (!UNP && e.mask) {
 #pragma unroll
             for (int k = 0; k < NRH; ++k) {
                 const int ml = wm * WTM + hh * HR + rsub + k * RPP;
@@ -572,7 +575,7 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                         acc[hh * (TM / 2) + mi][ni][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (BW == 16 && HR == 32 && CPR == 8) {
-            if (e.pool_y) {              // MaxPool fused (bias + ReLU only: no scale / shift here)
+            if (!UNP && e.pool_y) {      // MaxPool fused (bias + ReLU only: no scale / shift here)
                 const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
                 const float nil[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 pool_epi_rows<T, BW, HR>(p, wbuf + cch * 32, SROW, wm * WTM + hh * HR, oy0, ox0, img, col0, lane,
@@ -590,13 +593,13 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
             float v[8];
             splitk_lds8(wbuf + rr * SROW + cch * 32, v);
             float res[8], mk[8];
-            if (e.mask) Chunk<T>::unpack(mkv[k], mk);
+            if (!UNP && e.mask) Chunk<T>::unpack(mkv[k], mk);
             if (e.residual) {
                 const T* rp = reinterpret_cast<const T*>(e.residual) + img * e.res_img + pix * e.ld_res + col0;
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             }
             const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
-            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
+            const SegDropRun<8> drop(e.seed, gidx + col0, !UNP && e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
@@ -604,10 +607,14 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
                 const float sc = (e.scale && cv) ? e.scale[col] : 1.f, sh = (e.shift && cv) ? e.shift[col] : 0.f;
                 float x = v[j] * sc + sh + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
+                if (!UNP && e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (e.residual) x += res[j];
-                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                if (!UNP && e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
+            }
+            if constexpr (UNP) {     // MaxPoolGrad fused: the pooled gradient is not written
+                unpool_store8<T>(e, img, p.OH, p.OW, oy, ox, col0, v);
+                continue;
             }
             T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
             *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(512, 4) void conv_halo_duo(NTParams p, HaloGeom g) 
 // address (L1/L2-hot).  Measured (conv4_2 fwd, 4 x 48 x 156 x 512): 116 us;
 // no DMA 99, zero page 97, hot slice 108, no filter DMA 100 -- the filter
 // stream's L2 round trips, not the DMA instructions, cost the difference.
-template <int BW, int ABL = 0, typename T = bf16>
+template <int BW, int ABL = 0, typename T = bf16, bool UNP = false>
 __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
     constexpr int NW = 8, BM = 256, BN = 256, BH = BM / BW, HI = 6;
     constexpr int WTN = BN / 4, NFH = WTN / 32;   // per-wave columns, n-fragments per B half
@@ -875,7 +882,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             mkv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(e.mask) + img * e.mask_img +
                                                      halo_opix(p, oy, ox) * e.ld_mask + col0);
     };
-    if (e.mask) {
+    if (!UNP && e.mask) {
 #pragma unroll
         for (int k = 0; k < NRR; ++k) load_mask(0, k);
     }
@@ -894,7 +901,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (CPR == 8) {
-            if (e.pool_y) {              // MaxPool fused: pooled map + switches only
+            if (!UNP && e.pool_y) {      // MaxPool fused: pooled map + switches only
                 pool_epi_rows<T, BW, 64>(p, wbuf + cch * 32, SROW, wm * 128 + mh * 64, oy0, ox0, img, col0, lane,
                                          bias, scl, shf);
                 continue;
@@ -906,7 +913,7 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
             const int ml = wm * 128 + mh * 64 + rr;
             const int oy = oy0 + ml / BW, ox = ox0 + ml % BW;
             float mk[8];
-            if (e.mask) {
+            if (!UNP && e.mask) {
                 Chunk<T>::unpack(mkv[k], mk);
                 if (mh == 0) load_mask(1, k);
             }
@@ -920,16 +927,20 @@ __global__ __launch_bounds__(512) void conv_halo2(NTParams p, HaloGeom g) {
                 Chunk<T>::unpack(*reinterpret_cast<const uint4*>(rp), res);
             }
             const uint64_t gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * e.n_valid;
-            const SegDropRun<8> drop(e.seed, gidx + col0, e.keep_prob < 1.f);
+            const SegDropRun<8> drop(e.seed, gidx + col0, !UNP && e.keep_prob < 1.f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int col = col0 + j;
                 float x = v[j] * scl[j] + shf[j] + bias[j];
                 if (e.relu) x = fmaxf(x, 0.f);
-                if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
+                if (!UNP && e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                 if (e.residual) x += res[j];
-                if (e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
+                if (!UNP && e.mask) x = mk[j] > 0.f ? x * e.mask_scale : 0.f;
                 v[j] = col < e.n_valid ? x : 0.f;
+            }
+            if constexpr (UNP) {     // MaxPoolGrad fused: the pooled gradient is not written
+                unpool_store8<T>(e, img, p.OH, p.OW, oy, ox, col0, v);
+                continue;
             }
             T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
             *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
@@ -1937,6 +1948,15 @@ static void launch_halo_t(NTParams& p, const HaloGeom& g, long tiles, int gridz,
 
 template <int BW, int HI, int BN>
 static void launch_halo_duo_t(NTParams& p, const HaloGeom& g, long tiles, hipStream_t s, int dtype) {
+    if constexpr (BW == 16 && HI == 6) {
+        if (p.epi.unpool_y) {     // MaxPoolGrad epilogue (halo_unpools)
+            if (dtype == SEG_F16)
+                hipLaunchKernelGGL((conv_halo_duo<BW, HI, BN, f16, true>), dim3((unsigned)tiles), dim3(512), 0, s, p, g);
+            else
+                hipLaunchKernelGGL((conv_halo_duo<BW, HI, BN, bf16, true>), dim3((unsigned)tiles), dim3(512), 0, s, p, g);
+            return;
+        }
+    }
     if (dtype == SEG_F16)
         hipLaunchKernelGGL((conv_halo_duo<BW, HI, BN, f16>), dim3((unsigned)tiles), dim3(512), 0, s, p, g);
     else
@@ -1970,6 +1990,14 @@ int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype) {
 // The kernel has the fused MaxPool epilogue for this plan: conv_halo2 (16- and
 // 32-px tile rows, 64-column wave tiles), conv_halo_duo<16, 6, 128> (32-row
 // staging halves, 8 column chunks per row) -- never with split-K slabs.
+// The kernel has the MaxPoolGrad epilogue (EpiParams::unpool_y) for this
+// plan: conv_halo2 with 16-px tile rows, conv_halo_duo<16, 6, *> -- never
+// with split-K slabs.
+bool halo_unpools(const HaloPlan& hp, int kernel) {
+    if (hp.splits != 1 || hp.bw != 16) return false;
+    return kernel == HALO_K2 || (kernel == HALO_KDUO && hp.hi == 6);
+}
+
 bool halo_pools(const HaloPlan& hp, int kernel) {
     if (hp.splits != 1) return false;
     if (kernel == HALO_K2) return true;
@@ -2064,6 +2092,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
 // refused here, at the kernel choice itself.
 int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype) {
     if (p.epi.pool_y && !halo_pools(hp, kernel)) return SEG_EINVAL;
+    if (p.epi.unpool_y && !halo_unpools(hp, kernel)) return SEG_EINVAL;
     if (hp.splits > 1 && !p.partial) return SEG_EINVAL;
     HaloGeom g;
     g.taps_h = hp.geom[0]; g.tiles_x = hp.geom[1]; g.tiles_y = hp.geom[2]; g.nimg = hp.geom[3];
@@ -2085,6 +2114,11 @@ int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int 
             }
         }
 #endif
+        if (p.epi.unpool_y) {
+            if (dtype == SEG_F16) hipLaunchKernelGGL((conv_halo2<16, 0, f16, true>), grid, dim3(512), 0, s, p, g);
+            else hipLaunchKernelGGL((conv_halo2<16, 0, bf16, true>), grid, dim3(512), 0, s, p, g);
+            return SEG_OK;
+        }
         if (dtype == SEG_F16) {
             if (hp.bw == 16) hipLaunchKernelGGL((conv_halo2<16, 0, f16>), grid, dim3(512), 0, s, p, g);
             else hipLaunchKernelGGL((conv_halo2<32, 0, f16>), grid, dim3(512), 0, s, p, g);

@@ -56,7 +56,52 @@ struct EpiParams {
     float bn2_inv;
     int bn2_relu;
     int bn2_cv;
+    // MaxPoolGrad of the 2x2 / 2 MaxPool whose output this input gradient is
+    // (conv_halo / conv_halo_duo / conv_halo2, no split-K): the pooled
+    // gradient is not written; each value, rounded to the storage type, goes
+    // to the window element unpool_idx selects (seg_maxpool2x2_fwd_argmax's
+    // switches, row stride ld_uidx bytes; 0 with unpool_relu and bit 2 clear:
+    // the ReluGrad of the post-ReLU pool input), zeros to the other three, in
+    // unpool_y [img][2 OH][2 OW][ld_unpool] -- bit for bit the unfused
+    // output + seg_maxpool2x2_bwd_argmax.  Output dims (OH, OW) pooled, unit
+    // output stride (checked by the host).
+    void* unpool_y;
+    const unsigned char* unpool_idx;
+    int ld_unpool, ld_uidx, unpool_relu;
 };
+
+// The MaxPoolGrad store of EpiParams::unpool_y for the 8 channels col0.. of
+// pooled pixel (oy, ox) of image img, v = the epilogue's fp32 values.
+template <typename T>
+__device__ __forceinline__ void unpool_store8(const EpiParams& e, long img, int OH, int OW, int oy, int ox, int col0,
+                                              const float* v) {
+    static_assert(sizeof(T) == 2, "8 channels per 16-byte chunk");
+    const long pp = (img * OH + oy) * (long)OW + ox;
+    const unsigned long long code = *reinterpret_cast<const unsigned long long*>(e.unpool_idx + pp * e.ld_uidx + col0);
+    // the values rounded as the unfused output store rounds them, then routed
+    // as 16-bit halves of the packed words (few live registers: the halo
+    // kernels run at 128 VGPRs)
+    const uint4 g = Chunk<T>::pack(v);
+    const unsigned gw[4] = {g.x, g.y, g.z, g.w};
+    unsigned live = 0;             // bit j: channel j passes the ReluGrad
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (!e.unpool_relu || ((code >> (8 * j + 2)) & 1ull)) live |= 1u << j;
+    const long UW = 2L * OW;
+    T* b = reinterpret_cast<T*>(e.unpool_y) + ((img * 2 * OH + 2 * oy) * UW + 2 * ox) * e.ld_unpool + col0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        unsigned o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool k0 = (live >> (2 * i) & 1u) && ((code >> (16 * i)) & 3ull) == (unsigned long long)q;
+            const bool k1 = (live >> (2 * i + 1) & 1u) && ((code >> (16 * i + 8)) & 3ull) == (unsigned long long)q;
+            o[i] = (k0 ? (gw[i] & 0xffffu) : 0u) | (k1 ? (gw[i] & 0xffff0000u) : 0u);
+        }
+        T* dst = b + ((q >> 1) * UW + (q & 1)) * e.ld_unpool;
+        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
 
 // dgamma / dbeta from per-tile partial rows [nrows][2C] (eltwise.hip);
 // scratch: bn_grad_finish_scratch(C) bytes
@@ -187,6 +232,7 @@ struct TNParams {
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
 bool nt_pool_ok(const NTParams& p, int dtype);   // launch_nt's kernel fuses EpiParams::pool_y
+bool nt_unpool_ok(const NTParams& p, int dtype);
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);
@@ -323,6 +369,7 @@ int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
 enum { HALO_K1 = 0, HALO_KDUO = 1, HALO_K2 = 2 };   // conv_halo, conv_halo_duo, conv_halo2
 int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype);
+bool halo_unpools(const HaloPlan& hp, int kernel);
 bool halo_pools(const HaloPlan& hp, int kernel);
 int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype = SEG_BF16);
 extern int g_res64;

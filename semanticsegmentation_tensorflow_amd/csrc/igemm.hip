@@ -828,6 +828,18 @@ static bool nt_plan_pools(const NTPlan& pl) {
     return false;
 }
 
+// Whether the planned kernel has the fused MaxPoolGrad epilogue (EpiParams
+// unpool_y): halo_unpools (no split-K slabs), unit output stride.
+static bool nt_plan_unpools(const NTPlan& pl, const NTParams& p) {
+    return pl.kind == NTK_HALO && halo_unpools(pl.hp, pl.halo_kernel) && p.osh == 1 && p.osw == 1 && p.ooh == 0 &&
+           p.oow == 0 && !p.phase;
+}
+
+bool nt_unpool_ok(const NTParams& p, int dtype) {
+    if ((dtype != SEG_BF16 && dtype != SEG_F16) || p.pro.gamma || p.phase) return false;
+    return nt_plan_unpools(nt_plan(p, dtype, 1, p.M), p);
+}
+
 // Whether the planned kernel writes EpiParams.y2 (the BN(+ReLU) second
 // output): igemm_nt2 with its operand prologue or without, no split-K.
 static bool nt_plan_bn2(const NTPlan& pl, int dtype) {
@@ -843,7 +855,9 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     // a pooled launch writes no unpooled map (p.y is null): only a kernel with
     // the pooled epilogue and no split-K slabs may run it
     if (p.epi.pool_y && !nt_plan_pools(pl)) return SEG_EINVAL;
-    // likewise a second BN output: only the kernels that write it
+    // likewise the MaxPoolGrad epilogue (p.y unused) and a second BN output:
+    // only the kernels that write them
+    if (p.epi.unpool_y && (nphases != 1 || !nt_plan_unpools(pl, p))) return SEG_EINVAL;
     if (p.epi.y2 && (nphases != 1 || !nt_plan_bn2(pl, dt_traits<T>::id))) return SEG_EINVAL;
     int splits = pl.splits;
     p.partial = nullptr;

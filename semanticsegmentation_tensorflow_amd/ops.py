@@ -336,6 +336,30 @@ def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None, epi=None):
     return dx
 
 
+def conv2d_bwd_data_unpool_ok(desc):
+    """Whether seg_conv2d_bwd_data_unpool (Conv2DBackpropInput + MaxPoolGrad in
+    one launch) takes this convolution."""
+    return bool(_lib.lib().seg_conv2d_bwd_data_unpool_ok(ctypes.byref(desc)))
+
+
+def conv2d_bwd_data_unpool(desc, dy, w_hwio, idx, dx_full, relu_mask=False, residual=None, ws=None, stream=None):
+    """Conv2DBackpropInput of the conv after a 2x2 / 2 MaxPool, continued
+    through the MaxPoolGrad: dx_full [N, 2H, 2W, C] gets the input gradient
+    routed by the pool's switches idx (row stride = dx_full's channel count;
+    with relu_mask, ReluGrad of the post-ReLU pool input), the pooled gradient
+    is never written.  residual: the pooled gradient of the pool's other
+    consumers [N, H, W, C], added before routing."""
+    d = _with_ld(desc, residual, dy)
+    epi = None if residual is None else epilogue(residual=residual)
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_BWD_DATA))
+    check(_lib.lib().seg_conv2d_bwd_data_unpool(ctypes.byref(d), ptr(dy), ptr(w_hwio),
+                                                None if epi is None else ctypes.byref(epi), ptr(idx),
+                                                dx_full.shape[3], 1 if relu_mask else 0, ptr(dx_full),
+                                                pixel_stride(dx_full), wsp, wss, stream_ptr(stream)),
+          "conv2d_backprop_input_maxpool_grad")
+    return dx_full
+
+
 def conv2d_bwd_filter(desc, x, dy, dw, ws=None, stream=None, dbias=None):
     """Conv2DBackpropFilter (+ BiasAddGrad of dy into dbias when given)."""
     d = _with_ld(desc, x, dy)

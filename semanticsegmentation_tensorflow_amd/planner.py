@@ -373,6 +373,43 @@ class PlanMixin:
             p.buf[id(y)] = None                # never written
         p.pool_fused = {id(m) for m in p.pool_fuse.values()}
 
+    def _plan_unpool_fusion(self, p, consumers):
+        """max_pool -> conv_layer (Network/model/FCN.py:57-63, :63-69): the
+        MaxPoolGrad (+ the ReluGrad of the post-ReLU pool input) runs in the
+        epilogue of the input gradient of the pool output's first consumer in
+        forward order -- the last contribution in backward, so the pooled
+        gradient of any other consumer (FCN's score_pool3 / 4) is complete
+        and comes in as the epilogue residual (ops.conv2d_bwd_data_unpool).
+        The pooled gradient is never written and the MaxPool node's backward
+        is skipped.  The pool input has no other consumer, even dims and
+        recorded switches.  p.unpool_fuse: conv node id -> MaxPool node."""
+        p.unpool_fuse = {}
+        p.unpool_pools = set()
+        if not self.fuse_unpool or self.cdt == ops.F32:
+            return
+        pos = {id(n): i for i, n in enumerate(p.nodes)}
+        for m in p.nodes:
+            if m.kind != "MaxPool" or id(m) not in p.pool_idx or id(m.output) not in p.needs_grad:
+                continue
+            xf, y = m.inputs[0], m.output
+            if len(consumers.get(id(xf), [])) != 1 or id(xf) in p.alias or id(y) in p.alias:
+                continue
+            cs = consumers.get(id(y), [])
+            if not cs:
+                continue
+            c = min(cs, key=lambda q: pos[id(q)])
+            if c.kind != "conv" or c.inputs[0] is not y or getattr(c, "pro", None) is not None:
+                continue
+            if getattr(c, "residual", None) is y or sum(1 for q in cs if q is c) != 1:
+                continue
+            N, H, W = p.shapes[id(y)][:3]
+            if tuple(p.shapes[id(xf)][:3]) != (N, 2 * H, 2 * W):
+                continue
+            if not ops.conv2d_bwd_data_unpool_ok(c.desc):
+                continue
+            p.unpool_fuse[id(c)] = m
+        p.unpool_pools = {id(m) for m in p.unpool_fuse.values()}
+
     def _plan_bn_outputs(self, p, consumers):
         """Conv -> (its epilogue's dropout) -> BatchNorm(+ReLU): FC-DenseNet's
         bottleneck conv1 -> BN -> ReLU before the growth conv
@@ -444,6 +481,7 @@ class PlanMixin:
             c = cs[0]
             if c.kind in ("conv", "tconv") or (c.kind == "MaxPool" and n.kp is None):
                 p.mask_fuse.add(id(n))
+        self._plan_unpool_fusion(p, consumers)
         p.adam_fusable = set()
         p.wg_ws = {}                     # per-conv filter-gradient workspace (pending split-K slabs)
         for n in p.nodes:

@@ -150,6 +150,9 @@ class Session(PlanMixin, StreamMixin):
         self.fuse_bn_bwd = True         # folded BN: its backward in the consuming 1x1 conv's dgrad epilogue
         # conv (+bias +ReLU) -> 2x2 MaxPool as one launch (pooled epilogue)
         self.fuse_pool = True
+        # 2x2 MaxPool -> conv: the MaxPoolGrad in the conv's input-gradient
+        # epilogue (the pooled gradient never written)
+        self.fuse_unpool = True
         # conv -> BatchNorm(+ReLU): the BN output written by the conv epilogue
         self.fuse_bn_out = True
         # the dgamma / dbeta sums of the BN backwards fused into input-gradient
@@ -1039,6 +1042,7 @@ class Session(PlanMixin, StreamMixin):
                     self._bias_relu_bwd(dy, yb if n.relu else None, dz, db, K, n.relu, scale)
                 dx = None
                 dx_base = None
+                unpool = None       # tests: (full-res gradient, switches, relu) of a fused MaxPoolGrad
                 bnb = None          # tests: record of a BatchNorm backward run in this conv's dgrad epilogue
                 pro = getattr(n, "pro", None)
                 if (id(x) in ng and pro is not None and self.fuse_bn_bwd and id(pro.inputs[0]) in ng
@@ -1105,6 +1109,24 @@ class Session(PlanMixin, StreamMixin):
                     done(dxb, acc)
                     if bn_defer is None:
                         self._grad_ready([gn, bn_])
+                elif id(n) in p.unpool_fuse:
+                    # input gradient continued through the MaxPoolGrad of the pool
+                    # before this conv (and its input's ReluGrad): written at the
+                    # pool input's resolution; the pooled gradient of the pool's
+                    # other consumers (done earlier in backward) is the residual
+                    m = p.unpool_fuse[id(n)]
+                    xf = m.inputs[0]
+                    dxf, accf = dest(xf)
+                    prod = p.producer.get(id(xf))
+                    res = grad.get(id(x))
+                    if res is not None and self.capture is not None:
+                        dx_base = res.clone()
+                    self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_unpool, n.desc, dz,
+                                store.packed[(n.w.var_name, ops.PACK_HWIO)][0], p.pool_idx[id(m)], dxf,
+                                prod is not None and id(prod) in p.mask_fuse, res, ws)
+                    if self.capture is not None:
+                        unpool = (dxf.clone(), p.pool_idx[id(m)], prod is not None and id(prod) in p.mask_fuse)
+                    done(dxf, accf)
                 elif id(x) in ng and id(x) in p.alias:
                     # the input is an aliased concat root (FC-DenseNet decoder
                     # concat views): the input gradient lands in the shared
@@ -1152,6 +1174,7 @@ class Session(PlanMixin, StreamMixin):
                                                   if id(n) in p.pool_fuse else None),
                                          # a copy: later consumers may accumulate into the buffer
                                          "dx": None if dx is None else dx.clone(), "dx_base": dx_base,
+                                         "unpool": unpool,
                                          "dx_masked": mask is not None,
                                          "mask_scale": (mask.mask_scale if mask is not None else 1.0),
                                          "relu": n.relu, "keep_prob": n.kp_val, "seed": n.seed_val,
@@ -1254,6 +1277,8 @@ class Session(PlanMixin, StreamMixin):
                 self._grad_ready([n.w.var_name] + ([n.bias.var_name] if n.bias is not None else []))
             elif k == "MaxPool":
                 x = n.inputs[0]
+                if id(n) in p.unpool_pools:
+                    continue          # done in the consuming conv's input-gradient epilogue
                 if id(x) in ng:
                     dx, acc = dest(x)
                     prod = p.producer.get(id(x))

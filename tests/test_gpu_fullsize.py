@@ -210,6 +210,23 @@ def _layer_local(rec, w, b, sess, weights=None, rtol=4e-3, quant=bf16r, images=N
             res["dgrad"] = (dxd - want).abs() - (rtol * want.abs() + 1e-3 * dx.abs().max())
         else:
             res["dgrad"] = (dxd - dx).abs() - (rtol * dx.abs() + 1e-3 * dx.abs().max())
+    if dgrad and rec.get("unpool") is not None:
+        # input gradient continued through the MaxPoolGrad of the pool before
+        # this conv (ops.conv2d_bwd_data_unpool): the oracle's pooled dgrad
+        # (+ the other consumers' pooled sum) routed by the device's switches
+        full_d, idx, relu = rec["unpool"]
+        dx = xg.grad
+        if rec.get("dx_base") is not None:
+            dx = dx + _host(rec["dx_base"], C)
+        Nf, Hf, Wf, Cf = full_d.shape
+        code = idx.view(Nf, Hf // 2, Wf // 2, Cf)[..., :C].long().cpu()
+        g = dx * ((code >> 2) & 1) if relu else dx
+        pos = code & 3
+        want = torch.zeros(Nf, Hf, Wf, C, dtype=g.dtype)
+        for q in range(4):
+            want[:, q // 2::2, q % 2::2] = torch.where(pos == q, g, torch.zeros_like(g))
+        got = _host(full_d, C)
+        res["dgrad_unpool"] = (got - want).abs() - (rtol * want.abs() + 1e-3 * dx.abs().max())
     bb = rec.get("bn_bwd")
     if dgrad and bb is not None:
         res.update(_bn_bwd_local(bb, xg.grad, sess, weights, rtol))
@@ -313,6 +330,9 @@ def test_c2_kernel_set_is_the_benchmarked_one(c2):
     # (pooled epilogue); conv5_3 splits K and keeps the separate pool
     assert {n for n, r in recs.items() if r["pool"] is not None} == {
         "conv1_2/weights", "conv2_2/weights", "conv3_3/weights", "conv4_4/weights"}
+    # pool1 / pool2's MaxPoolGrad inside conv2_1 / conv3_1's input-gradient
+    # launches; conv4_1 / conv5_1 split K and keep the separate MaxPoolGrad
+    assert {n for n, r in recs.items() if r["unpool"] is not None} == {"conv2_1/weights", "conv3_1/weights"}
 
 
 def test_c2_layer_local_parity(c2):

@@ -8,7 +8,8 @@ kernel-trace CSV of a bench run (`rocprofv3 --kernel-trace --stats
 Steps are delimited by the train step's input preparation kernel
 (prepare_input_k, the first launch of every Session.run with a feed): the
 W warm-up steps come first, then the K timed steps (bench.measure), so the
-timed region is [start of the W-th prepare_input, start of the (W+K)-th).
+timed region is steps W .. W+K-1, each from its prepare_input to its last
+adam_pack launch (--end-marker).
 Prints (and with --out writes) rocprof-style per-kernel rows -- name, calls,
 total / average / min / max ns -- for that region, and, with --family (a
 bench.kernel_symbol pattern), the family's calls per step, average launch
@@ -32,6 +33,7 @@ def main():
     ap.add_argument("--gbytes", type=float, default=None, help="algorithmic GB per launch of the family (HBM bound)")
     ap.add_argument("--peak", type=float, default=2500.0, help="TFLOP/s (or GB/s with --gbytes)")
     ap.add_argument("--marker", default="prepare_input")
+    ap.add_argument("--end-marker", default="adam_pack", help="last kernel of a train step")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
@@ -39,8 +41,13 @@ def main():
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     if len(marks) < a.warmup + a.steps + 1:
         sys.exit(f"{len(marks)} '{a.marker}' launches: fewer than warmup + steps + 1")
-    lo, hi = marks[a.warmup], marks[a.warmup + a.steps]
-    seg = rows[lo:hi]
+    # each step: its input preparation .. its last Adam launch (the loss fetch
+    # bench.py runs after the timed steps is not part of the last one)
+    seg = []
+    for j in range(a.warmup, a.warmup + a.steps):
+        part = rows[marks[j]:marks[j + 1]]
+        last = max((i for i, r in enumerate(part) if a.end_marker in r["Kernel_Name"]), default=len(part) - 1)
+        seg += part[:last + 1]
     t0 = int(seg[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in seg)
     agg = collections.OrderedDict()
