@@ -100,6 +100,16 @@ int seg_tconv_desc_init(seg_conv_desc* d, int N, int H, int W, int C, int OH, in
 /* w_krsc: packed filter [K][R][S][C] in `dtype` (seg_pack_filter mode 0). */
 int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w_krsc,
                    const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
+/* Conv2D from the HWIO filter copy w_hwio [R][S][C][K] (seg_pack_filter mode
+ * 1, the copy seg_conv2d_bwd_data reads): same results as seg_conv2d_fwd on
+ * the KRSC copy, so a weight needs one packed copy (FCN conv6 / conv7,
+ * Network/model/FCN.py:78-83: the fused filter-gradient + Adam launch then
+ * writes no KRSC copy).  16-bit dtypes, C a multiple of 64, and a conv
+ * whose launch runs igemm_nt3 whole: seg_conv2d_fwd_hwio_ok(d) == 1,
+ * SEG_EINVAL otherwise. */
+int seg_conv2d_fwd_hwio_ok(const seg_conv_desc* d);
+int seg_conv2d_fwd_hwio(const seg_conv_desc* d, const void* x, const void* w_hwio,
+                        const seg_epilogue* epi, void* y, void* ws, size_t ws_bytes, void* stream);
 /* Conv2D + bias + ReLU + MaxPool(2x2, stride 2) in one launch: conv_layer
  * followed by max_pool (Network/model/FCN.py:56-57, :63, :69, :75, :81 with
  * :158-160).  The conv output is never written: y_pool gets the pooled map

@@ -142,6 +142,8 @@ SIGNATURES = {
     "seg_conv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "seg_tconv_desc_init": (_I, [_DP, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "seg_conv2d_fwd": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_fwd_hwio_ok": (_I, [_DP]),
+    "seg_conv2d_fwd_hwio": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
     "seg_conv2d_fwd_pool_ok": (_I, [_DP]),
     "seg_conv2d_fwd_pool": (_I, [_DP, _P, _P, _EP, _P, _I, _P, _I, _P, _Z, _P]),
     "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),

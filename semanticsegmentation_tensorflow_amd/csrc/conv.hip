@@ -602,6 +602,34 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Conv2D reading the HWIO filter copy ([R][S][C][K], the one the input
+// gradient reads) on igemm_nt3's B-transposed form: a weight with one packed
+// copy instead of two (seg_conv2d_fwd_hwio_ok).
+static NTParams fwd_hwio_params(const seg_conv_desc* d) {
+    NTParams p = conv_fwd_params(d);
+    p.bt = 1;
+    p.w_col = d->K;                      // [r][s][c][k]: c rows of K (padded) columns
+    p.w_tap = (long)d->C * d->K;
+    return p;
+}
+
+extern "C" int seg_conv2d_fwd_hwio_ok(const seg_conv_desc* d) {
+    if (!d || check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return 0;
+    return seg::nt_fwd_bt_ok(fwd_hwio_params(d), d->dtype) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_fwd_hwio(const seg_conv_desc* d, const void* x, const void* w_hwio, const seg_epilogue* epi,
+                                   void* y, void* ws, size_t ws_bytes, void* stream) {
+    int st = check_desc(d);
+    if (st) return st;
+    if (!x || !w_hwio || !y) return SEG_EINVAL;
+    if (!seg_conv2d_fwd_hwio_ok(d)) return SEG_EINVAL;
+    NTParams p = fwd_hwio_params(d);
+    p.x = x; p.w = w_hwio; p.y = y;
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
 // Conv2D + bias + ReLU + MaxPool 2x2 / 2 in one launch: the pooled epilogue of
 // conv_res64 / conv_halo_duo / conv_halo2 (seg_conv2d_fwd_pool_ok).
 static bool fwd_pool_params(const seg_conv_desc* d, const seg_epilogue* epi, NTParams* out) {

@@ -145,6 +145,9 @@ struct NTParams {
     int phase, st_h, st_w, pad_t, pad_l, Nimg;
     ProParams pro;
     int kv;        // valid reduction channels per tap (0: all C; the rest are zero padding)
+    // B given as [k][n] rows (w = tap * w_tap + c * w_col + n: the HWIO copy);
+    // igemm_nt3 only (nt_fwd_bt_ok)
+    int bt;
 };
 
 // C[m][n] = sum_p A[p][m] B[p][n].  p -> (img, a, b) on an Ha x Wa grid;
@@ -232,6 +235,7 @@ struct TNParams {
 
 int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s);
 bool nt_pool_ok(const NTParams& p, int dtype);   // launch_nt's kernel fuses EpiParams::pool_y
+bool nt_fwd_bt_ok(const NTParams& p, int dtype);
 bool nt_unpool_ok(const NTParams& p, int dtype);
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction

@@ -835,6 +835,13 @@ static bool nt_plan_unpools(const NTPlan& pl, const NTParams& p) {
            p.oow == 0 && !p.phase;
 }
 
+// Whether the plan for p runs igemm_nt3 whole (the kernel with the B-transposed
+// form) and the reduction channels tile by 64 (a k tile never crosses a tap).
+bool nt_fwd_bt_ok(const NTParams& p, int dtype) {
+    if ((dtype != SEG_BF16 && dtype != SEG_F16) || p.pro.gamma || p.phase || p.C % 64 || p.kv) return false;
+    return nt_plan(p, dtype, 1, p.M).kind == NTK_NT3;
+}
+
 bool nt_unpool_ok(const NTParams& p, int dtype) {
     if ((dtype != SEG_BF16 && dtype != SEG_F16) || p.pro.gamma || p.phase) return false;
     return nt_plan_unpools(nt_plan(p, dtype, 1, p.M), p);
@@ -858,6 +865,7 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     // likewise the MaxPoolGrad epilogue (p.y unused) and a second BN output:
     // only the kernels that write them
     if (p.epi.unpool_y && (nphases != 1 || !nt_plan_unpools(pl, p))) return SEG_EINVAL;
+    if (p.bt && (nphases != 1 || pl.kind != NTK_NT3 || p.C % 64 || p.kv)) return SEG_EINVAL;
     if (p.epi.y2 && (nphases != 1 || !nt_plan_bn2(pl, dt_traits<T>::id))) return SEG_EINVAL;
     int splits = pl.splits;
     p.partial = nullptr;

@@ -28,7 +28,18 @@ namespace seg {
 int g_nt3 = 1;
 __device__ uint4 g_nt3_zero[4];
 
-template <typename T = bf16>
+// XOR swizzle of the 16-byte chunks of a [k][n] row image (512-byte rows):
+// the column-wise ds_read_b64_tr_b16 fragment reads are conflict-free
+// (igemm_tn3's operands, igemm_nt3's B-transposed form)
+__device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+
+// BT: B given as [k][n] rows (n contiguous: the HWIO filter copy, the one the
+// input gradient reads) instead of [n][k]: staged as 64 x 512-byte k rows like
+// igemm_tn3's operands and read with transposing ds_read_b64_tr_b16, so one
+// packed copy serves the forward and the input gradient (FCN conv6 / conv7:
+// no KRSC copy, no rows_to_tr after their fused Adam).  Needs C % 64 == 0
+// (a k tile never crosses a tap).
+template <typename T = bf16, bool BT = false>
 __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
     constexpr int NW = 8, BM = 256, BN = 256, BK = 64;
     constexpr int WTM = 128, WTN = 64, TN = WTN / 16;   // TM = 8 (two halves of 4)
@@ -110,6 +121,19 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         b_ok[i] = n < p.N;
         b_off[i] = (long)(b_ok[i] ? n : 0) * p.w_col;
     }
+    // BT: lane -> (row of the 2-row DMA piece, physical chunk) -> column bn;
+    // pieces differ by 16 rows, which the swizzle ignores
+    const int rsubb = lane >> 5, pcb = lane & 31;
+    const int rowb0 = w * 2 + rsubb;
+    const int bn_bt = n0 + ((pcb & ~15) | ((pcb & 15) ^ tn3_swz(rowb0))) * 8;
+    const bool bnok_bt = bn_bt < p.N;
+    int bt_cc = 0, bt_ti = 0, bt_tj = 0, bt_kg = kt_begin * BK;
+    if constexpr (BT) {
+        const int tap = bt_kg / p.C;
+        bt_cc = bt_kg - tap * p.C;
+        bt_tj = tap / p.taps_w;
+        bt_ti = tap - bt_tj * p.taps_w;
+    }
     // independent k trackers: A runs two tiles ahead, B one
     struct KState { int kg, cc, ti, tj; };
     auto kinit = [&](int kt) {
@@ -146,6 +170,23 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         kadv(ka);
     };
     auto issue_b = [&](int buf) {
+        if constexpr (BT) {
+            const bool kok = bt_kg < p.K;
+            const long wtap = (long)((rb + p.rstep * bt_tj) * p.Sfull + (sb + p.sstep * bt_ti)) * p.w_tap +
+                              (long)(bt_cc + rowb0) * p.w_col + bn_bt;
+#pragma unroll
+            for (int i = 0; i < B_INS; ++i) {
+                const void* src = (kok && bnok_bt) ? (const void*)(Wt + wtap + (long)(i * NW * 2) * p.w_col) : zero;
+                glds16(src, ldsB + buf * BBUF + (i * NW + w) * 1024);
+            }
+            bt_kg += BK;
+            bt_cc += BK;
+            if (bt_cc >= p.C) {
+                bt_cc -= p.C;
+                if (++bt_ti == p.taps_w) { bt_ti = 0; ++bt_tj; }
+            }
+            return;
+        }
         const bool kok = kb.kg < p.K;
         const long wtap = (long)((rb + p.rstep * kb.tj) * p.Sfull + (sb + p.sstep * kb.ti)) * p.w_tap + kb.cc;
 #pragma unroll
@@ -177,6 +218,18 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
     if (wm == 1) __builtin_amdgcn_s_barrier();
 
     const int fr = lane & 15, fg = lane >> 4;
+    // BT fragment offsets (igemm_tn3's B reads): row fr1 = 8 fg + tq, chunk of
+    // column col0 + ..., the second 4 rows at +4 * 512
+    unsigned boff_bt[TN];
+    if constexpr (BT) {
+        const int tq = (lane & 15) >> 2, tpp = lane & 3;
+        const int fr1 = 8 * fg + tq, fsw = tn3_swz(fr1);
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+            const int chk = ((wn * WTN + ni * 16) >> 3) + (tpp >> 1);
+            boff_bt[ni] = (unsigned)(fr1 * 512 + 16 * ((chk & ~15) | ((chk & 15) ^ fsw)) + 8 * (tpp & 1));
+        }
+    }
     int abuf = 0, bbuf = 0;
     for (int it = 0; it < nk; ++it) {
         const char* As = smem + abuf * ABUF;
@@ -205,13 +258,27 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
         };
         // h0: A half 0 + B slice; B(t+1) into the other B buffer (last read at h0(t-1))
         read_a(0);
+        if constexpr (BT) {
+            typedef short s16x8 __attribute__((ext_vector_type(8)));
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+            for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) {
-                const int row = wn * WTN + ni * 16 + fr;
-                bq[ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
-            }
+                for (int ni = 0; ni < TN; ++ni) {
+                    SEG_LDS char* a = (SEG_LDS char*)Bs + boff_bt[ni] + ks * 32 * 512;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)a);
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SEG_LDS s16x4*)(a + 4 * 512));
+                    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    bq[ks][ni] = __builtin_bit_cast(uint4, v);
+                }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const int row = wn * WTN + ni * 16 + fr;
+                    bq[ks][ni] = *reinterpret_cast<const uint4*>(Bs + row * 128 + 16 * ((ks * 4 + fg) ^ ((row >> 1) & 7)));
+                }
+        }
         if (it + 1 < nk) issue_b(bbuf ^ 1);
         __builtin_amdgcn_s_barrier();
         mma(0);
@@ -333,7 +400,8 @@ bool nt3_ok(const NTParams& p, int dtype) {
 template <typename T>
 static void launch_nt3_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
     const int tiles = ((max_m + 255) / 256) * ((p.N + 255) / 256);
-    hipLaunchKernelGGL((igemm_nt3<T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    if (p.bt) hipLaunchKernelGGL((igemm_nt3<T, true>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((igemm_nt3<T>), dim3(tiles, 1, gridz), dim3(512), 0, s, p);
 }
 
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype) {
@@ -351,7 +419,6 @@ void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype) {
 // igemm_nt3.  Epilogue: fp32 tile staged in LDS, 32-byte row-contiguous
 // stores (filter gradient or split-K slab).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int tn3_swz(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
 
 int g_tn3 = 1;
 int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores

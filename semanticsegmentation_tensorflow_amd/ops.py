@@ -181,6 +181,21 @@ def conv2d_fwd(desc, x, w_krsc, y, epi=None, ws=None, stream=None):
     return y
 
 
+def conv2d_fwd_hwio_ok(desc):
+    """Whether seg_conv2d_fwd_hwio (the forward from the HWIO copy) takes this conv."""
+    return bool(_lib.lib().seg_conv2d_fwd_hwio_ok(ctypes.byref(desc)))
+
+
+def conv2d_fwd_hwio(desc, x, w_hwio, y, epi=None, ws=None, stream=None):
+    """Conv2D (+ epilogue) reading the HWIO filter copy (the input gradient's)."""
+    d = _with_ld(desc, x, y)
+    wsp, wss = (ws or Workspace(x.device)).ptr_size(conv_workspace(d, OP_FWD))
+    check(_lib.lib().seg_conv2d_fwd_hwio(ctypes.byref(d), ptr(x), ptr(w_hwio),
+                                         None if epi is None else ctypes.byref(epi), ptr(y), wsp, wss,
+                                         stream_ptr(stream)), "conv2d_hwio")
+    return y
+
+
 def conv2d_fwd_pool_ok(desc):
     """Whether seg_conv2d_fwd_pool (Conv2D + bias + ReLU + MaxPool 2x2/2 in one
     launch) takes this convolution."""

@@ -295,8 +295,15 @@ class PlanMixin:
                 R, S, _, K = n.w.shape
                 n.desc = ops.conv_desc(N, H, W, C, K, R, S, n.stride, n.dilation, n.padding, self.cdt)
                 ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_FWD))
-                p.packs.add((n.w.var_name, ops.PACK_KRSC))
-                if id(x) in p.needs_grad:
+                # a large filter (FCN conv6 / conv7) keeps ONE packed copy: its
+                # forward reads the HWIO copy the input gradient reads
+                # (ops.conv2d_fwd_hwio), and its fused filter-gradient + Adam
+                # launch has no KRSC copy to rewrite
+                n.fwd_hwio = (self.fwd_hwio and getattr(n, "pro", None) is None and R * S * C * K >= (1 << 23)
+                              and ops.conv2d_fwd_hwio_ok(n.desc))
+                if not n.fwd_hwio:
+                    p.packs.add((n.w.var_name, ops.PACK_KRSC))
+                if id(x) in p.needs_grad or n.fwd_hwio:
                     p.packs.add((n.w.var_name, ops.PACK_HWIO))
                 if p.train:
                     ws_need = max(ws_need, ops.conv_workspace(n.desc, ops.OP_BWD_DATA),
@@ -356,7 +363,8 @@ class PlanMixin:
         if not self.fuse_pool or self.cdt == ops.F32:
             return
         for n in p.nodes:
-            if n.kind != "conv" or getattr(n, "pro", None) is not None or n.kp is not None:
+            if (n.kind != "conv" or getattr(n, "pro", None) is not None or n.kp is not None
+                    or getattr(n, "fwd_hwio", False)):
                 continue
             y = n.output
             cs = consumers.get(id(y), [])
@@ -428,7 +436,8 @@ class PlanMixin:
             if b.kind != "bn" or id(b) in p.folded or id(b.output) in p.fetched:
                 continue
             c = producer.get(id(b.inputs[0]))
-            if c is None or id(c) in p.pool_fuse or id(c) in p.bn_out2 or id(c.output) in p.fetched:
+            if (c is None or id(c) in p.pool_fuse or id(c) in p.bn_out2 or id(c.output) in p.fetched
+                    or getattr(c, "fwd_hwio", False)):
                 continue
             cs = consumers.get(id(c.output), [])
             if len(cs) != 1 or cs[0] is not b.ops[0]:

@@ -117,6 +117,36 @@ def test_conv2d_fwd_bias_relu(dev, ntv, case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", [(4, 12, 39, 512, 4096, 7, 0.8), (4, 12, 39, 4096, 4096, 1, 0.8),
+                                  (2, 6, 10, 512, 520, 7, 1.0), (4, 2, 3, 4096, 4096, 1, 0.5)],
+                         ids=["conv6", "conv7", "conv6-ntail-split64", "conv7-small-split10"])
+def test_conv2d_fwd_hwio_equals_krsc(dev, case, dtype):
+    """igemm_nt3's B-transposed form (ops.conv2d_fwd_hwio: the forward from the
+    HWIO copy the input gradient reads, FCN conv6 / conv7 with their bias +
+    ReLU + dropout epilogue) equals the KRSC forward bit for bit: the same
+    k order into the same MFMAs (full-size conv6 / conv7 of C2, split-K
+    plans, an N tail of 8)."""
+    N, H, W, C, K, R, kp = case
+    cs = (N, H, W, C, K, R, R, 1, 1, "SAME")
+    x, w, b = _conv_case(cs, 3)
+    d = ops.conv_desc(N, H, W, C, K, R, R, 1, 1, "SAME", DT[dtype])
+    assert ops.conv2d_fwd_hwio_ok(d), case
+    assert ops.conv_kernel_info(d, ops.OP_FWD)[0].startswith("igemm_nt3")
+    xd = to_dev(x, dtype, dev)
+    wk = _pack(w, ops.PACK_KRSC, dtype, dev)
+    wh = _pack(w, ops.PACK_HWIO, dtype, dev)
+    bd = b.float().to(dev)
+    epi = ops.epilogue(bias=bd, relu=True, keep_prob=kp, seed=77)
+    ref = torch.full((N, H, W, d.K), float("nan"), dtype=dtype, device=dev)
+    got = torch.full_like(ref, float("nan"))
+    ops.conv2d_fwd(d, xd, wk, ref, epi)
+    ops.conv2d_fwd_hwio(d, xd, wh, got, epi)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    assert ref[..., :K].float().abs().max().item() > 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_first_layer_kernels_cover_16bit(dev, dtype):
     """conv1_1 (C = 3 -> 8, 3x3) runs the small-channel kernels in both 16-bit
     storage types (the parity of both is in the CONV_CASES / SPLIT_WGRAD_CASES
