@@ -761,7 +761,7 @@ def main():
         ops.set_option(name, int(val))
     for kv in args.schedule:
         name, val = kv.split("=")
-        SCHEDULE[name] = int(val)
+        SCHEDULE[name] = float(val) if "." in val else int(val)
     dH, dW, dB, dkp = DEFAULTS[args.model]
     if args.dtype is None:
         args.dtype = DEFAULT_DTYPE[args.model]

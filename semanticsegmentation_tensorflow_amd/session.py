@@ -182,10 +182,6 @@ class Session(PlanMixin, StreamMixin):
         # collectives complete, on the side stream beside the rest of backward
         # (0: all at the end)
         self.overlap_big_mb = 0
-        # single process: once this fraction of the non-fused variables' elements
-        # has final gradients, their Adam runs as one side-stream launch beside
-        # the last input gradients (0: all in one launch at the end)
-        self.late_adam = 0.0
 
         self._side = None
         self._adam_ctx = None
@@ -787,11 +783,6 @@ class Session(PlanMixin, StreamMixin):
                 self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set)
                 if dpa is not None:
                     dpa.on_launch = self._adam_ctx.after_work
-            elif (self._fused is not None and self.late_adam > 0 and self._red is not None
-                  and self.device.type == "cuda"):
-                skip = {nm for n in p.nodes if id(n) in p.adam_fusable
-                        for nm in [n.w.var_name] + ([n.bias.var_name] if n.bias is not None else [])}
-                self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set, late=(skip, self.late_adam))
             elif (opt is not None and dpa is not None and not zero and self.overlap_big_mb and not scaled
                   and not p.train.accum and self.device.type == "cuda"):
                 self._adam_ctx = _AdamOverlap(self, opt, gs, p.var_set, big_only=True)
@@ -846,7 +837,7 @@ class Session(PlanMixin, StreamMixin):
                     ops.axpy(store.aux[acc].view(-1), store.grad(var).view(-1), sc / world / S)
                 store.aux_version += 1
             elif self._adam_ctx is not None:
-                self._adam_ctx.finish(self._fused[2] if self._fused is not None else ())
+                self._adam_ctx.finish()
                 self._adam_ctx = None
             elif zero:
                 self._zero_update(p, opt, gs)

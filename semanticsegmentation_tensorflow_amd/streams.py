@@ -22,7 +22,7 @@ class _AdamOverlap:
     (its input gradient is enqueued before its filter gradient).  finish()
     updates the remaining variables and makes the compute stream wait."""
 
-    def __init__(self, sess, opt, gs, var_set, big_only=False, late=None):
+    def __init__(self, sess, opt, gs, var_set, big_only=False):
         self.s = sess
         self.opt = opt
         self.gs = gs
@@ -42,20 +42,6 @@ class _AdamOverlap:
             st = sess.store
             lim = sess.overlap_big_mb * (1 << 20) / 4
             self.big = {nm for nm in var_set if nm in st.by_name and math.prod(st.by_name[nm].shape) >= lim}
-        # late = (skip, frac) (single process, Session.late_adam): the variables
-        # outside `skip` (the fused conv6 / conv7 launches') collect as their
-        # gradients complete; once they hold >= frac of those variables'
-        # elements, ONE launch updates them on the side stream, beside the
-        # compute stream's last input gradients; finish() the rest
-        self.late = late
-        self.tail_on_main = big_only or late is not None
-        if late is not None:
-            st = sess.store
-            self.late_sizes = {nm: math.prod(st.by_name[nm].shape) for nm in var_set
-                               if nm in st.by_name and nm not in late[0]}
-            self.late_total = sum(self.late_sizes.values())
-            self.late_have = []
-            self.late_done = False
 
     def _adam(self, names, stream=None):
         st = self.s.store
@@ -69,14 +55,6 @@ class _AdamOverlap:
         self.done.update(names)
 
     def launch(self, names):
-        if self.late is not None:
-            if self.late_done:
-                return
-            self.late_have += [nm for nm in names if nm in self.late_sizes]
-            if sum(self.late_sizes[nm] for nm in self.late_have) < self.late[1] * self.late_total:
-                return
-            self.late_done = True
-            names = self.late_have
         ev = torch.cuda.Event()
         ev.record(self.main)
         self.side.wait_event(ev)
@@ -97,10 +75,9 @@ class _AdamOverlap:
             self.side.wait_event(ev)
         self._adam(names)
 
-    def finish(self, fused=()):
-        rest = [v.var_name for v in self.s.store.order
-                if v.var_name in self.var_set and v.var_name not in self.done and v.var_name not in fused]
-        if self.tail_on_main:              # the rest: one launch on the compute stream
+    def finish(self):
+        rest = [v.var_name for v in self.s.store.order if v.var_name in self.var_set and v.var_name not in self.done]
+        if self.big is not None:           # the small variables: one launch on the compute stream
             self.main.wait_stream(self.side)
             if rest:
                 self._adam(rest, stream=self.main)

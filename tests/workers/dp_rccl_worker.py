@@ -38,7 +38,6 @@ CASES = [
     ("sp_bf16_serial", "bf16", None, {"side_wgrad": 0, "main_wgrad": 0, "fused_delay": 0}),
     ("sp_bf16_side1", "bf16", None, {"side_wgrad": 1, "main_wgrad": 1}),
     ("sp_bf16_nofuse", "bf16", None, {"fuse_pool": False, "fuse_grad_sum": False}),
-    ("sp_bf16_late", "bf16", None, {"late_adam": 0.9}),
     ("dp_bf16_zero", "bf16", "zero", {}),
     ("dp_bf16_zero_serial", "bf16", "zero", {"side_wgrad": 0, "main_wgrad": 0}),
     ("dp_bf16_allreduce", "bf16", "allreduce", {"side_wgrad": 1}),
