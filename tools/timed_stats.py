@@ -39,13 +39,13 @@ def main():
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
-    if len(marks) < a.warmup + a.steps + 1:
-        sys.exit(f"{len(marks)} '{a.marker}' launches: fewer than warmup + steps + 1")
+    if len(marks) < a.warmup + a.steps:
+        sys.exit(f"{len(marks)} '{a.marker}' launches: fewer than warmup + steps")
     # each step: its input preparation .. its last Adam launch (the loss fetch
     # bench.py runs after the timed steps is not part of the last one)
     seg = []
     for j in range(a.warmup, a.warmup + a.steps):
-        part = rows[marks[j]:marks[j + 1]]
+        part = rows[marks[j]:marks[j + 1]] if j + 1 < len(marks) else rows[marks[j]:]
         last = max((i for i, r in enumerate(part) if a.end_marker in r["Kernel_Name"]), default=len(part) - 1)
         seg += part[:last + 1]
     t0 = int(seg[0]["Start_Timestamp"])
