@@ -814,6 +814,14 @@ def main():
     }
     if "loss_scaling" in m:
         result["loss_scaling"] = m["loss_scaling"]
+    # the world-1 RCCL probe right after the headline: after the CPU baseline
+    # its host-heavy step shared the host with that run's still-spinning OpenMP
+    # threads and lost ~10 % (495 vs 548 img/s in round 5)
+    if world == 1 and dp is None and args.model == "fcn" and not args.no_dp_probe:
+        try:
+            result["dp_mode"] = dp_probe(args, B, H, W, kp, device)
+        except Exception as exc:  # report, never crash the headline line
+            result["dp_mode"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_pipeline and args.model == "fcn":
         try:
             result["data_pipeline"] = pipeline_rate(H, W, device)
@@ -868,11 +876,6 @@ def main():
                 result["cpu_baseline_160x576"] = cpu_baseline(160, 576, 160, 576, args.cpu_steps, "fcn")
         except Exception as exc:  # report, never crash the headline line
             result["cpu_baseline"] = {"value": None, "error": repr(exc)}
-    if world == 1 and dp is None and args.model == "fcn" and not args.no_dp_probe:
-        try:
-            result["dp_mode"] = dp_probe(args, B, H, W, kp, device)
-        except Exception as exc:  # report, never crash the headline line
-            result["dp_mode"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist.is_initialized():
