@@ -173,10 +173,11 @@ class Session(PlanMixin, StreamMixin):
         self.fused_delay = 6
         self._pending_fused = []
         # the filter gradients of the first `main_wgrad` convs (the last in the
-        # backward: conv1_1 / conv1_2 in FCN) stay on the compute stream, which
-        # has no input gradient left to run then, beside the side stream's
-        # remaining filter gradients instead of after them
-        self.main_wgrad = 2
+        # backward: conv1_1 / conv1_2 / conv2_1 in FCN) stay on the compute
+        # stream, which has no input gradient left to run then, beside the side
+        # stream's remaining filter gradients instead of after them (round 5:
+        # 3 over 2 by 0.3 % in five A/B pairs)
+        self.main_wgrad = 3
         # data-parallel all-reduce steps: the Adam update of every variable of
         # >= overlap_big_mb MB (FCN conv6 / conv7) as soon as its buckets'
         # collectives complete, on the side stream beside the rest of backward

@@ -33,7 +33,7 @@ from tests.workers.dp_rccl_worker import CASES
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STREAM_ONLY = {"sp_bf16_serial", "sp_bf16_side1"}
+STREAM_ONLY = {"sp_bf16_serial", "sp_bf16_side1", "sp_bf16_mw2"}
 
 
 def _free_port():

@@ -37,6 +37,7 @@ CASES = [
     ("ref_bf16", "bf16", None, {}),
     ("sp_bf16_serial", "bf16", None, {"side_wgrad": 0, "main_wgrad": 0, "fused_delay": 0}),
     ("sp_bf16_side1", "bf16", None, {"side_wgrad": 1, "main_wgrad": 1}),
+    ("sp_bf16_mw2", "bf16", None, {"main_wgrad": 2}),
     ("sp_bf16_nofuse", "bf16", None, {"fuse_pool": False, "fuse_grad_sum": False}),
     ("dp_bf16_zero", "bf16", "zero", {}),
     ("dp_bf16_zero_serial", "bf16", "zero", {"side_wgrad": 0, "main_wgrad": 0}),
