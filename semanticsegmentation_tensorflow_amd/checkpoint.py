@@ -48,7 +48,11 @@ def _adam_step(d, offset=1):
     ~103k steps, e.g. the reference's MAX_ITERATION = 100001 loops past their
     end): float32 underflow, so the bias correction sqrt(1-b2^t)/(1-b1^t) is 1
     to float32 precision -- `global_step` when the checkpoint holds one, else
-    the first step at which beta2^t underflows.  No beta powers: step 0."""
+    the first step at which beta2^t underflows.  No beta powers: step 0.
+    Known limit: tensor-bundle checkpoints this package wrote before round 4
+    (it stored beta^t there too, until the bundle writer switched to TF's
+    beta^(t+1)) restore one Adam step low; resave them, or set the step from
+    their `global_step` after restore."""
     b1 = float(d.get("beta1_power", BETA1))
     b2 = float(d.get("beta2_power", BETA2))
     if 0.0 < b2 < 1.0:

@@ -65,6 +65,30 @@ def main():
                 res["v:" + k] = sess.store.adam_v(k).cpu().numpy()
             np.savez(os.path.join(out, f"rank{rank}_{case_tag(dtype, overlap, shard)}.npz"), **res)
             dist.barrier()
+        # a ZeRO-1 step (m / v current on this rank's slices only),
+        # then an all-reduce-mode step (the overlapped per-layer optimizer reads
+        # whole variables) with no explicit sync between them: the Session
+        # gathers the stale slices first, so the ranks stay bit-identical
+        image, labels, keep, pred, logits, loss, train_step = build_fcn(H, W)
+        dp = DataParallel(bucket_mb=16.0, shard_optimizer=True)
+        sess = tf.Session(compute_dtype="f32", data_parallel=dp, seed=5)
+        sess.run(tf.global_variables_initializer())
+        for k, v in weights.items():
+            sess.assign(k, v)
+        feed = {image: img[part], labels: lab[part], keep: 1.0}
+        sess.run(train_step, feed_dict=feed)
+        assert dp.mode == "zero" and dp.slots_stale
+        sess.overlap_optimizer = True
+        sess.run(train_step, feed_dict=feed)
+        torch.cuda.synchronize()
+        assert dp.mode == "allreduce" and not dp.slots_stale, (dp.mode, dp.slots_stale)
+        res = {}
+        for k in weights:
+            res["p:" + k] = sess.variable_value(k)
+            res["m:" + k] = sess.store.adam_m(k).cpu().numpy()
+            res["v:" + k] = sess.store.adam_v(k).cpu().numpy()
+        np.savez(os.path.join(out, f"rank{rank}_mixed.npz"), **res)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
 
