@@ -630,15 +630,24 @@ def dp_probe(args, B, H, W, kp, device):
     slices (ZeRO-1), the all-gather of the updated parameters and the repack
     of the compute copies (the conv6 / conv7 filter-gradient + Adam fusion is
     off: a collective sits between gradient and update)."""
+    import torch
     import torch.distributed as dist
     from semanticsegmentation_tensorflow_amd.dp import DataParallel
+    own = not dist.is_initialized()
     init_rccl(device)
     dp = DataParallel(bucket_mb=args.bucket_mb, force_collectives=True, shard_optimizer=args.dp_mode == "zero")
     m = measure(args.model, B, H, W, kp, args.steps, args.warmup, args.dtype, device, dp, 0)
     exchange = ("zero1 (reduce-scatter, sharded Adam, all-gather)" if args.dp_mode == "zero"
                 else "all-reduce per bucket during backward, every rank's Adam")
-    return {"backend": dist.get_backend(), "world": dist.get_world_size(), "bucket_mb": args.bucket_mb,
-            "buckets": len(dp.buckets), "exchange": exchange,
+    backend, world, nb = dist.get_backend(), dist.get_world_size(), len(dp.buckets)
+    if own:
+        # the group exists for this probe only: its RCCL proxy thread would
+        # otherwise keep polling beside the side lines (C3 measured 197 instead
+        # of 214 img/s after it) and the CPU baseline
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+    return {"backend": backend, "world": world, "bucket_mb": args.bucket_mb,
+            "buckets": nb, "exchange": exchange,
             "value": round(m["value"], 3), "unit": "images/s", "ms_per_step": round(m["ms_per_step"], 3),
             "note": "same workload as the headline; collectives forced on at world 1 (a real world-1 job "
                     "skips them and runs the single-process plan)"}
