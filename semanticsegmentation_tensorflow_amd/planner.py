@@ -166,6 +166,11 @@ class PlanMixin:
         reader: its input gradient is the first write into the root's gradient
         buffer (it runs first in backward) and covers it whole.
 
+        DeepLab's ASPP concat [image pooling, aspp0..3] (Network/utils/utils.py
+        :186-229, 332) qualifies too: its parts are BatchNorm+ReLU outputs and
+        the image-pooling branch's 1x1 -> HxW resize (a broadcast through the
+        row stride), its one reader the concat_projection conv.
+
         Nested roots: FC-DenseNet's decoder concat [transition_up, dense_block]
         (Network/model/FCDenseNet.py:141-154) has the dense block's own root as
         a part, so that block buffer becomes a channel slice of the decoder
@@ -191,6 +196,12 @@ class PlanMixin:
                 return False
             if i in p.alias:
                 return False
+            if prod.kind == "ResizeBilinear":
+                # the 1x1 -> HxW align_corners resize is a broadcast written
+                # (and its gradient, a spatial sum, read) through the row
+                # stride: DeepLab's image-pooling ASPP branch
+                xs = shp[id(prod.inputs[0])]
+                return len(xs) == 4 and xs[1] == 1 and xs[2] == 1
             return prod.kind in ("conv", "AvgPool", "MaxPool", "bn", "tconv") or (
                 prod.kind == "ConcatV2" and i not in nested)
 

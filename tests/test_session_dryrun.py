@@ -241,3 +241,32 @@ def test_pool_fusion_choice_at_c2_shapes():
     assert not ops.conv2d_fwd_pool_ok(ops.conv_desc(4, 24, 78, 512, 512, 3, 3, dtype=ops.BF16))
     # odd output size (375 x 1242 unpadded is even; 375 x 1241 is not): no whole windows
     assert not ops.conv2d_fwd_pool_ok(ops.conv_desc(1, 375, 1241, 64, 64, 3, 3, dtype=ops.BF16))
+
+
+def test_deeplab_aspp_concat_is_a_view(dry):
+    """C5: the ASPP concat [image pooling, aspp0..3] (Network/utils/utils.py
+    :186-229, 332) is a channel view: the branches' BatchNorm+ReLU and the
+    image-pooling branch's 1x1 -> HxW broadcast write their slices of one
+    buffer, the concat_projection conv's input gradient is the first write into
+    its gradient buffer and the branches read theirs from it -- no concat copy
+    in either direction."""
+    from semanticsegmentation_tensorflow_amd.deeplab import DeepLabASPP
+    G.reset_default_graph()
+    H, W = 64, 96
+    image = tf.placeholder(tf.float32, [None, H, W, 3])
+    labels = tf.placeholder(tf.uint8, [None, H, W])
+    keep = tf.placeholder(tf.float32)
+    pred, logits = DeepLabASPP(image, keep, 2)
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="f16")
+    sess.run(tf.global_variables_initializer())
+    dry.calls.clear()
+    sess.run([train, loss], feed_dict={image: np.zeros((1, H, W, 3), np.float32),
+                                       labels: np.zeros((1, H, W), np.uint8), keep: 0.8})
+    c = dry.calls
+    assert c.count("seg_concat_fwd") == 0
+    assert c.count("seg_concat_bwd") == 0
+    assert c.count("seg_spatial_broadcast") >= 1        # the image-pooling resize, into its slice
+    (p,) = [q for q in sess.plans.values() if q.train]
+    assert len(p.alias_nodes) == 1
