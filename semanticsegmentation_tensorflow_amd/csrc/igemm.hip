@@ -39,7 +39,7 @@ __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<
 // NT epilogue, split into a per-row part (one pixel decomposition) and a
 // per-element part; used by the v1 GEMM and by the split-K reducer.
 struct NtRow {
-    long yoff, roff, moff;
+    long yoff, roff, moff, y2off;
     uint64_t gidx;   // dropout counter base: (img*OH*OW + pix) * n_valid
 };
 
@@ -54,6 +54,7 @@ __device__ __forceinline__ NtRow nt_row(const NTParams& p, int row, int Ha, int 
     r.yoff = img * p.y_img + pix * p.ldy;
     r.roff = img * p.epi.res_img + pix * p.epi.ld_res;
     r.moff = img * p.epi.mask_img + pix * p.epi.ld_mask;
+    r.y2off = img * p.epi.y2_img + pix * p.epi.ld_y2;
     r.gidx = ((uint64_t)((long)img * p.OH * p.OW + pix)) * p.epi.n_valid;
     return r;
 }
@@ -351,8 +352,25 @@ __global__ __launch_bounds__(256) void splitk_reduce_nt(NTParams p, int splits) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = nt_apply(p.epi, rw, col0 + j, v[j], res[j], mk[j]);
         T* yp = reinterpret_cast<T*>(p.y) + rw.yoff + col0;
-        *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+        const uint4 packed = Chunk<T>::pack(v);
+        *reinterpret_cast<uint4*>(yp) = packed;
         if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(yp + 4) = Chunk<T>::pack(v + 4);
+        if constexpr (sizeof(T) == 2) {
+            if (p.epi.y2) {      // BN2(+ReLU) of the stored values (seg_bn_relu_fwd's arithmetic, as igemm_nt2)
+                const EpiParams& e = p.epi;
+                float r[8], o2[8];
+                Chunk<T>::unpack(packed, r);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int col = col0 + j;
+                    const bool c2 = col < e.bn2_cv;
+                    float v2 = __builtin_fmaf(r[j], c2 ? e.bn2_gamma[col] * e.bn2_inv : 0.f, c2 ? e.bn2_beta[col] : 0.f);
+                    if (e.bn2_relu) v2 = fmaxf(v2, 0.f);
+                    o2[j] = v2;
+                }
+                *reinterpret_cast<uint4*>(reinterpret_cast<T*>(e.y2) + rw.y2off + col0) = Chunk<T>::pack(o2);
+            }
+        }
     }
 }
 
@@ -847,10 +865,13 @@ bool nt_unpool_ok(const NTParams& p, int dtype) {
     return nt_plan_unpools(nt_plan(p, dtype, 1, p.M), p);
 }
 
-// Whether the planned kernel writes EpiParams.y2 (the BN(+ReLU) second
-// output): igemm_nt2 with its operand prologue or without, no split-K.
+// Whether the planned launch writes EpiParams.y2 (the BN(+ReLU) second
+// output): igemm_nt2 with its operand prologue or without, no split-K; and
+// igemm_nt3 with split-K, whose splitk_reduce_nt writes it (DeepLab's ASPP
+// convs -> BN -> ReLU on the 1/8-resolution map).
 static bool nt_plan_bn2(const NTPlan& pl, int dtype) {
-    return dtype != SEG_F32 && pl.splits == 1 && (pl.kind == NTK_PRO2 || pl.kind == NTK_NT2);
+    if (dtype == SEG_F32) return false;
+    return (pl.splits == 1 && (pl.kind == NTK_PRO2 || pl.kind == NTK_NT2)) || (pl.kind == NTK_NT3 && pl.splits > 1);
 }
 
 bool nt_bn2_ok(const NTParams& p, int dtype) { return nt_plan_bn2(nt_plan(p, dtype, 1, p.M), dtype); }

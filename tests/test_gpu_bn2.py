@@ -81,3 +81,43 @@ def test_conv_bn2_refused_on_split_k(dev):
         ops.conv2d_fwd_bn2(d, x, None, wk, y, a, one, one)
     torch.cuda.synchronize()
     assert bool((y == 7.0).all()) and bool((a == 7.0).all())
+
+
+# igemm_nt3 with split-K carries the second output too, written by its
+# splitk_reduce_nt: DeepLab's ASPP convs -> BN -> ReLU (Network/utils/utils.py
+# :186-229) on C5's 1/8-resolution feature map -- the rate-6 / rate-18 3x3
+# convs and the 1280 -> 256 concat_projection
+NT3_CASES = [(2, 48, 156, 512, 256, 3, 6), (2, 48, 156, 512, 256, 3, 18), (2, 48, 156, 1280, 256, 1, 1)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", NT3_CASES, ids=["aspp1_rate6", "aspp3_rate18", "projection_1x1"])
+def test_nt3_split_bn2_equals_conv_then_bn_relu(dev, case, dtype):
+    N, H, W, C, K, R, dil = case
+    dt = ops.BF16 if dtype == torch.bfloat16 else ops.F16
+    d = ops.conv_desc(N, H, W, C, K, R, R, dilation=dil, dtype=dt)
+    name, splits, _ = ops.conv_kernel_info(d, ops.OP_FWD)
+    assert name.startswith("igemm_nt3") and splits > 1, (name, splits)
+    assert ops.conv2d_fwd_bn2_ok(d, False)
+    g = torch.Generator(device=dev).manual_seed(23)
+    x = torch.randn(N, H, W, C, device=dev, generator=g).to(dtype)
+    w32 = torch.randn(R, R, C, K, device=dev, generator=g) / (R * R * C) ** 0.5
+    wk = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, C), dtype=dtype, device=dev)
+    ops.pack_filter(w32, wk, C, K, ops.PACK_KRSC)
+    g2 = 1.0 + 0.1 * torch.randn(K, device=dev, generator=g)
+    b2 = 0.1 * torch.randn(K, device=dev, generator=g)
+    bias = 0.1 * torch.randn(K, device=dev, generator=g)
+    epi = ops.epilogue(bias=bias)
+    ws = ops.Workspace(dev)
+    y_ref = torch.full((N, H, W, K), float("nan"), dtype=dtype, device=dev)
+    ops.conv2d_fwd(d, x, wk, y_ref, epi, ws)
+    a_ref = torch.full_like(y_ref, float("nan"))
+    ops.bn_relu_fwd(y_ref, a_ref, g2, b2, K, True)
+    y = torch.full_like(y_ref, float("nan"))
+    a = torch.full_like(y_ref, float("nan"))
+    ops.conv2d_fwd_bn2(d, x, None, wk, y, a, g2, b2, True, 1e-3, epi, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+    assert torch.equal(a.view(torch.int16), a_ref.view(torch.int16))
+    zero = (a == 0).float().mean().item()
+    assert 0.2 < zero < 0.8, zero
