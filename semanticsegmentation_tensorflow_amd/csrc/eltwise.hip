@@ -831,8 +831,55 @@ __global__ __launch_bounds__(256) void resize_fwd_k(const T* __restrict__ x, T* 
         const float lx = fx - x0;
         const float tl = to_f32(r0[x0 * C + c]), tr = to_f32(r0[x1 * C + c]);
         const float bl = to_f32(r1[x0 * C + c]), br = to_f32(r1[x1 * C + c]);
-        const float top = tl + (tr - tl) * lx, bot = bl + (br - bl) * lx;
-        yr[j] = from_f32<T>(top + (bot - top) * ly);
+        // explicit fmas (the 8-channel kernel's arithmetic, whatever the contraction)
+        // (the fp32 result is pinned before the 16-bit rounding: hipcc would
+        // otherwise fold fma + fp16 conversion into one v_fma_mixlo_f16, a
+        // single rounding the 8-channel kernel's packed form does not get)
+        const float top = __builtin_fmaf(tr - tl, lx, tl), bot = __builtin_fmaf(br - bl, lx, bl);
+        float r = __builtin_fmaf(bot - top, ly, top);
+        asm volatile("" : "+v"(r));
+        yr[j] = from_f32<T>(r);
+    }
+}
+
+// The same with 8 channels per thread (C % 8 == 0, 16-byte aligned rows):
+// 16-byte gathers and stores instead of 2-byte ones -- DeepLab's logits (2
+// classes padded to 8) made the scalar form a 2-byte store stream at 0.15
+// TB/s.  Per-channel arithmetic identical to resize_fwd_k (explicit fmas in
+// both, so the compiler's contraction choices cannot differ).
+template <typename T>
+__global__ __launch_bounds__(256) void resize_fwd8_k(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W,
+                                                     int C, int OH, int OW) {
+    const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+    const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+    const int row = blockIdx.x;                   // n * OH + oy
+    const int n = row / OH, oh = row - n * OH;
+    const float fy = oh * sh;
+    const int y0 = (int)floorf(fy);
+    const int y1 = min(y0 + 1, H - 1);
+    const float ly = fy - y0;
+    const T* r0 = x + ((long)n * H + y0) * W * C;
+    const T* r1 = x + ((long)n * H + y1) * W * C;
+    T* yr = y + (long)row * OW * C;
+    const int c8 = C / 8, nch = OW * c8;
+    for (int j = blockIdx.y * blockDim.x + threadIdx.x; j < nch; j += gridDim.y * blockDim.x) {
+        const int ow = j / c8, c = (j - ow * c8) * 8;
+        const float fx = ow * sw;
+        const int x0 = (int)floorf(fx);
+        const int x1 = min(x0 + 1, W - 1);
+        const float lx = fx - x0;
+        float tl[8], tr[8], bl[8], br[8], o[8];
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(r0 + x0 * C + c), tl);
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(r0 + x1 * C + c), tr);
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(r1 + x0 * C + c), bl);
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(r1 + x1 * C + c), br);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float top = __builtin_fmaf(tr[k] - tl[k], lx, tl[k]), bot = __builtin_fmaf(br[k] - bl[k], lx, bl[k]);
+            o[k] = __builtin_fmaf(bot - top, ly, top);
+            asm volatile("" : "+v"(o[k]));
+        }
+        *reinterpret_cast<uint4*>(yr + ow * C + c) = Chunk<T>::pack(o);
     }
 }
 
@@ -882,11 +929,51 @@ __global__ __launch_bounds__(256) void resize_bwd_k(const T* __restrict__ dy, fl
             float racc = 0.f;
             for (int ox = ox_lo; ox <= ox_hi; ++ox) {
                 const float wx = resize_weight(ox, xx, sw, W);
-                if (wx != 0.f) racc += wx * to_f32(dr[ox * C]);
+                if (wx != 0.f) racc = __builtin_fmaf(wx, to_f32(dr[ox * C]), racc);
             }
-            acc += wy * racc;
+            acc = __builtin_fmaf(wy, racc, acc);
         }
         dx[(long)row * rowlen + j] = acc;
+    }
+}
+
+// The gather with 8 channels per thread (C % 8 == 0): 16-byte dy loads, two
+// 16-byte dx stores; per-channel summation order identical to resize_bwd_k.
+template <typename T>
+__global__ __launch_bounds__(256) void resize_bwd8_k(const T* __restrict__ dy, float* __restrict__ dx, int N, int H,
+                                                     int W, int C, int OH, int OW) {
+    const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+    const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+    const int row = blockIdx.x;                   // n * H + y
+    const int n = row / H, yy = row - n * H;
+    int oy_lo, oy_hi;
+    resize_src_range(yy, sh, OH, oy_lo, oy_hi);
+    const int c8 = C / 8, nch = W * c8;
+    for (int j = blockIdx.y * blockDim.x + threadIdx.x; j < nch; j += gridDim.y * blockDim.x) {
+        const int xx = j / c8, c = (j - xx * c8) * 8;
+        int ox_lo, ox_hi;
+        resize_src_range(xx, sw, OW, ox_lo, ox_hi);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const float wy = resize_weight(oy, yy, sh, H);
+            if (wy == 0.f) continue;
+            const T* dr = dy + ((long)n * OH + oy) * OW * C + c;
+            float racc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const float wx = resize_weight(ox, xx, sw, W);
+                if (wx != 0.f) {
+                    float d[8];
+                    Chunk<T>::unpack(*reinterpret_cast<const uint4*>(dr + ox * C), d);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) racc[k] = __builtin_fmaf(wx, d[k], racc[k]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] = __builtin_fmaf(wy, racc[k], acc[k]);
+        }
+        float* dp = dx + ((long)row * W + xx) * C + c;
+        *reinterpret_cast<float4*>(dp) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(dp + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
     }
 }
 
@@ -1519,6 +1606,17 @@ extern "C" int seg_resize_bilinear_fwd(const void* x, void* y, int N, int H, int
     if (!x || !y || N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return SEG_EINVAL;
     if ((long)W * C > 0x7fffffffL || (long)OW * C > 0x7fffffffL || (long)N * OH > 0x7fffffffL) return SEG_EINVAL;
     const int rowlen = OW * C;
+    if (dtype != SEG_F32 && C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+        const dim3 grid8((unsigned)(N * OH), (unsigned)std::min((rowlen / 8 + 255) / 256, 64));
+        if (dtype == SEG_BF16)
+            hipLaunchKernelGGL(resize_fwd8_k<bf16>, grid8, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y,
+                               N, H, W, C, OH, OW);
+        else
+            hipLaunchKernelGGL(resize_fwd8_k<f16>, grid8, dim3(256), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, N,
+                               H, W, C, OH, OW);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     const dim3 grid((unsigned)(N * OH), (unsigned)std::min((rowlen + 255) / 256, 64));
     DISPATCH_T(dtype, hipLaunchKernelGGL(resize_fwd_k<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y,
                                          N, H, W, C, OH, OW));
@@ -1532,6 +1630,15 @@ extern "C" int seg_resize_bilinear_bwd(const void* dy, float* dx, int N, int H, 
     if ((long)W * C > 0x7fffffffL || (long)OW * C > 0x7fffffffL || (long)N * H > 0x7fffffffL) return SEG_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     const int rowlen = W * C;                       // every dx element is written: no memset
+    if (dtype != SEG_F32 && C % 8 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+        const dim3 grid8((unsigned)(N * H), (unsigned)std::min((rowlen / 8 + 255) / 256, 64));
+        if (dtype == SEG_BF16)
+            hipLaunchKernelGGL(resize_bwd8_k<bf16>, grid8, dim3(256), 0, s, (const bf16*)dy, dx, N, H, W, C, OH, OW);
+        else
+            hipLaunchKernelGGL(resize_bwd8_k<f16>, grid8, dim3(256), 0, s, (const f16*)dy, dx, N, H, W, C, OH, OW);
+        SEG_CHECK_LAUNCH();
+        return SEG_OK;
+    }
     const dim3 grid((unsigned)(N * H), (unsigned)std::min((rowlen + 255) / 256, 64));
     DISPATCH_T(dtype, hipLaunchKernelGGL(resize_bwd_k<T>, grid, dim3(256), 0, s, (const T*)dy, dx, N, H, W, C, OH,
                                          OW));

@@ -664,6 +664,39 @@ def test_resize_bilinear(dev, case):
     assert_close(dxd.double().cpu(), x.grad, torch.float32, "resize bwd", 1e-5)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", [(2, 48, 156, 8, 384, 1248), (2, 6, 9, 16, 41, 65), (1, 3, 3, 8, 128, 96),
+                                  (1, 9, 15, 8, 5, 7)])
+def test_resize_bilinear_8wide_equals_scalar(dev, case, dtype):
+    """The 8-channel (16-byte) resize kernels (16-bit, C % 8 == 0, aligned
+    rows: DeepLab's x8 logits upsampling) against the per-element kernels the
+    launcher takes for misaligned storage of the same values: bit-identical
+    forward and gradient."""
+    N, H, W, C, OH, OW = case
+    g = torch.Generator(device=dev).manual_seed(19)
+
+    def misaligned(shape, dt):
+        buf = torch.empty(int(np.prod(shape)) + 1, dtype=dt, device=dev)
+        return buf[1:].view(shape)
+    x = torch.randn(N, H, W, C, device=dev, generator=g).to(dtype)
+    dy = torch.randn(N, OH, OW, C, device=dev, generator=g).to(dtype)
+    y8 = torch.full((N, OH, OW, C), float("nan"), dtype=dtype, device=dev)
+    ops.resize_bilinear_fwd(x, y8)
+    xs = misaligned(x.shape, dtype)
+    xs.copy_(x)
+    ys = misaligned(y8.shape, dtype)
+    ops.resize_bilinear_fwd(xs, ys)
+    dx8 = torch.full((N, H, W, C), float("nan"), device=dev)
+    ops.resize_bilinear_bwd(dy, dx8)
+    dys = misaligned(dy.shape, dtype)
+    dys.copy_(dy)
+    dxs = misaligned(dx8.shape, torch.float32)
+    ops.resize_bilinear_bwd(dys, dxs)
+    torch.cuda.synchronize()
+    assert torch.equal(y8.view(torch.int16), ys.view(torch.int16))
+    assert torch.equal(dx8.view(torch.int32), dxs.view(torch.int32))
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_adam_tf1_pack_matches_step_plus_pack(dev, dtype):
     """Fused multi-tensor Adam + packed copies == adam_tf1_step then pack_filter.
