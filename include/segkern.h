@@ -163,9 +163,11 @@ int seg_conv2d_fwd_pro(const seg_conv_desc* d, const void* x, const seg_prologue
  * dropout -> BN -> ReLU (Network/model/FCDenseNet.py:28-31, utils.py:300-303):
  * writes y as seg_conv2d_fwd[_pro] and y2 = relu(y * gamma2 / sqrt(1 + eps2)
  * + beta2) from the stored y, bit-identical to seg_bn_relu_fwd(y, y2, ...),
- * so the BN forward pass never re-reads y.  ld_y2: y2's pixel stride
- * (elements, multiple of 8).  SEG_EINVAL when the kernel the conv runs on
- * has no second output (query: seg_conv2d_fwd_bn2_ok). */
+ * so the BN forward pass never re-reads y.  Also DeepLab's ASPP conv -> BN
+ * -> ReLU (Network/utils/utils.py:186-229), where the split-K reducer after
+ * igemm_nt3 writes y2.  ld_y2: y2's pixel stride (elements, multiple of 8).
+ * SEG_EINVAL when the kernel the conv runs on has no second output (query:
+ * seg_conv2d_fwd_bn2_ok). */
 int seg_conv2d_fwd_bn2(const seg_conv_desc* d, const void* x, const seg_prologue* pro, const void* w,
                        const seg_epilogue* epi, void* y, void* y2, int ld_y2, const float* gamma2,
                        const float* beta2, float eps2, int relu2, void* ws, size_t ws_bytes, void* stream);
