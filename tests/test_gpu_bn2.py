@@ -85,8 +85,9 @@ def test_conv_bn2_refused_on_split_k(dev):
 
 # igemm_nt3 with split-K carries the second output too, written by its
 # splitk_reduce_nt: DeepLab's ASPP convs -> BN -> ReLU (Network/utils/utils.py
-# :186-229) on C5's 1/8-resolution feature map -- the rate-6 / rate-18 3x3
-# convs and the 1280 -> 256 concat_projection
+# :186-229) on the 1/8-resolution map of a 384x1248 input (48x156, where the
+# plan splits K) -- the rate-6 / rate-18 3x3 convs and the 1280 -> 256
+# concat_projection
 NT3_CASES = [(2, 48, 156, 512, 256, 3, 6), (2, 48, 156, 512, 256, 3, 18), (2, 48, 156, 1280, 256, 1, 1)]
 
 
