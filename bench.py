@@ -39,7 +39,8 @@ FCN_TRAIN_FLOP_PER_IMG = 1348.97e9                 # SURVEY.md 8d at 384x1248, C
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); default 1, or WORLD_SIZE when started by torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="fcn", choices=["fcn", "fcdensenet", "deeplab"],
@@ -300,6 +301,8 @@ def kernel_symbol(name):
     a = rest.rstrip(">").split(",")
     bm, bn = a[1], a[2]
     # dtype-templated kernels appear mangled (`_ZN3seg10conv_halo2ILi16E...`)
+    if fam == "conv_halo4":
+        return r"conv_halo4[<I]"
     if fam == "conv_halo":
         return r"conv_halo2[<I]" if bn == "256" else r"conv_halo(_duo)?[<I]"
     if fam in ("igemm_nt3", "igemm_tn3"):
@@ -550,8 +553,10 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
     torch.cuda.synchronize()
     ev = [s_ev.elapsed_time(e_ev) for _, _, s_ev, e_ev in sess.timer]
     sess.timer, sess.timer_match = None, None
+    timing_mode = "all_events"
     if len(ev) == dn * reps:
         dms = sum(ev) / reps
+        timing_mode = "family"
     achieved = (dflops / dn) / (dms / dn * 1e-3)
     peak = PEAK[dtype]
     # roofline bound of the dominant kernel group from its arithmetic intensity
@@ -568,9 +573,15 @@ def measure(model, B, H, W, kp, steps, warmup, dtype, device, dp=None, rank=0, f
                 "traffic": None, "launches_per_step": dn, "algorithmic_gflop_per_launch": round(dflops / dn / 1e9, 3),
                 "algorithmic_bytes_per_launch": round(dbytes / dn), "avg_launch_ms": round(dms / dn, 4)}
     roof["all_events_avg_launch_ms"] = round(all_ev_ms, 4)
-    roof["timing"] = (f"HIP events (hipEventDisableSystemFence: no cache flush in the interval) on the launch "
-                      f"stream around the {dn} launches per step of this family only, {reps} train steps after the "
-                      f"timed ones; all_events_avg_launch_ms: the same with every conv launch of the step bracketed")
+    roof["timing_mode"] = timing_mode
+    if timing_mode == "family":
+        roof["timing"] = (f"HIP events (hipEventDisableSystemFence: no cache flush in the interval) on the launch "
+                          f"stream around the {dn} launches per step of this family only, {reps} train steps after "
+                          f"the timed ones; all_events_avg_launch_ms: the same with every conv launch of the step "
+                          f"bracketed")
+    else:
+        roof["timing"] = (f"HIP events around EVERY conv launch of one train step (the family-only re-timing "
+                          f"recorded {len(ev)} events, not {dn} x {reps}, and was discarded)")
     if dname in alone and alone[dname][1] > 0:
         an, ams = alone[dname]
         if hbm_bound:
@@ -742,6 +753,8 @@ def dry_run(args):
 
 def main():
     args = parse()
+    if args.gpus is None:   # torchrun without --gpus: one rank per process it started
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.dry_run:
@@ -750,7 +763,7 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
+    if world != args.gpus:   # only an explicit --gpus can disagree with the launcher
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))

@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libsegkern.so")
 # MFMA / no stores -- garbage results) exist only in this separate library;
 # SEG_DIAG_LIB=1 loads it instead of the product library
 DIAG_LIB_PATH = os.path.join(PKG_DIR, "build_diag", "libsegkern_diag.so")
-SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
+SOURCES = ["igemm.hip", "igemm2.hip", "igemm3.hip", "halo.hip", "halo4.hip", "wgrad.hip", "conv.hip", "eltwise.hip", "optim.hip", "smallc.hip", "augment.hip", "dense1x1.hip"]
 HOST_SOURCES = ["pngdec.cpp", "crc32c.cpp"]
 HIP_HOST_SOURCES = ["timing.cpp"]   # host code against the HIP runtime API (hipcc, no kernels)
 HOST_LIBS = ["-lz"]

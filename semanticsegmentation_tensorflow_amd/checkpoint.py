@@ -27,6 +27,7 @@ import os
 import re
 
 import numpy as np
+import torch.distributed as dist
 
 from . import tf_bundle
 
@@ -96,17 +97,26 @@ class Saver:
         Adam slots is a collective (`Session.sync_optimizer_slots`), so a
         rank-0-only call would hang the job.  Only one rank writes and prunes
         the files: `write=None` means rank 0 of the Session's data-parallel
-        group (every process when there is none); the other ranks return the
-        same path without touching the file system."""
+        group (every process when there is none).  Every rank returns only
+        once the bundle, the pruning and the `checkpoint` state file are on
+        disk (a barrier on the data-parallel group after the write), so a
+        rank may restore or call latest_checkpoint right after save."""
         store = sess._ensure_store()
         sess.sync_optimizer_slots()        # ZeRO-1 data parallelism: Adam slots gathered first (collective)
         gs = self._global_step_value(sess, global_step)
         path = save_path if gs is None else f"{save_path}-{gs}"
+        dp = getattr(sess, "dp", None)
         if write is None:
-            dp = getattr(sess, "dp", None)
             write = dp is None or getattr(dp, "rank", 0) == 0
-        if not write:
-            return path
+        try:
+            if write:
+                self._write(sess, store, path)
+        finally:
+            if dp is not None and dist.is_available() and dist.is_initialized():
+                dist.barrier(group=getattr(dp, "group", None))
+        return path
+
+    def _write(self, sess, store, path):
         out = {}
         for v in self._vars(sess):
             name = v.var_name

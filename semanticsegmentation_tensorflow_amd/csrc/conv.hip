@@ -3,6 +3,7 @@
 // each mapped onto the implicit-GEMM kernels of igemm.hip.
 #include "common.h"
 #include "igemm.h"
+#include "halo.h"
 #include <stdio.h>
 #include <string.h>
 #include <math.h>
@@ -529,6 +530,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"halo_duo", &seg::g_halo_duo, 0, 1, 1, {}},
         {"nt_halo", &seg::g_nt_halo, 0, 1, 1, {}},
         {"halo_wide", &seg::g_halo_wide, 0, 1, 1, {}},
+        {"halo4", &seg::g_halo4, 0, 5, 1, {}},
         {"halo_min_splits", &seg::g_halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
         {"adam_tr_fused", &g_adam_tr_fused, 0, 1, 1, {}},
         {"nt2_short", &seg::g_nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
@@ -567,7 +569,7 @@ extern "C" int seg_set_option(const char* name, int value) {
         {"smallk_abl", &seg::g_smallk_abl, 0, 3, 1, {}},
         {"tn3_adam_abl", &seg::g_tn3_adam_abl, 0, 31, 1, {}},
         {"wgrad_abl", &seg::g_wgrad_abl, 0, 3, 1, {}},
-        {"nt2_ablate", &seg::g_nt2_ablate, 0, 9, 1, {}},
+        {"nt2_ablate", &seg::g_nt2_ablate, 0, 19, 1, {}},
 #endif
     };
     for (const Knob& k : knobs) {
@@ -608,8 +610,13 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
 static NTParams fwd_hwio_params(const seg_conv_desc* d) {
     NTParams p = conv_fwd_params(d);
     p.bt = 1;
-    p.w_col = d->K;                      // [r][s][c][k]: c rows of K (padded) columns
-    p.w_tap = (long)d->C * d->K;
+    // [r][s][c][k]: c rows of K (+ the diagnostic row padding, as
+    // conv_bwd_data_params reads the same copy) columns.  The HWIO-only
+    // forward exists only while the plan picks igemm_nt3 whole: a kernel
+    // option changed after the Session planned (e.g. nt3 = 0) makes this
+    // entry refuse (SEG_EINVAL) -- such filters have no KRSC copy.
+    p.w_col = d->K + g_wpad;
+    p.w_tap = (long)d->C * (d->K + g_wpad);
     return p;
 }
 

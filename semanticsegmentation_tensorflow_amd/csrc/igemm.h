@@ -371,7 +371,7 @@ extern int g_halo_wide;
 extern int g_halo_min_splits;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
-enum { HALO_K1 = 0, HALO_KDUO = 1, HALO_K2 = 2 };   // conv_halo, conv_halo_duo, conv_halo2
+enum { HALO_K1 = 0, HALO_KDUO = 1, HALO_K2 = 2, HALO_K4 = 3 };   // conv_halo, conv_halo_duo, conv_halo2, conv_halo4
 int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype);
 bool halo_unpools(const HaloPlan& hp, int kernel);
 bool halo_pools(const HaloPlan& hp, int kernel);

@@ -20,6 +20,7 @@
 #include <mutex>
 #include "common.h"
 #include "igemm.h"
+#include "halo.h"
 
 namespace seg {
 
@@ -1015,7 +1016,7 @@ const char* nt_choice(const NTParams& p, int dtype, int nphases, int max_m, int*
         case NTK_PRO_REG: return "igemm_nt_pro";
         case NTK_RES16C: return "conv_res16c";
         case NTK_RES64: return "conv_res64";
-        case NTK_HALO: return "conv_halo";
+        case NTK_HALO: return pl.halo_kernel == HALO_K4 ? "conv_halo4" : "conv_halo";
         case NTK_NT3:
         case NTK_NT3_NSPLIT: return "igemm_nt3";
         case NTK_NT2: return "igemm_nt2";

@@ -243,11 +243,19 @@ def _saver_worker(rank, world, port, d, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from semanticsegmentation_tensorflow_amd import tf_bundle
+        from semanticsegmentation_tensorflow_amd.checkpoint import latest_checkpoint
         sess = _SaverSession(rank)
         saver = Saver(max_to_keep=2)
-        paths = [saver.save(sess, os.path.join(d, "model"), global_step=s) for s in (1, 2, 3)]
-        dist.barrier()
-        q.put((rank, paths, sess.syncs))
+        paths, seen = [], []
+        for s in (1, 2, 3):
+            paths.append(saver.save(sess, os.path.join(d, "model"), global_step=s))
+            # save returns on every rank only once rank 0's files
+            # exist -- no barrier of the caller's own before reading them back
+            latest = latest_checkpoint(d)
+            val = tf_bundle.read_bundle(latest, ["c1/weights"])["c1/weights"]
+            seen.append((os.path.basename(latest), float(val.reshape(-1)[0])))
+        q.put((rank, paths, sess.syncs, seen))
     finally:
         dist.destroy_process_group()
 
@@ -255,7 +263,9 @@ def _saver_worker(rank, world, port, d, q):
 def test_dp_world2_saver_every_rank_calls_rank0_writes(tmp_path):
     """every rank calls Saver.save (the slot gather is a
     collective); only rank 0 writes and prunes -- no race on the shared
-    directory, max_to_keep pruning intact, and the files hold rank 0's values."""
+    directory, max_to_keep pruning intact, and the files hold rank 0's values.
+    ADVICE r5: rank 1 reads latest_checkpoint + the bundle right after each
+    save and sees the new step (save ends with a barrier on the group)."""
     from semanticsegmentation_tensorflow_amd import tf_bundle
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -263,11 +273,14 @@ def test_dp_world2_saver_every_rank_calls_rank0_writes(tmp_path):
     procs = [ctx.Process(target=_saver_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = {r: (paths, n) for r, paths, n in (q.get(timeout=120) for _ in range(2))}
+    res = {r: (paths, n, seen) for r, paths, n, seen in (q.get(timeout=120) for _ in range(2))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1] == 3
+    # both ranks, straight after each save: the new checkpoint, rank 0's values
+    for r in (0, 1):
+        assert res[r][2] == [("model-1", 1.0), ("model-2", 1.0), ("model-3", 1.0)], res[r][2]
     kept = sorted(f for f in os.listdir(tmp_path) if f.endswith(".index"))
     assert kept == ["model-2.index", "model-3.index"]
     d = tf_bundle.read_bundle(os.path.join(tmp_path, "model-3"), ["c1/weights", "c1/weights/Adam"])

@@ -312,9 +312,9 @@ def test_c2_kernel_set_is_the_benchmarked_one(c2):
     """The composed paths the bench times are the ones under test."""
     names, sess, plan = c2["kernels"], c2["sess"], c2["plan"]
     print(sorted(names))
-    # conv_halo<bf16,256,256>: conv_halo2 (conv3_x..conv5_x); conv_halo<bf16,256,128>: conv2_x on the
-    # two-blocks-per-CU conv_halo_duo
-    for fam in ("conv_halo<bf16,256,256>", "conv_halo<bf16,256,128>", "conv_res64", "conv_c8", "wgrad_c8",
+    # conv_halo4<bf16,256,256>: conv_halo4 (conv3_x..conv5_x); conv_halo<bf16,256,128>: conv2_x on
+    # the two-blocks-per-CU conv_halo_duo
+    for fam in ("conv_halo4<bf16,256,256>", "conv_halo<bf16,256,128>", "conv_res64", "conv_c8", "wgrad_c8",
                 "wgrad_halo", "igemm_nt3", "igemm_tn3"):
         assert any(n.startswith(fam) for n in names), (fam, names)
     recs = {r["name"]: r for r in sess.capture}

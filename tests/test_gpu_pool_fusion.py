@@ -22,8 +22,8 @@ CASES = [
     (1, 22, 70, 64, 64, "conv_res64"),           # last tile row half outside the image
     (4, 96, 128, 128, 128, "conv_halo<"),        # conv_halo_duo 256 x 128 tiles
     (4, 96, 128, 128, 120, "conv_halo<"),        # N tail (padded columns stay 0)
-    (2, 96, 312, 256, 256, "conv_halo<"),        # conv_halo2, 16 x 16 tiles
-    (9, 40, 96, 256, 256, "conv_halo<"),         # conv_halo2, 8 x 32 tiles
+    (2, 96, 312, 256, 256, "conv_halo4<"),       # conv_halo4, 16 x 16 tiles
+    (9, 40, 96, 256, 256, "conv_halo4<"),        # conv_halo4, 8 x 32 tiles
 ]
 
 

@@ -54,7 +54,7 @@ def test_dgrad_unpool_fused_equals_unfused(dev, case, dtype, relu, residual):
     d, idx, dy, wh, base = _setup(dev, case, dtype, 17)
     assert ops.conv2d_bwd_data_unpool_ok(d), case
     name, splits, _ = ops.conv_kernel_info(d, ops.OP_BWD_DATA)
-    assert name.startswith("conv_halo<") and splits == 1, (name, splits)
+    assert name.startswith("conv_halo") and splits == 1, (name, splits)
     ws = ops.Workspace(dev)
     # unfused: the pooled input gradient (+ the other consumers' sum in place), then MaxPoolGrad
     dxp = base.clone() if residual else torch.full((N, H, W, C), float("nan"), dtype=dtype, device=dev)
