@@ -310,8 +310,23 @@ class PlanMixin:
                 # forward reads the HWIO copy the input gradient reads
                 # (ops.conv2d_fwd_hwio), and its fused filter-gradient + Adam
                 # launch has no KRSC copy to rewrite
-                n.fwd_hwio = (self.fwd_hwio and getattr(n, "pro", None) is None and R * S * C * K >= (1 << 23)
-                              and ops.conv2d_fwd_hwio_ok(n.desc))
+                # The choice is sticky per filter: once a plan made it HWIO-only,
+                # every later plan (another batch size, an inference plan) that
+                # can read the HWIO copy does, so no KRSC copy appears that
+                # each training step's update would then rewrite.  A later
+                # plan whose shape igemm_nt3 does not take
+                # (conv2d_fwd_hwio_ok false) still adds the KRSC copy, and
+                # the filter leaves the HWIO-only set
+                # (tests/test_session_dryrun.py::test_hwio_only_filter_stays_single_copy).
+                hwio_only = store.hwio_only
+                name = n.w.var_name
+                n.fwd_hwio = (getattr(n, "pro", None) is None and ops.conv2d_fwd_hwio_ok(n.desc)
+                              and (name in hwio_only or (self.fwd_hwio and R * S * C * K >= (1 << 23)
+                                                         and (name, ops.PACK_KRSC) not in store.packed)))
+                if n.fwd_hwio:
+                    hwio_only.add(name)
+                else:
+                    hwio_only.discard(name)
                 if not n.fwd_hwio:
                     p.packs.add((n.w.var_name, ops.PACK_KRSC))
                 if id(x) in p.needs_grad or n.fwd_hwio:

@@ -83,6 +83,7 @@ class VariableStore:
         self.order = order
         self.step = 0           # Adam t (TF beta powers)
         self.packed = {}        # (var_name, mode) -> (tensor, a_pad, b_pad)
+        self.hwio_only = set()  # filters whose forward reads the HWIO copy (no KRSC copy; planner.py)
         self.version = 0        # bumped on every update -> repack
 
     def _view(self, buf, name):

@@ -24,7 +24,7 @@ class _Rec:
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
                              "seg_adam_segments_plan", "seg_tconv_filter_apad",
                              "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace",
-                             "seg_conv2d_fwd_pool_ok", "seg_conv2d_fwd_bn2_ok")
+                             "seg_conv2d_fwd_pool_ok", "seg_conv2d_fwd_bn2_ok", "seg_conv2d_fwd_hwio_ok")
 
         def fn(*a):
             if host_only:
@@ -63,7 +63,9 @@ def test_fcn_train_plan(dry):
     # forward: 17 fused conv launches, 3 tconv, 5 pools, 1 loss; a pool whose
     # conv's kernel has the pooled epilogue runs inside that conv's launch
     fused = c.count("seg_conv2d_fwd_pool")
-    assert c.count("seg_conv2d_fwd") + fused == 17
+    # conv6 / conv7 read their one (HWIO) packed copy
+    assert c.count("seg_conv2d_fwd_hwio") == 2
+    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_hwio") + fused == 17
     assert c.count("seg_tconv2d_fwd") == 3
     # train plans record the pool switches; MaxPoolGrad reads them instead of x
     assert c.count("seg_maxpool2x2_fwd_argmax") + fused == 5
@@ -82,9 +84,10 @@ def test_fcn_train_plan(dry):
     # skip fusion: pool3/pool4 gradients = sum of two consumers, the second
     # accumulated in its input-gradient epilogue (no separate add)
     assert c.count("seg_add") == 0
-    # filter copies are packed once per update (first run) -- KRSC for all 17 convs,
-    # HWIO for the 16 with input grads, 2 layouts x 3 tconvs
-    assert c.count("seg_pack_filter") == 17 + 16 + 6
+    # filter copies are packed once per update (first run) -- KRSC for the 15 convs
+    # below 8 M elements, HWIO for the 16 with input grads (conv6 / conv7 HWIO
+    # only), 2 layouts x 3 tconvs
+    assert c.count("seg_pack_filter") == 15 + 16 + 6
     assert c.index("seg_adam_tf1_pack") > c.index("seg_conv2d_bwd_filter")
     dry.calls.clear()
     sess.run(train, feed_dict={image: img, labels: lab, keep: 1.0})
@@ -97,7 +100,8 @@ def test_fcn_train_plan(dry):
     (gk, plan), = sess._adam_groups.items()
     assert plan.nsegs == len(sess.store.vars) - 2
     assert "conv6/weights" not in gk[1] and "conv7/weights" not in gk[1]
-    assert dry.calls.count("seg_conv2d_fwd") + dry.calls.count("seg_conv2d_fwd_pool") == 17
+    assert (dry.calls.count("seg_conv2d_fwd") + dry.calls.count("seg_conv2d_fwd_pool")
+            + dry.calls.count("seg_conv2d_fwd_hwio")) == 17
 
 
 def test_adam_segment_plan_host():
@@ -125,6 +129,40 @@ def test_inference_plan_has_no_backward(dry):
     sess.run(pred, feed_dict={image: np.zeros((1, 64, 96, 3), np.float32)})
     assert "seg_conv2d_bwd_data" not in dry.calls
     assert dry.calls.count("seg_argmax") == 1
+
+
+def test_hwio_only_filter_stays_single_copy(dry):
+    """FCN conv6 / conv7 (>= 8 M elements) keep ONE packed bf16 copy: the
+    training plan reads their HWIO copy in the forward (seg_conv2d_fwd_hwio).
+    A second plan at another batch size and an inference plan of the same
+    Session reuse that choice, so the store never gains a KRSC copy that every
+    later training step's update would rewrite (planner.py)."""
+    G.reset_default_graph()
+    H, W = 64, 96
+    image = tf.placeholder(tf.float32, [None, H, W, 3])
+    labels = tf.placeholder(tf.uint8, [None, H, W])
+    keep = tf.placeholder(tf.float32)
+    pred, logits = FCN(image, keep, 2).create()
+    loss = tf.reduce_mean(tf.nn.softmax_cross_entropy_with_logits(logits=logits, labels=labels))
+    train = tf.train.AdamOptimizer(1e-4).minimize(loss)
+    sess = S.Session(device=torch.device("cpu"), compute_dtype="bf16")
+    sess.run(tf.global_variables_initializer())
+    big = {n for n, v in sess.store.by_name.items() if len(v.shape) == 4 and int(np.prod(v.shape)) >= (1 << 23)}
+    assert len(big) == 2, big           # conv6, conv7
+
+    def packs():
+        return {k for k in sess.store.packed if k[0] in big}
+    sess.run(train, feed_dict={image: np.zeros((4, H, W, 3), np.float32),
+                               labels: np.zeros((4, H, W), np.uint8), keep: 0.8})
+    first = packs()
+    assert first == {(n, ops.PACK_HWIO) for n in big}, first
+    assert sess.store.hwio_only == big
+    dry.calls.clear()
+    sess.run(train, feed_dict={image: np.zeros((1, H, W, 3), np.float32),
+                               labels: np.zeros((1, H, W), np.uint8), keep: 0.8})
+    sess.run(pred, feed_dict={image: np.zeros((1, H, W, 3), np.float32), keep: 1.0})
+    assert packs() == first
+    assert dry.calls.count("seg_conv2d_fwd_hwio") >= 4
 
 
 def test_tconv_shape_rule_at_375x1242(dry):
