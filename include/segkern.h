@@ -283,10 +283,16 @@ size_t seg_conv_workspace(const seg_conv_desc* d, int op);
 int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, int len, int* splits,
                          double* flops);
 
-/* Tuning knobs (host-only): "igemm_nt_variant" / "igemm_tn_variant" = 1
- * (register-staged 128-row tiles) or 2 (LDS-DMA 3-stage ring, 256-wide
- * tiles, 8 waves; default). */
+/* Kernel-selection knobs (host-only): the library's only mutable state, one
+ * set per HIP device (the tuned defaults until changed; SURVEY.md 8b:
+ * "stateless apart from a mutex-guarded, per-device tuned-config cache").
+ * seg_set_option validates the value, then writes the calling thread's current
+ * device's set under a mutex; every later launch on that device reads it.
+ * No reference interface: TensorFlow's kernels pick their algorithms
+ * internally (Network/ never selects one).  Returns SEG_EINVAL for an unknown
+ * name or a value outside the knob's parity-tested set. */
 int seg_set_option(const char* name, int value);
+int seg_get_option(const char* name, int* value);
 
 /* ---- filter packing: fp32 master -> compute copy ----------------------- */
 /* src: fp32 master [R][S][A][B] with A=a_valid, B=b_valid; dst (dtype,

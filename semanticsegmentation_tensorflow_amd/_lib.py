@@ -172,6 +172,7 @@ SIGNATURES = {
     "seg_softmax": (_I, [_P, _I, _I, _L, _P, _I, _I, _P]),
     "seg_conv2d_bwd_filter_adam": (_I, [_DP, _P, _P, _P, _P, ctypes.POINTER(SegAdamFused), _P, _Z, _P]),
     "seg_set_option": (_I, [ctypes.c_char_p, _I]),
+    "seg_get_option": (_I, [ctypes.c_char_p, ctypes.POINTER(_I)]),
     "seg_timing_event_create": (_I, [ctypes.POINTER(ctypes.c_void_p)]),
     "seg_timing_event_record": (_I, [_P, _P]),
     "seg_timing_event_elapsed_ms": (_I, [ctypes.POINTER(ctypes.c_float), _P, _P]),

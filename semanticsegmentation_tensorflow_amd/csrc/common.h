@@ -5,6 +5,7 @@
 #include <algorithm>
 
 #include "../../include/segkern.h"
+#include "knobs.h"
 
 typedef __bf16 bf16;
 typedef _Float16 f16;

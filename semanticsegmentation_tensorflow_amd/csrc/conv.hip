@@ -4,6 +4,7 @@
 #include "common.h"
 #include "igemm.h"
 #include "halo.h"
+#include <mutex>
 #include <stdio.h>
 #include <string.h>
 #include <math.h>
@@ -112,7 +113,6 @@ static seg::EpiParams make_epi(const seg_epilogue* e, int n_valid, long res_img,
 // ---------------------------------------------------------------------------
 // diagnostics only: extra elements of row padding in the packed KRSC (fwd) /
 // HWIO (dgrad) filter copies the caller allocated (L2 channel-stride probe)
-static int g_wpad = 0;
 
 static NTParams conv_fwd_params(const seg_conv_desc* d) {
     NTParams p = {};
@@ -352,7 +352,7 @@ extern "C" size_t seg_conv_workspace(const seg_conv_desc* d, int op) {
             TNParams p = conv_bwd_filter_params(d);
             size_t need = seg::tn_workspace(p.M, p.N, p.P, d->dtype);
             seg::WgradPlan wp;
-            if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp))
+            if (g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp))
                 need = std::max(need, seg::wgrad_workspace(wp, p));
             if (seg::smallc_wgrad_ok(p, d->dtype))
                 need = std::max(need, (size_t)seg::smallc_wgrad_splits(p, seg::device_cus()) * (p.M + 1) * p.N *
@@ -418,11 +418,11 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             seg::WgradPlan wp;
             if (seg::smallc_wgrad_ok(p, d->dtype)) {
                 fam = "wgrad_c8"; bm = 72; bn = p.N; sp = seg::smallc_wgrad_splits(p, seg::device_cus());
-            } else if (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
+            } else if (g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp)) {
                 fam = "wgrad_halo"; bm = 576; bn = wp.nt; sp = wp.splits;
-            } else if (seg::g_tn_variant == 2 && seg::tn3_ok(p, d->dtype)) {
+            } else if (g_tn_variant == 2 && seg::tn3_ok(p, d->dtype)) {
                 fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(p.M, p.N, p.P, seg::device_cus(), &sp);
-            } else if (seg::g_tn_variant == 2 && d->dtype != SEG_F32 && p.M >= 128) {
+            } else if (g_tn_variant == 2 && d->dtype != SEG_F32 && p.M >= 128) {
                 fam = "igemm_tn2";
             }
             macs = macs_conv;
@@ -457,8 +457,8 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
         case 5: {
             const int Mt = tconv_dense_kq(d) ? d->R * d->S * tconv_dense_kq(d) : d->R * d->S * d->K;
             seg::tn_info(Mt, d->C, d->N * d->H * d->W, d->dtype, &bm, &bn, &sp);
-            fam = (seg::g_tn_variant == 2 && d->dtype != SEG_F32 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
-            if (seg::g_tn_variant == 2 && seg::tn3_applies(Mt, d->C, d->dtype)) {
+            fam = (g_tn_variant == 2 && d->dtype != SEG_F32 && Mt >= 128) ? "igemm_tn2" : "igemm_tn";
+            if (g_tn_variant == 2 && seg::tn3_applies(Mt, d->C, d->dtype)) {
                 fam = "igemm_tn3"; bm = bn = 256; seg::tn3_info(Mt, d->C, d->N * d->H * d->W, seg::device_cus(), &sp);
             }
             macs = macs_t;
@@ -479,7 +479,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             macs = macs_conv;
             if (seg::s1x1_ok(p, d->dtype, 1)) {
                 fam = "conv1x1_stream"; bm = 128; bn = 64;
-            } else if (seg::g_nt_variant == 2 && seg::nt2_pro_ok(p, d->dtype, 1)) {
+            } else if (g_nt_variant == 2 && seg::nt2_pro_ok(p, d->dtype, 1)) {
                 fam = "igemm_nt2_pro"; bm = 192; bn = p.N <= 64 ? 64 : 128;
             } else {
                 fam = "igemm_nt_pro"; bm = 128; bn = p.N <= 64 ? 64 : 128;
@@ -490,7 +490,7 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
             TNParams p = conv_bwd_filter_params(d);
             macs = macs_conv;
             seg::tn_info(p.M, p.N, p.P, d->dtype, &bm, &bn, &sp);
-            fam = (d->dtype != SEG_F32 && seg::g_tn_variant == 2 && p.M == p.Cg) ? "igemm_tn2_pro" : "igemm_tn_pro";
+            fam = (d->dtype != SEG_F32 && g_tn_variant == 2 && p.M == p.Cg) ? "igemm_tn2_pro" : "igemm_tn_pro";
             break;
         }
         default: return SEG_EINVAL;
@@ -501,10 +501,6 @@ extern "C" int seg_conv_kernel_info(const seg_conv_desc* d, int op, char* name, 
     return SEG_OK;
 }
 
-int g_adam_tr_fused = 0;   // 1: the fused epilogue also writes the KRSC copy (transposed 16-byte stores)
-
-extern int g_adam_blocks;   // optim.hip
-
 // Kernel-selection knobs (A/B runs and the variant parity tests): every value
 // an entry accepts selects a parity-tested kernel or schedule.  The ablation
 // modes behind kernel diagnostics (no DMA / no MFMA / no stores: garbage
@@ -513,79 +509,103 @@ extern int g_adam_blocks;   // optim.hip
 namespace {
 struct Knob {
     const char* name;
-    int* var;
+    std::atomic<int> seg::KnobSet::*var;
     int lo, hi;        // accepted range ...
     int step;          // ... in multiples of step (0: any listed in `only`)
     int only[8];
 };
-}  // namespace
 
-extern "C" int seg_set_option(const char* name, int value) {
-    if (!name) return SEG_EINVAL;
+std::mutex g_knob_mu;   // serialises seg_set_option writers
+
+const Knob* find_knob(const char* name) {
     static const Knob knobs[] = {
-        {"igemm_nt_variant", &seg::g_nt_variant, 1, 2, 1, {}},
-        {"igemm_tn_variant", &seg::g_tn_variant, 1, 2, 1, {}},
-        {"tn_nsplit", &seg::g_tn_nsplit, 0, 1, 1, {}},
-        {"nt_nsplit", &seg::g_nt_nsplit, 0, 1, 1, {}},
-        {"halo_duo", &seg::g_halo_duo, 0, 1, 1, {}},
-        {"nt_halo", &seg::g_nt_halo, 0, 1, 1, {}},
-        {"halo_wide", &seg::g_halo_wide, 0, 1, 1, {}},
-        {"halo4", &seg::g_halo4, 0, 5, 1, {}},
-        {"halo_min_splits", &seg::g_halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
-        {"adam_tr_fused", &g_adam_tr_fused, 0, 1, 1, {}},
-        {"nt2_short", &seg::g_nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
-        {"tn_fill", &seg::g_tn_fill, 1, 64, 1, {}},                   // filter-gradient split-K target, blocks/CU
-        {"tn_split_cap", &seg::g_tn_split_cap, 1, 4096, 1, {}},
-        {"tn_reduce_sl", &seg::g_tn_reduce_sl, 0, 0, 0, {1, 2, 4, 8, 16, 32, 64}},
-        {"tn2_smallm", &seg::g_tn2_smallm, 0, 1, 1, {}},
-        {"adam_blocks", &g_adam_blocks, 0, 1 << 30, 1, {}},           // grid cap of seg_adam_tf1_pack (0: per tile)
-        {"nt3_fill", &seg::g_nt3_fill, 0, 1, 1, {}},
-        {"tn3_stagger_us", &seg::g_tn3_stagger_us, 0, 1000, 1, {}},
-        {"s1x1", &seg::g_s1x1, 0, 1, 1, {}},
-        {"tn3_half", &seg::g_tn3_half, 0, 7, 1, {}},
-        {"tn3_mfast", &seg::g_tn3_mfast, 0, 1, 1, {}},
-        {"tn3", &seg::g_tn3, 0, 1, 1, {}},
-        {"nt3", &seg::g_nt3, 0, 1, 1, {}},
-        {"wgrad_fill", &seg::g_wgrad_fill, 1, 800, 1, {}},            // filter-gradient split-K, % of the CUs
-        {"wgrad_nt32", &seg::g_wgrad_nt32, 0, 1, 1, {}},
-        {"wgrad_nbias", &seg::g_wgrad_nbias, 1, 4, 1, {}},
-        {"wgrad_nt", &seg::g_wgrad_nt, 0, 0, 0, {64, 128}},
-        {"wgrad_halo", &seg::g_wgrad_halo, 0, 1, 1, {}},
-        {"res16c", &seg::g_res16c, 0, 1, 1, {}},
-        {"res16", &seg::g_res16, 0, 1, 1, {}},
-        {"res64", &seg::g_res64, 0, 1, 1, {}},
-        {"res64_pp", &seg::g_res64_pp, 0, 2, 1, {}},
-        {"res16_dma", &seg::g_res16_dma, 0, 1, 1, {}},
-        {"res16c_bh", &seg::g_res16c_bh, 0, 0, 0, {4, 8}},
-        {"bn1x1s", &seg::g_bn1x1s, 0, 1, 1, {}},
-        {"s1x1_st", &seg::g_s1x1_st, 0, 2, 1, {}},
-        {"res16c_st", &seg::g_res16c_st, 0, 1, 1, {}},
-        {"dropout_flat", &seg::g_dropout_flat, 0, 1, 1, {}},
-        {"smallc", &seg::g_smallc, 0, 1, 1, {}},
-        {"smallk", &seg::g_smallk, 0, 1, 1, {}},
-        {"wpad", &g_wpad, 0, 256, 8, {}},
+        {"igemm_nt_variant", &seg::KnobSet::nt_variant, 1, 2, 1, {}},
+        {"igemm_tn_variant", &seg::KnobSet::tn_variant, 1, 2, 1, {}},
+        {"tn_nsplit", &seg::KnobSet::tn_nsplit, 0, 1, 1, {}},
+        {"nt_nsplit", &seg::KnobSet::nt_nsplit, 0, 1, 1, {}},
+        {"halo_duo", &seg::KnobSet::halo_duo, 0, 1, 1, {}},
+        {"nt_halo", &seg::KnobSet::nt_halo, 0, 1, 1, {}},
+        {"halo_wide", &seg::KnobSet::halo_wide, 0, 1, 1, {}},
+        {"halo4", &seg::KnobSet::halo4, 0, 2, 1, {}},         // 2: conv_halo4 8 waves, 1: 4 waves, 0: conv_halo2
+        {"halo_min_splits", &seg::KnobSet::halo_min_splits, 1, 64, 1, {}},   // force split-K in the halo planner
+        {"adam_tr_fused", &seg::KnobSet::adam_tr_fused, 0, 1, 1, {}},
+        {"nt2_short", &seg::KnobSet::nt2_short, 0, 64, 1, {}},                // max k tiles of the 2-stage igemm_nt2
+        {"tn_fill", &seg::KnobSet::tn_fill, 1, 64, 1, {}},                   // filter-gradient split-K target, blocks/CU
+        {"tn_split_cap", &seg::KnobSet::tn_split_cap, 1, 4096, 1, {}},
+        {"tn_reduce_sl", &seg::KnobSet::tn_reduce_sl, 0, 0, 0, {1, 2, 4, 8, 16, 32, 64}},
+        {"tn2_smallm", &seg::KnobSet::tn2_smallm, 0, 1, 1, {}},
+        {"adam_blocks", &seg::KnobSet::adam_blocks, 0, 1 << 30, 1, {}},           // grid cap of seg_adam_tf1_pack (0: per tile)
+        {"nt3_fill", &seg::KnobSet::nt3_fill, 0, 1, 1, {}},
+        {"tn3_stagger_us", &seg::KnobSet::tn3_stagger_us, 0, 1000, 1, {}},
+        {"s1x1", &seg::KnobSet::s1x1, 0, 1, 1, {}},
+        {"tn3_half", &seg::KnobSet::tn3_half, 0, 7, 1, {}},
+        {"tn3_mfast", &seg::KnobSet::tn3_mfast, 0, 1, 1, {}},
+        {"tn3", &seg::KnobSet::tn3, 0, 1, 1, {}},
+        {"nt3", &seg::KnobSet::nt3, 0, 1, 1, {}},
+        {"wgrad_fill", &seg::KnobSet::wgrad_fill, 1, 800, 1, {}},            // filter-gradient split-K, % of the CUs
+        {"wgrad_nt32", &seg::KnobSet::wgrad_nt32, 0, 1, 1, {}},
+        {"wgrad_nbias", &seg::KnobSet::wgrad_nbias, 1, 4, 1, {}},
+        {"wgrad_nt", &seg::KnobSet::wgrad_nt, 0, 0, 0, {64, 128}},
+        {"wgrad_halo", &seg::KnobSet::wgrad_halo, 0, 1, 1, {}},
+        {"res16c", &seg::KnobSet::res16c, 0, 1, 1, {}},
+        {"res16", &seg::KnobSet::res16, 0, 1, 1, {}},
+        {"res64", &seg::KnobSet::res64, 0, 1, 1, {}},
+        {"res64_pp", &seg::KnobSet::res64_pp, 0, 2, 1, {}},
+        {"res16_dma", &seg::KnobSet::res16_dma, 0, 1, 1, {}},
+        {"res16c_bh", &seg::KnobSet::res16c_bh, 0, 0, 0, {4, 8}},
+        {"bn1x1s", &seg::KnobSet::bn1x1s, 0, 1, 1, {}},
+        {"s1x1_st", &seg::KnobSet::s1x1_st, 0, 2, 1, {}},
+        {"res16c_st", &seg::KnobSet::res16c_st, 0, 1, 1, {}},
+        {"dropout_flat", &seg::KnobSet::dropout_flat, 0, 1, 1, {}},
+        {"smallc", &seg::KnobSet::smallc, 0, 1, 1, {}},
+        {"smallk", &seg::KnobSet::smallk, 0, 1, 1, {}},
+        {"wpad", &seg::KnobSet::wpad, 0, 256, 8, {}},
 #ifdef SEG_DIAG
-        {"tn3_abl", &seg::g_tn3_abl, 0, 3, 1, {}},
-        {"smallk_abl", &seg::g_smallk_abl, 0, 3, 1, {}},
-        {"tn3_adam_abl", &seg::g_tn3_adam_abl, 0, 31, 1, {}},
-        {"wgrad_abl", &seg::g_wgrad_abl, 0, 3, 1, {}},
-        {"nt2_ablate", &seg::g_nt2_ablate, 0, 19, 1, {}},
+        {"tn3_abl", &seg::KnobSet::tn3_abl, 0, 3, 1, {}},
+        {"smallk_abl", &seg::KnobSet::smallk_abl, 0, 3, 1, {}},
+        {"tn3_adam_abl", &seg::KnobSet::tn3_adam_abl, 0, 31, 1, {}},
+        {"wgrad_abl", &seg::KnobSet::wgrad_abl, 0, 3, 1, {}},
+        {"nt2_ablate", &seg::KnobSet::nt2_ablate, 0, 19, 1, {}},
 #endif
     };
-    for (const Knob& k : knobs) {
-        if (strcmp(name, k.name)) continue;
-        bool ok;
-        if (k.step) {
-            ok = value >= k.lo && value <= k.hi && (value - k.lo) % k.step == 0;
-        } else {
-            ok = false;
-            for (int v : k.only) ok = ok || (v != 0 && v == value);
-        }
-        if (!ok) return SEG_EINVAL;
-        *k.var = value;
-        return SEG_OK;
+    for (const Knob& k : knobs)
+        if (!strcmp(name, k.name)) return &k;
+    return nullptr;
+}
+}  // namespace
+
+namespace seg {
+KnobSet& knobs() {
+    constexpr int MAXDEV = 64;
+    static KnobSet sets[MAXDEV];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAXDEV) d = 0;
+    return sets[d];
+}
+}  // namespace seg
+
+// Sets one knob for the calling thread's current device (see knobs.h).
+extern "C" int seg_set_option(const char* name, int value) {
+    const Knob* k = name ? find_knob(name) : nullptr;
+    if (!k) return SEG_EINVAL;
+    bool ok;
+    if (k->step) {
+        ok = value >= k->lo && value <= k->hi && (value - k->lo) % k->step == 0;
+    } else {
+        ok = false;
+        for (int v : k->only) ok = ok || (v != 0 && v == value);
     }
-    return SEG_EINVAL;
+    if (!ok) return SEG_EINVAL;
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    (seg::knobs().*(k->var)).store(value, std::memory_order_relaxed);
+    return SEG_OK;
+}
+
+extern "C" int seg_get_option(const char* name, int* value) {
+    const Knob* k = name ? find_knob(name) : nullptr;
+    if (!k || !value) return SEG_EINVAL;
+    *value = (seg::knobs().*(k->var)).load(std::memory_order_relaxed);
+    return SEG_OK;
 }
 
 extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
@@ -959,7 +979,7 @@ extern "C" int seg_conv2d_bwd_filter_begin(const seg_conv_desc* d, const void* x
     p.x = x; p.b = dy; p.out = dw; p.dbias = dbias;
     seg::WgradPlan wp;
     const bool fuses_bias = seg::smallc_wgrad_ok(p, d->dtype) ||
-                            (seg::g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp));
+                            (g_tn_variant == 2 && seg::wgrad_plan(p, d->dtype, seg::device_cus(), &wp));
     if (dbias && !fuses_bias) {          // reduce it now, while the workspace is free
         st = bias_grad_fallback(d, dy, dbias, ws, ws_bytes, stream);
         if (st) return st;
@@ -989,7 +1009,7 @@ extern "C" int seg_conv2d_bwd_filter_end(const seg_conv_desc* d, float* dw, floa
 }
 
 static bool wgrad_adam_params(const seg_conv_desc* d, TNParams* out) {
-    if (check_desc(d) || d->dtype != SEG_BF16 || seg::g_tn_variant != 2) return false;
+    if (check_desc(d) || d->dtype != SEG_BF16 || g_tn_variant != 2) return false;
     TNParams p = conv_bwd_filter_params(d);
     if (seg::smallc_wgrad_ok(p, d->dtype)) return false;
     seg::WgradPlan wp;
@@ -1069,7 +1089,7 @@ extern "C" int seg_conv2d_bwd_filter_adam(const seg_conv_desc* d, const void* x,
     p.adam.gs = a->grad_scale;
     p.adam.store_grad = dw != nullptr;
 #ifdef SEG_DIAG
-    p.adam.abl = seg::g_tn3_adam_abl;
+    p.adam.abl = g_tn3_adam_abl;
 #endif
     p.Mp = p.M;
     p.partial = nullptr;

@@ -24,7 +24,6 @@
 
 namespace seg {
 
-int g_s1x1 = 1;
 static __device__ uint4 s1_zero[4];
 static __device__ uint2 s1_trash[64 * 64];
 
@@ -423,7 +422,6 @@ bool s1x1_ok(const NTParams& p, int dtype, int nphases) {
 
 // The 1x1 input gradient through the BN backward on bn1x1_dgrad_stream: K = 64
 // (the bottleneck's 4 * growth filters), dense 1x1 stride-1 geometry, 16-bit.
-int g_bn1x1s = 1;
 
 // geometry (from the descriptor alone: it also fixes the partial-row count)
 bool bn1x1s_ok(const NTParams& p, int dtype) {
@@ -467,7 +465,6 @@ int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s) {
 // staged 16-byte output stores: 0 never, 1 for single-k-tile launches (C <= 64:
 // write-dominated, 393 vs 475 us at 384x1248x8, C = 48; C3 212 -> 213.5 img/s),
 // 2 always (C = 128 / 144: 1-4 % slower)
-int g_s1x1_st = 1;
 
 template <typename T, bool PRO>
 static void launch_s1x1_t(NTParams& p, int grid, int ntiles, int kt, bool st, hipStream_t s) {

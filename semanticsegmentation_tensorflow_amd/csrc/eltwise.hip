@@ -1283,7 +1283,6 @@ extern "C" int seg_dropout_bwd(const void* dy, void* dx, long n, float kp, uint6
 }
 
 namespace seg {
-int g_dropout_flat = 1;   // dropout re-draw: one chunk per thread (0: the grid-stride loop)
 }
 
 extern "C" int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, long P, int C, int cv, float kp,
@@ -1292,7 +1291,7 @@ extern "C" int seg_dropout_bwd_ch(const void* dy, int ldy, void* dz, int ldz, lo
     if (C > 4096) return SEG_EINVAL;
     const RedGeom g = red_geom(C, epc_of(dtype));
     const long chunks = P * (long)g.CK;
-    if (seg::g_dropout_flat && chunks < (1L << 31) - 256) {
+    if (g_dropout_flat && chunks < (1L << 31) - 256) {
         const int CK = g.CK;
         DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_ch_flat_k<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                                              (hipStream_t)stream, (const T*)dy, ldy, (T*)dz, ldz, (int)P, CK, cv, kp,

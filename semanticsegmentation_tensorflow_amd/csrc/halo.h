@@ -76,7 +76,6 @@ __device__ __forceinline__ void pool_epi_rows(const NTParams& p, const char* wbu
 }
 
 // conv_halo4 (halo4.hip): 256 x 256 plans at one wave per SIMD
-extern int g_halo4;
 bool halo4_ok(const NTParams& p, const HaloPlan& hp);
 void launch_halo4(NTParams& p, const HaloPlan& hp, const HaloGeom& g, hipStream_t s, int dtype);
 

@@ -35,19 +35,9 @@ namespace seg {
 
 static __device__ uint4 halo_zero_page[4];
 
-int g_nt_halo = 1;
-int g_halo_wide = 1;
-int g_res64 = 1;
-int g_res16 = 1;        // conv_res64 with 16-wide output blocks for N <= 16
 // 64-wide blocks on the two-group ping-pong conv_res64pp: 0 never, 1 for the
 // pooled forward and the ReluGrad-masked input gradient (conv1_2: 191 vs 192
 // and 259 vs 277 us; the plain forward measured 214 vs 202 on it), 2 always
-int g_res64_pp = 1;
-int g_res16_dma = 1;
-int g_res16c_bh = 4;   // tile rows of the BN-backward conv_res16c (8 or 4)
-int g_res16c = 1;       // conv_res16c: 16 input channels (growth-conv input gradients)
-int g_halo_duo = 1;     // N <= 128 without split-K: conv_halo_duo (two blocks per CU)
-int g_halo_min_splits = 1;   // at least this many split-K slabs (tests: a split plan on any shape)
 
 
 
@@ -1964,7 +1954,6 @@ int res16c_grid(const NTParams& p, int cus) {
 
 // staged 16-byte dx stores in the BN-backward form: 403 -> 336 us at
 // 384x1248x8, C3 213 -> 215.8 img/s (0: 8-byte stores from the accumulators)
-int g_res16c_st = 1;
 
 template <typename T, int BH>
 static void launch_res16c_bn_t(NTParams& p, int grid, hipStream_t s) {

@@ -42,7 +42,6 @@ namespace seg {
 
 static __device__ uint4 h4_zero_page[4];
 
-int g_halo4 = 2;   // 256 x 256 halo plans on conv_halo4: 2 = 8 waves (default), 1 = 4 waves, 0 = conv_halo2
 
 // Geometry per wave count: NW = 4 (one wave per SIMD, 128 px x 128 ch per
 // wave) or NW = 8 (two waves per SIMD, 128 px x 64 ch: one wave's DMA /
@@ -65,11 +64,12 @@ template <int NW> struct H4Geo {
 // ABL (diagnostic builds, garbage results; tools/kbench.py --opts nt2_ablate=1N):
 // 1 no barrier in the loop, 2 no end-of-step waits, 3 no DMA in the loop,
 // 4 no fragment reads, 5 no MFMA, 6 no barrier and no waits.
-// VAR (NW = 8 schedule experiments): bit 0 -- the wm = 1 waves (the second
-// wave of each SIMD) issue their filter DMA in half-1 groups 4-7 and their
-// halo pieces in half-2 groups 5-6, so the two waves of a SIMD do not stall on
-// DMA issue together; bit 1 -- s_setprio 1 around each MFMA group.
-template <int BW, int NW, typename T = bf16, bool UNP = false, int ABL = 0, int VAR = 0>
+// (Measured within noise and removed in round 6: the second wave of each
+// SIMD issuing its DMA in other MFMA groups than the first, s_setprio around
+// each MFMA group, fragment reads placed between the MFMAs of a group; the
+// same tile on 32x32x16 MFMAs -- 4.6 % fewer wave cycles but a 3 % lower
+// clock, 2-5 % slower per launch.)
+template <int BW, int NW, typename T = bf16, bool UNP = false, int ABL = 0>
 __global__ __launch_bounds__(NW * 64) void conv_halo4(NTParams p, HaloGeom g) {
     using G = H4Geo<NW>;
     constexpr int BM = 256, BN = 256, BH = BM / BW;
@@ -212,31 +212,6 @@ __global__ __launch_bounds__(NW * 64) void conv_halo4(NTParams p, HaloGeom g) {
             else aa[k - NF] = rd(va, a_imm(k - NF));
         }
     };
-    // VAR & 4: the group's MFMAs with its fragment reads placed between them
-    // (one read after every NF / 2 MFMAs) instead of after the whole group
-    auto group = [&](auto q_tag, const uint4& af, const uint4* bf, f32x4* ac, uint4* aa, uint4* bb, unsigned va,
-                     unsigned vb) __attribute__((always_inline)) {
-        constexpr int Q = decltype(q_tag)::value;
-        int r = 0;
-#pragma unroll
-        for (int ni = 0; ni < NF; ++ni) {
-            mma(af, bf[ni], ac[ni]);
-            if (ni % (NF / 2) == NF / 2 - 1) {
-                __builtin_amdgcn_sched_barrier(0);
-                int seen = 0;
-#pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    if (k * 8 / NR != Q) continue;
-                    if (seen++ != r) continue;
-                    if (k < NF) bb[k] = rd(vb, k * 2048);
-                    else aa[k - NF] = rd(va, a_imm(k - NF));
-                }
-                ++r;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    };
-
     // one (tap, chunk) step; FIRST: no ks1 of a previous slice to finish
     auto step = [&](auto first_tag) __attribute__((always_inline)) {
         constexpr bool FIRST = decltype(first_tag)::value;
@@ -261,26 +236,14 @@ __global__ __launch_bounds__(NW * 64) void conv_halo4(NTParams p, HaloGeom g) {
         };
         auto half1 = [&](auto q_tag) __attribute__((always_inline)) {
             constexpr int Q = decltype(q_tag)::value;
-            if constexpr (VAR & 4) {
-                if constexpr (!FIRST) group(q_tag, a1[Q], b1, acc[Q], a0, b0, va0, vb0);
-                else reads(q_tag, a0, b0, va0, vb0);
-            } else {
-                if constexpr (!FIRST) {
-                    if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(1);
+            if constexpr (!FIRST) {
 #pragma unroll
-                    for (int ni = 0; ni < NF; ++ni) mma(a1[Q], b1[ni], acc[Q][ni]);
-                    if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                reads(q_tag, a0, b0, va0, vb0);
+                for (int ni = 0; ni < NF; ++ni) mma(a1[Q], b1[ni], acc[Q][ni]);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ABL != 3 && (VAR & 1)) {
-                if (Q < 4 && wm == 0) issue_b(std::integral_constant<int, Q % 4>{});
-                if (Q >= 4 && wm == 1) issue_b(std::integral_constant<int, Q % 4>{});
-            } else if constexpr (ABL != 3 && Q < 4) {
-                issue_b(q_tag);
-            }
+            reads(q_tag, a0, b0, va0, vb0);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL != 3 && Q < 4) issue_b(q_tag);
             __builtin_amdgcn_sched_barrier(0);
         };
         half1(std::integral_constant<int, 0>{});
@@ -299,23 +262,12 @@ __global__ __launch_bounds__(NW * 64) void conv_halo4(NTParams p, HaloGeom g) {
         const int nh = hp ? max(0, min(G::HPT, h_n - h0)) : 0;
         auto half2 = [&](auto q_tag) __attribute__((always_inline)) {
             constexpr int Q = decltype(q_tag)::value;
-            if constexpr (VAR & 4) {
-                group(q_tag, a0[Q], b0, acc[Q], a1, b1, va1, vb1);
-            } else {
-                if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int ni = 0; ni < NF; ++ni) mma(a0[Q], b0[ni], acc[Q][ni]);
-                if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-                reads(q_tag, a1, b1, va1, vb1);
-            }
+            for (int ni = 0; ni < NF; ++ni) mma(a0[Q], b0[ni], acc[Q][ni]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ABL != 3 && (VAR & 1)) {
-                constexpr int QQ = Q % 4;
-                if (QQ >= 1 && QQ <= G::HPT && (Q < 4) == (wm == 0)) {
-                    if (QQ - 1 < nh) load_halo(h0 + QQ - 1, kc + 1, hbuf ^ 1);
-                }
-            } else if constexpr (ABL != 3 && Q >= 1 && Q <= G::HPT) {
+            reads(q_tag, a1, b1, va1, vb1);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL != 3 && Q >= 1 && Q <= G::HPT) {
                 if (Q - 1 < nh) load_halo(h0 + Q - 1, kc + 1, hbuf ^ 1);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -537,15 +489,6 @@ static void launch_halo4_t(NTParams& p, const HaloPlan& hp, const HaloGeom& g, h
 }
 
 void launch_halo4(NTParams& p, const HaloPlan& hp, const HaloGeom& g, hipStream_t s, int dtype) {
-    if (g_halo4 >= 3 && hp.bw == 16 && dtype == SEG_BF16 && !p.epi.unpool_y) {   // schedule experiments
-        const dim3 grid((unsigned)hp.tiles, 1, hp.splits), block(512);
-        switch (g_halo4) {
-            case 3: hipLaunchKernelGGL((conv_halo4<16, 8, bf16, false, 0, 1>), grid, block, 0, s, p, g); return;
-            case 4: hipLaunchKernelGGL((conv_halo4<16, 8, bf16, false, 0, 4>), grid, block, 0, s, p, g); return;
-            default: hipLaunchKernelGGL((conv_halo4<16, 4, bf16, false, 0, 4>), dim3((unsigned)hp.tiles, 1, hp.splits),
-                                        dim3(256), 0, s, p, g); return;
-        }
-    }
     if (g_halo4 >= 2) launch_halo4_t<8>(p, hp, g, s, dtype);
     else launch_halo4_t<4>(p, hp, g, s, dtype);
 }

@@ -248,29 +248,13 @@ void launch_nt2(NTParams& p, int dtype, int bn, int gridz, int max_m, hipStream_
 void launch_nt2_bn(NTParams& p, int dtype, hipStream_t s);
 long nt2_bn_rows(int M);
 // dense1x1.hip: the 1x1 BN-backward input gradient streamed (K = 64)
-extern int g_bn1x1s;
-extern int g_s1x1_st;
-extern int g_res16c_st;
-extern int g_dropout_flat;
 bool bn1x1s_ok(const NTParams& p, int dtype);
 int bn1x1s_rows(const NTParams& p, int cus);
 int launch_bn1x1s(NTParams& p, int dtype, int cus, hipStream_t s);
-extern int g_nt2_short;
 bool nt2_short(const NTParams& p, int dtype);
-extern int g_nt_variant;
-extern int g_tn_nsplit;
-extern int g_nt_nsplit;     // igemm_nt3 head + igemm_nt2 tail for N = 256 k + <= 128
-extern int g_halo_duo;      // halo.hip: two-blocks-per-CU conv_halo_duo for N <= 128
-extern int g_tn_variant;
-extern int g_tn_fill;
-extern int g_tn_split_cap;
-extern int g_tn2_smallm;
-extern int g_tn_reduce_sl;
-extern int g_nt2_ablate;
 void launch_tn2(TNParams& p, int bm, int bn, int splits, hipStream_t s, int dtype = SEG_BF16);
 
 // 256 x 256 NT tiles (igemm3.hip) for bf16 with N > 128
-extern int g_nt3;
 bool nt3_ok(const NTParams& p, int dtype);
 // the 16-byte chunk v of channels c0..c0+EPC-1 through the prologue
 template <typename T>
@@ -319,7 +303,6 @@ __device__ __forceinline__ uint4 pro_affine8(uint4 v, const float* ss, int relu)
 constexpr int NT2_PRO_MAXK = 1024;    // (scale, shift) table in LDS
 bool nt2_pro_ok(const NTParams& p, int dtype, int nphases);
 // persistent streaming 1x1 conv (dense1x1.hip): FC-DenseNet bottleneck convs
-extern int g_s1x1;
 bool s1x1_ok(const NTParams& p, int dtype, int nphases);
 void launch_s1x1(NTParams& p, int dtype, int cus, hipStream_t s);
 void launch_nt2_pro(NTParams& p, int dtype, int gridz, int max_m, hipStream_t s);
@@ -345,13 +328,6 @@ inline int one_round_splits(long tiles, int cus, int smax) {
 }
 void nt3_info(int M, int N, int K, int cus, int* splits);
 void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype);
-extern int g_tn3;
-extern int g_tn3_abl;
-extern int g_tn3_mfast;
-extern int g_tn3_adam_abl;
-extern int g_tn3_half;
-extern int g_nt3_fill;
-extern int g_tn3_stagger_us;
 bool tn3_ok(const TNParams& p, int dtype);
 inline bool tn3_applies(int M, int N, int dtype) {
     return g_tn3 && (dtype == SEG_BF16 || dtype == SEG_F16) && M >= 256 && N > 128;
@@ -366,9 +342,6 @@ struct HaloPlan {
     long tiles;
     int geom[10];
 };
-extern int g_nt_halo;
-extern int g_halo_wide;
-extern int g_halo_min_splits;
 int device_cus();
 bool halo_plan(const NTParams& p, int dtype, int max_splits, int cus, HaloPlan* hp);
 enum { HALO_K1 = 0, HALO_KDUO = 1, HALO_K2 = 2, HALO_K4 = 3 };   // conv_halo, conv_halo_duo, conv_halo2, conv_halo4
@@ -376,15 +349,8 @@ int halo_kernel(const NTParams& p, const HaloPlan& hp, int dtype);
 bool halo_unpools(const HaloPlan& hp, int kernel);
 bool halo_pools(const HaloPlan& hp, int kernel);
 int launch_halo(NTParams& p, const HaloPlan& hp, int kernel, hipStream_t s, int dtype = SEG_BF16);
-extern int g_res64;
-extern int g_res16;
-extern int g_res64_pp;
-extern int g_res16_dma;
-extern int g_res16c_bh;
-extern int g_smallk_abl;
 // the launch plan for p writes EpiParams.y2 (seg_conv2d_fwd_bn2)
 bool nt_bn2_ok(const NTParams& p, int dtype);
-extern int g_res16c;
 bool res16c_ok(const NTParams& p, int dtype);
 void launch_res16c(NTParams& p, int cus, hipStream_t s, int dtype);
 int res16c_grid(const NTParams& p, int cus);
@@ -393,11 +359,9 @@ bool res64_ok(const NTParams& p, int dtype);
 int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype = SEG_BF16);
 
 // 8-input-channel first layer (smallc.hip)
-extern int g_smallc;
 bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil);
 void launch_smallc_fwd(NTParams& p, int dtype, hipStream_t s);
 // single-tap NT with K <= 16 (a classifier head's input gradient): streaming kernel
-extern int g_smallk;
 bool smallk_ok(const NTParams& p, int dtype);
 void launch_smallk(NTParams& p, int dtype, int cus, hipStream_t s);
 bool smallc_wgrad_ok(const TNParams& p, int dtype);
@@ -410,12 +374,6 @@ struct WgradPlan {
     long blocks;
     int g[10];
 };
-extern int g_wgrad_halo;
-extern int g_wgrad_nt;
-extern int g_wgrad_abl;
-extern int g_wgrad_nbias;
-extern int g_wgrad_nt32;
-extern int g_wgrad_fill;
 bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp);
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p);
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype = SEG_BF16);

@@ -698,13 +698,10 @@ static int num_cus() {
 
 int device_cus() { return num_cus(); }
 
-int g_nt_nsplit = 1;    // N = 256 k + tail <= 128: igemm_nt3 head + igemm_nt2 tail
-int g_tn_nsplit = 1;    // TN: igemm_tn3 head + igemm_tn2 tail for N = 256 k + <= 128
 
 
 // Kernel generation for the NT GEMMs (1 = register-staged 128-row tiles,
 // 2 = LDS-DMA 3-stage ring, 256-row tiles).  Runtime-selectable for tests.
-int g_nt_variant = 2;
 
 // Tile / split selection: fill >= ~2 workgroups per CU; split K only when the
 // (M,N) tiling cannot, and keep >= 8 k tiles per split.
@@ -744,7 +741,6 @@ size_t nt_workspace(int M, int N, int K, int dtype, int phase) {
     return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
-int g_nt3_fill = 1;
 
 // 256x256 tiles only when the launch (tiles x splits x phases) fills at least
 // half the CUs; narrow problems (phased conv2d_transpose, K <= 6 k-tiles) run
@@ -1031,11 +1027,6 @@ int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t w
     return SEG_EINVAL;
 }
 
-int g_tn_variant = 2;
-int g_tn_fill = 2;          // split-K target: g_tn_fill blocks per CU
-int g_tn_split_cap = 256;   // max split-K slabs
-int g_tn2_smallm = 0;       // 16-bit M < 128: igemm_tn2 (padded 128-row tiles) instead of igemm_tn
-int g_tn_reduce_sl = 16;    // max split-lanes of splitk_reduce_tn (1 = one thread per output float4)
 
 // v2: 0 = igemm_tn tiles, 1 = igemm_tn2 tiles when M >= 128, 2 = igemm_tn2 tiles
 static void choose_tn(int M, int N, int P, int bkp, int v2, int& bm, int& bn, int& splits) {

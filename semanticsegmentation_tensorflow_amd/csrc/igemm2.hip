@@ -678,7 +678,6 @@ void launch_tn2_pro(TNParams& p, int bm, int bn, int splits, hipStream_t s, int 
     else launch_tn2_typed<bf16, true>(p, bm, bn, splits, s);
 }
 
-int g_nt2_ablate = 0;
 
 template <typename T, int BM, int BN, int WM, int WN>
 void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
@@ -698,7 +697,6 @@ void launch_nt2_t(NTParams& p, int gridz, int max_m, hipStream_t s) {
 
 // Short-K bf16 problems (<= g_nt2_short 64-deep k tiles, no split-K) on the
 // 2-stage ring with 64-column tiles: two blocks per CU.  0 = off (tests / A-B).
-int g_nt2_short = 8;
 
 bool nt2_short(const NTParams& p, int dtype) {
     return dtype == SEG_BF16 && !p.partial && p.K <= 64 * g_nt2_short && g_nt2_ablate == 0;

@@ -25,7 +25,6 @@
 
 namespace seg {
 
-int g_nt3 = 1;
 __device__ uint4 g_nt3_zero[4];
 
 // XOR swizzle of the 16-byte chunks of a [k][n] row image (512-byte rows):
@@ -420,18 +419,12 @@ void launch_nt3(NTParams& p, int gridz, int max_m, hipStream_t s, int dtype) {
 // stores (filter gradient or split-K slab).
 // ---------------------------------------------------------------------------
 
-int g_tn3 = 1;
-int g_tn3_abl = 0;     // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
-int g_tn3_mfast = 0;       // tile order: M fastest when the B (dy) panel is the larger operand
-int g_tn3_half = 1;       // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split
-int g_tn3_stagger_us = 40;  // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
 // Main loop unstaggered: the DMA wait for slice t+1 sits at the end of the
 // iteration, a full iteration after its issue.  The dy / x slices of a filter
 // gradient miss L2 far more often than a forward conv's filter slices, so the
 // longer window beats conv_halo2's wave-group stagger here (conv6 main loop
 // 445 -> 307 us measured with the staggered form, since removed).
 __device__ int g_tn3_cu_slots[4096];
-int g_tn3_adam_abl = 0;   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue
 
 // ABL: see g_tn3_abl.  MFAST: consecutive tiles walk M (share the dy panel).
 // ADAM: TF1 Adam on the parameters of the tile (p.adam) instead of (or besides)

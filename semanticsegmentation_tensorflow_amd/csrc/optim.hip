@@ -167,7 +167,6 @@ __global__ __launch_bounds__(256) void adam_pack_k(float* __restrict__ P, const 
 }  // namespace
 
 
-int g_adam_blocks = 0;    // seg_set_option("adam_blocks"): grid cap of seg_adam_tf1_pack (0 = one block per tile)
 
 extern "C" int seg_adam_segments_plan(seg_adam_segment* segs, int nsegs) {
     if (!segs || nsegs <= 0) return -SEG_EINVAL;

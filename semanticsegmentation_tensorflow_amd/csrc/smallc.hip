@@ -119,7 +119,6 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
 
 }  // namespace
 
-int g_smallc = 1;
 
 bool smallc_fwd_ok(const NTParams& p, int dtype, int R, int S, int dil) {
     return g_smallc && (dtype == SEG_BF16 || dtype == SEG_F16) && p.C == 8 && p.K == 72 && R == 3 && S == 3 && dil == 1 && p.ish == 1 &&
@@ -251,8 +250,6 @@ __global__ __launch_bounds__(256) void smallk_nt_k(NTParams p, int abl) {
 }
 }  // namespace
 
-int g_smallk = 1;
-int g_smallk_abl = 0;   // diagnostics only (see smallk_nt_k)
 
 bool smallk_ok(const NTParams& p, int dtype) {
     return g_smallk && (dtype == SEG_BF16 || dtype == SEG_F16) && !p.phase && p.taps_w == 1 && p.K == p.C &&

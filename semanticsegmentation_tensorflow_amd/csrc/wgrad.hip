@@ -30,12 +30,6 @@ namespace seg {
 
 static __device__ uint4 wg_zero_page[4];
 
-int g_wgrad_halo = 1;
-int g_wgrad_nt = 128;
-int g_wgrad_abl = 0;
-int g_wgrad_nt32 = 1;     // 32-wide dy tiles for N <= 32
-int g_wgrad_fill = 100;   // split-K target: blocks = this percentage of the CUs
-int g_wgrad_nbias = 1;   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)
 
 struct WGGeom {
     int tiles_x, tiles_y, nimg, hwd, hrows;

@@ -153,7 +153,15 @@ def conv_kernel_info(desc, op):
 
 
 def set_option(name: str, value: int):
+    """Set a kernel-selection knob for the current HIP device (include/segkern.h)."""
     check(_lib.lib().seg_set_option(name.encode(), int(value)), f"set_option({name})")
+
+
+def get_option(name: str) -> int:
+    """The current HIP device's value of a kernel-selection knob."""
+    v = ctypes.c_int(0)
+    check(_lib.lib().seg_get_option(name.encode(), ctypes.byref(v)), f"get_option({name})")
+    return v.value
 
 
 def conv_workspace(desc, op):

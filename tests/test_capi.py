@@ -93,6 +93,60 @@ def test_product_library_has_no_ablation_knobs():
     assert lib.seg_set_option(b"res16c_bh", 4) == 0
 
 
+def test_knobs_are_a_guarded_per_device_set():
+    """VERDICT r05 item 7 / SURVEY.md 8b: the kernel-selection knobs are the
+    library's only mutable state, one mutex-guarded set per HIP device
+    (csrc/knobs.h).  seg_get_option reads back the tuned defaults; a change
+    applies to the very next call's plan (seg_conv_kernel_info re-plans from
+    the descriptor and the knobs on every call -- nothing else is cached);
+    invalid values leave the set untouched; concurrent writers and readers
+    from several host threads see only values some writer stored."""
+    import ctypes
+    import threading
+    lib = _lib.load()
+    v = ctypes.c_int(-1)
+    defaults = {b"halo4": 2, b"nt3": 1, b"tn_reduce_sl": 16, b"wgrad_nt": 128, b"wpad": 0}
+    for k, want in defaults.items():
+        assert lib.seg_get_option(k, ctypes.byref(v)) == 0 and v.value == want, (k, v.value)
+    assert lib.seg_get_option(b"no_such_knob", ctypes.byref(v)) == 1
+    d = _lib.SegConvDesc()
+    assert lib.seg_conv_desc_init(ctypes.byref(d), 4, 96, 312, 256, 256, 3, 3, 1, 1, 0, 1) == 0
+    name = ctypes.create_string_buffer(64)
+    sp, fl = ctypes.c_int(0), ctypes.c_double(0)
+
+    def kernel():
+        assert lib.seg_conv_kernel_info(ctypes.byref(d), 0, name, 64, ctypes.byref(sp), ctypes.byref(fl)) == 0
+        return name.value
+    assert kernel().startswith(b"conv_halo4<")
+    try:
+        assert lib.seg_set_option(b"halo4", 0) == 0
+        assert kernel().startswith(b"conv_halo<")        # conv_halo2 (reported under the family name)
+        assert lib.seg_set_option(b"halo4", 99) == 1       # rejected: the set keeps 0
+        assert lib.seg_get_option(b"halo4", ctypes.byref(v)) == 0 and v.value == 0
+    finally:
+        assert lib.seg_set_option(b"halo4", 2) == 0
+    assert kernel().startswith(b"conv_halo4<")
+    seen, errs = set(), []
+
+    def writer(val):
+        for _ in range(2000):
+            if lib.seg_set_option(b"tn_split_cap", val) != 0:
+                errs.append(val)
+
+    def reader():
+        r = ctypes.c_int(0)
+        for _ in range(2000):
+            lib.seg_get_option(b"tn_split_cap", ctypes.byref(r))
+            seen.add(r.value)
+    ts = [threading.Thread(target=writer, args=(a,)) for a in (64, 128)] + [threading.Thread(target=reader)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and seen <= {64, 128, 256}, (errs, seen)
+    assert lib.seg_set_option(b"tn_split_cap", 256) == 0
+
+
 def test_bn_part_launch_refuses_a_foreign_row_count():
     """seg_conv2d_bwd_data_bn_part writes exactly seg_conv_bwd_data_bn_part_rows
     partial rows -- the count a batched finish plan was made for; any other

@@ -54,7 +54,7 @@ def test_accumulate_template_plan(dry):  # noqa: F811
     dry.calls.clear()
     sess.run(accum_ops, feed_dict=feed)
     c = dry.calls
-    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pool") == 17
+    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pool") + c.count("seg_conv2d_fwd_hwio") == 17
     # no optimizer in this run: every filter gradient is a plain launch
     assert c.count("seg_conv2d_bwd_filter") == 17 and "seg_conv2d_bwd_filter_adam" not in c
     assert "seg_adam_tf1_pack" not in c
@@ -64,6 +64,7 @@ def test_accumulate_template_plan(dry):  # noqa: F811
     sess.run(train_step, feed_dict=feed)
     c = dry.calls
     assert "seg_conv2d_fwd" not in c and "seg_conv2d_fwd_pool" not in c   # apply_gradients: no forward pass
+    assert "seg_conv2d_fwd_hwio" not in c
     assert c.count("seg_axpy") == 40 and c.count("seg_adam_tf1_pack") == 1
     assert st.step == 1
 
