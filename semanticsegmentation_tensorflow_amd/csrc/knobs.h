@@ -48,7 +48,7 @@ namespace seg {
     X(tn3, 1) \
     X(tn3_abl, 0) \
     X(tn3_mfast, 0) \
-    X(tn3_half, 1) \
+    X(tn3_half, 0) \
     X(tn3_stagger_us, 40) \
     X(tn3_adam_abl, 0) \
     X(adam_blocks, 0) \
@@ -106,7 +106,7 @@ KnobSet& knobs();
 #define g_tn3 (::seg::knobs().tn3.load(std::memory_order_relaxed))
 #define g_tn3_abl (::seg::knobs().tn3_abl.load(std::memory_order_relaxed))   // diagnostics (garbage results): 1 no DMA in the loop, 2 no MFMA, 3 no epilogue stores
 #define g_tn3_mfast (::seg::knobs().tn3_mfast.load(std::memory_order_relaxed))   // tile order: M fastest when the B (dy) panel is the larger operand
-#define g_tn3_half (::seg::knobs().tn3_half.load(std::memory_order_relaxed))   // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split
+#define g_tn3_half (::seg::knobs().tn3_half.load(std::memory_order_relaxed))   // 256 x 128 two-blocks-per-CU tiles: 1 for the fused Adam (multi-round grids; +4: any grid), 2 for plain single-split; 0 (default since round 6): 256 x 256 everywhere
 #define g_tn3_stagger_us (::seg::knobs().tn3_stagger_us.load(std::memory_order_relaxed))   // half-tile fused Adam: start offset of the second block on each CU (multi-round grids)
 #define g_tn3_adam_abl (::seg::knobs().tn3_adam_abl.load(std::memory_order_relaxed))   // diagnostics: 1 no p/m/v loads, 2 no p/m/v stores, 4 no HWIO copy, 8 no KRSC copy, 16 no epilogue
 #define g_adam_blocks (::seg::knobs().adam_blocks.load(std::memory_order_relaxed))   // seg_set_option("adam_blocks"): grid cap of seg_adam_tf1_pack (0 = one block per tile)

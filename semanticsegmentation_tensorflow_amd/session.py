@@ -169,8 +169,10 @@ class Session(PlanMixin, StreamMixin):
         # the fused conv6 / conv7 filter-gradient + Adam launches go to the side
         # stream after the next `fused_delay` filter gradients there (the
         # HBM-bound update then overlaps the smaller conv4_x / conv3_x layers
-        # instead of starving conv5_x's input gradients: 547 -> 554 img/s at 5-7)
-        self.fused_delay = 6
+        # instead of starving conv5_x's input gradients: 547 -> 554 img/s at 5-7
+        # in round 3; round 6, with conv_halo4 and the update on 256 x 256
+        # tiles: 2 -- 592.1 / 590.8 vs 583.6 / 582.8 img/s at 6 on the same box)
+        self.fused_delay = 2
         self._pending_fused = []
         # the filter gradients of the first `main_wgrad` convs (the last in the
         # backward: conv1_1 / conv1_2 / conv2_1 in FCN) stay on the compute

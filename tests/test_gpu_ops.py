@@ -203,9 +203,9 @@ def tnv(request, dev):
     ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
-    ops.set_option("tn3_half", 7 if v == 7 else 1)
+    ops.set_option("tn3_half", 7 if v == 7 else 0)
     yield v
-    ops.set_option("tn3_half", 1)
+    ops.set_option("tn3_half", 0)
     ops.set_option("tn3", 1)
     ops.set_option("wgrad_nbias", 1)
     ops.set_option("igemm_tn_variant", 2)
@@ -770,14 +770,14 @@ ADAM_FUSED_CASES = [
 
 # (tn3_half, adam_tr_fused): igemm_tn3's fused epilogue on half / full tiles
 # (the KRSC copy by the transpose, or in the epilogue)
-@pytest.fixture(params=[(1, 0), (5, 0), (0, 0), (0, 1)],
-                ids=["default", "half-tiles", "full-tiles", "full-tiles-tr-fused"])
+@pytest.fixture(params=[(0, 0), (1, 0), (5, 0), (0, 1)],
+                ids=["default", "half-tiles-multi-round", "half-tiles", "full-tiles-tr-fused"])
 def adam_tiles(request, dev):
     half, trf = request.param
     ops.set_option("tn3_half", half)
     ops.set_option("adam_tr_fused", trf)
     yield request.param
-    ops.set_option("tn3_half", 1)
+    ops.set_option("tn3_half", 0)
     ops.set_option("adam_tr_fused", 0)
 
 
