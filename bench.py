@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--force-dp", action="store_true",
                     help="data-parallel Session over an RCCL ('nccl') process group even at world size 1 "
                          "(e.g. torchrun --nproc-per-node 1): the C4 per-rank step, all-reduces included")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="with --force-dp at world size 1: issue the bucket collectives anyway (the per-rank path "
+                         "of a world > 1 job minus the wire time, as the dp_mode probe line)")
     ap.add_argument("--no-dp-probe", action="store_true",
                     help="N=1: skip the side line that re-times the step through a world-1 RCCL data-parallel Session")
     ap.add_argument("--no-inference", action="store_true", help="skip the inference-latency line")
@@ -771,10 +774,13 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dp = None
+    from semanticsegmentation_tensorflow_amd.session import side_stream_for
+    side_stream_for(device)     # before RCCL takes hardware queues (session.side_stream_for)
     if world > 1 or args.force_dp:
         init_rccl(device)
         from semanticsegmentation_tensorflow_amd.dp import DataParallel
-        dp = DataParallel(bucket_mb=args.bucket_mb, shard_optimizer=args.dp_mode == "zero")
+        dp = DataParallel(bucket_mb=args.bucket_mb, shard_optimizer=args.dp_mode == "zero",
+                          force_collectives=args.force_collectives)
         world = dist.get_world_size()     # what RCCL saw
 
     from semanticsegmentation_tensorflow_amd import ops

@@ -864,11 +864,12 @@ bool nt_unpool_ok(const NTParams& p, int dtype) {
 
 // Whether the planned launch writes EpiParams.y2 (the BN(+ReLU) second
 // output): igemm_nt2 with its operand prologue or without, no split-K; and
-// igemm_nt3 with split-K, whose splitk_reduce_nt writes it (DeepLab's ASPP
-// convs -> BN -> ReLU on the 1/8-resolution map).
+// igemm_nt3 -- unsplit in its own epilogue (round 6: DeepLab's ASPP convs ->
+// BN -> ReLU at 1024 x 2048, C5), split through splitk_reduce_nt (the same
+// convs on the 1/8-resolution map of a 384 x 1248 input).
 static bool nt_plan_bn2(const NTPlan& pl, int dtype) {
     if (dtype == SEG_F32) return false;
-    return (pl.splits == 1 && (pl.kind == NTK_PRO2 || pl.kind == NTK_NT2)) || (pl.kind == NTK_NT3 && pl.splits > 1);
+    return (pl.splits == 1 && (pl.kind == NTK_PRO2 || pl.kind == NTK_NT2)) || pl.kind == NTK_NT3;
 }
 
 bool nt_bn2_ok(const NTParams& p, int dtype) { return nt_plan_bn2(nt_plan(p, dtype, 1, p.M), dtype); }

@@ -379,7 +379,22 @@ __global__ __launch_bounds__(512) void igemm_nt3(NTParams p) {
                 v[j] = col < e.n_valid ? x : 0.f;
             }
             T* yp = reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0;
-            *reinterpret_cast<uint4*>(yp) = Chunk<T>::pack(v);
+            const uint4 packed = Chunk<T>::pack(v);
+            *reinterpret_cast<uint4*>(yp) = packed;
+            if (e.y2) {      // BN2(+ReLU) of the stored values (seg_bn_relu_fwd's arithmetic, as igemm_nt2)
+                float r2[8], o2[8];
+                Chunk<T>::unpack(packed, r2);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int col = col0 + j;
+                    const bool c2 = col < e.bn2_cv;
+                    float v2 = __builtin_fmaf(r2[j], c2 ? e.bn2_gamma[col] * e.bn2_inv : 0.f, c2 ? e.bn2_beta[col] : 0.f);
+                    if (e.bn2_relu) v2 = fmaxf(v2, 0.f);
+                    o2[j] = v2;
+                }
+                *reinterpret_cast<uint4*>(reinterpret_cast<T*>(e.y2) + img * e.y2_img + pix * e.ld_y2 + col0) =
+                    Chunk<T>::pack(o2);
+            }
         }
     }
 }

@@ -59,7 +59,7 @@ namespace seg {
     X(wgrad_nt, 128) \
     X(wgrad_abl, 0) \
     X(wgrad_nt32, 1) \
-    X(wgrad_fill, 100) \
+    X(wgrad_fill, 88) \
     X(wgrad_nbias, 1)
 
 struct KnobSet {
@@ -117,5 +117,5 @@ KnobSet& knobs();
 #define g_wgrad_nt (::seg::knobs().wgrad_nt.load(std::memory_order_relaxed))
 #define g_wgrad_abl (::seg::knobs().wgrad_abl.load(std::memory_order_relaxed))
 #define g_wgrad_nt32 (::seg::knobs().wgrad_nt32.load(std::memory_order_relaxed))   // 32-wide dy tiles for N <= 32
-#define g_wgrad_fill (::seg::knobs().wgrad_fill.load(std::memory_order_relaxed))   // split-K target: blocks = this percentage of the CUs
+#define g_wgrad_fill (::seg::knobs().wgrad_fill.load(std::memory_order_relaxed))   // split-K target: blocks = this percentage of the CUs (round 6: 88 -- in the overlapped step the side-stream filter gradients share the CUs with the input-gradient chain; 596.5 / 596.8 vs 591.5 / 591.9 img/s at 100 on one box)
 #define g_wgrad_nbias (::seg::knobs().wgrad_nbias.load(std::memory_order_relaxed))   // max channel blocks sharing the fused BiasAddGrad (1 measured best: the per-wave spread suffices)

@@ -90,6 +90,30 @@ def _np(x):
     return torch.from_numpy(np.ascontiguousarray(x))
 
 
+_SIDE_STREAMS = {}
+
+
+def side_stream_for(device):
+    """The process-wide side stream of a device (filter gradients, their
+    split-K reductions, the fused conv6 / conv7 update, bucket collectives),
+    shared by every Session on it.  HIP maps streams onto a fixed pool of
+    hardware queues (GPU_MAX_HW_QUEUES, 4 on the box), and a stream created
+    after an RCCL communicator took some of them can land on the compute
+    stream's queue: every launch of the step then runs serialised on one queue
+    (round 6: the world-1 data-parallel step at 7.6 ms instead of 6.8,
+    tools/queue_probe.py).  Created before init_process_group -- bench.py
+    calls this first; a data-parallel program should too -- it keeps a queue
+    of its own."""
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+        with torch.cuda.stream(s):      # a first launch binds the stream to its queue now
+            torch.zeros(1, device=device)
+    return s
+
+
 class Session(PlanMixin, StreamMixin):
     def __init__(self, graph=None, compute_dtype="bf16", device=None, seed=0, data_parallel=None,
                  overlap_optimizer=False, fuse_adam=True, loss_scale=None):
@@ -183,8 +207,9 @@ class Session(PlanMixin, StreamMixin):
         # data-parallel all-reduce steps: the Adam update of every variable of
         # >= overlap_big_mb MB (FCN conv6 / conv7) as soon as its buckets'
         # collectives complete, on the side stream beside the rest of backward
-        # (0: all at the end)
-        self.overlap_big_mb = 0
+        # (0: all at the end).  Default since round 6: the world-1 RCCL probe
+        # 558.0 vs 555.7 img/s with the side stream on a queue of its own
+        self.overlap_big_mb = 64
 
         self._side = None
         self._adam_ctx = None
@@ -510,6 +535,12 @@ class Session(PlanMixin, StreamMixin):
         world 1 where every collective is the identity)."""
         return self.dp if (self.dp is not None and self.dp.active) else None
 
+    def side_stream(self):
+        """The side stream of this Session's device (side_stream_for)."""
+        if self._side is None:
+            self._side = side_stream_for(self.device)
+        return self._side
+
     def sync_optimizer_slots(self):
         """After ZeRO-1 steps each rank's Adam m / v are current on its own
         slices only: gather them (checkpoints, tests)."""
@@ -776,9 +807,7 @@ class Session(PlanMixin, StreamMixin):
             if self.defer_wgrad_reduce and self.device.type == "cuda":
                 # (with the overlapped optimizer the reductions and each layer's
                 # Adam share the side stream: a layer's reduction precedes its update)
-                if self._side is None:
-                    self._side = torch.cuda.Stream(device=self.device)
-                self._red = (self._side, torch.cuda.current_stream(self.device))
+                self._red = (self.side_stream(), torch.cuda.current_stream(self.device))
                 if dpa is not None:
                     dpa.launch_streams = self._red
             if opt is not None and self.overlap_optimizer and self.device.type == "cuda":

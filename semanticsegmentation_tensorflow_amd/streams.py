@@ -27,9 +27,7 @@ class _AdamOverlap:
         self.opt = opt
         self.gs = gs
         self.var_set = var_set
-        if sess._side is None:
-            sess._side = torch.cuda.Stream(device=sess.device)
-        self.side = sess._side
+        self.side = sess.side_stream()
         self.main = torch.cuda.current_stream(sess.device)
         self.done = set()
         # big_only (data-parallel all-reduce steps, Session.overlap_big_mb):

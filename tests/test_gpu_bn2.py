@@ -88,17 +88,23 @@ def test_conv_bn2_refused_on_split_k(dev):
 # :186-229) on the 1/8-resolution map of a 384x1248 input (48x156, where the
 # plan splits K) -- the rate-6 / rate-18 3x3 convs and the 1280 -> 256
 # concat_projection
-NT3_CASES = [(2, 48, 156, 512, 256, 3, 6), (2, 48, 156, 512, 256, 3, 18), (2, 48, 156, 1280, 256, 1, 1)]
+# concat_projection.  Round 6: unsplit igemm_nt3 writes it in its own
+# epilogue -- the same convs on the 128 x 256 map of C5's 1024 x 2048 input
+# (the ASPP 1x1 branch too), where the five separate bn_relu_fwd passes ran.
+NT3_CASES = [(2, 48, 156, 512, 256, 3, 6), (2, 48, 156, 512, 256, 3, 18), (2, 48, 156, 1280, 256, 1, 1),
+             (2, 128, 256, 512, 256, 3, 6), (2, 128, 256, 512, 256, 3, 18), (2, 128, 256, 1280, 256, 1, 1),
+             (2, 128, 256, 512, 256, 1, 1)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("case", NT3_CASES, ids=["aspp1_rate6", "aspp3_rate18", "projection_1x1"])
-def test_nt3_split_bn2_equals_conv_then_bn_relu(dev, case, dtype):
+@pytest.mark.parametrize("case", NT3_CASES, ids=["aspp1_rate6", "aspp3_rate18", "projection_1x1", "c5_aspp1_rate6",
+                                                 "c5_aspp3_rate18", "c5_projection_1x1", "c5_aspp0_1x1"])
+def test_nt3_bn2_equals_conv_then_bn_relu(dev, case, dtype):
     N, H, W, C, K, R, dil = case
     dt = ops.BF16 if dtype == torch.bfloat16 else ops.F16
     d = ops.conv_desc(N, H, W, C, K, R, R, dilation=dil, dtype=dt)
     name, splits, _ = ops.conv_kernel_info(d, ops.OP_FWD)
-    assert name.startswith("igemm_nt3") and splits > 1, (name, splits)
+    assert name.startswith("igemm_nt3") and (splits > 1) == (H == 48), (name, splits)
     assert ops.conv2d_fwd_bn2_ok(d, False)
     g = torch.Generator(device=dev).manual_seed(23)
     x = torch.randn(N, H, W, C, device=dev, generator=g).to(dtype)

@@ -44,6 +44,7 @@ CASES = [
     ("dp_bf16_allreduce", "bf16", "allreduce", {"side_wgrad": 1}),
     ("dp_bf16_allreduce_big", "bf16", "allreduce", {"overlap_big_mb": 4}),
     ("dp_f32_allreduce_big", "f32", "allreduce", {"overlap_big_mb": 1}),
+    ("dp_bf16_allreduce_end", "bf16", "allreduce", {"overlap_big_mb": 0}),
 ]
 
 
