@@ -235,6 +235,24 @@ int seg_conv2d_bwd_data_bn(const seg_conv_desc* d, const void* dy, const void* w
                            void* dx, void* ws, size_t ws_bytes, void* stream);
 int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const void* w_hwio,
                         const seg_epilogue* epi, void* dx, void* ws, size_t ws_bytes, void* stream);
+/* The ReluGrad mask as bits (round 6).  seg_conv2d_fwd_relu_bits = seg_conv2d_fwd
+ * that also writes the ReLU mask of the stored y: bit k & 7 of
+ * bits[pixel * ld_bits + k / 8] = (y[pixel][k] > 0), pixels dense over the
+ * batch, ld_bits >= K / 8 bytes (K = 64: a multiple of 8, bits 8-byte
+ * aligned -- one 8-byte store per pixel).  seg_conv2d_bwd_data_bits = seg_conv2d_bwd_data
+ * whose ReluGrad mask (epi->relu_mask, which must be NULL here; epi->mask_scale
+ * applies) is read from such bits, 8-byte aligned: dx bit for bit the same as
+ * with the 16-bit map.  FCN / VGG conv1_1 -> conv1_2 (Network/model/FCN.py:55-56):
+ * conv1_2's input gradient reads 8 bytes per pixel instead of conv1_1's
+ * 128-byte output row.  Only the kernels with these epilogues take them (the
+ * first-layer C <= 8 forward; the 64 -> 64 3x3 input gradient): the _ok
+ * queries, SEG_EINVAL otherwise. */
+int seg_conv2d_fwd_relu_bits_ok(const seg_conv_desc* d);
+int seg_conv2d_fwd_relu_bits(const seg_conv_desc* d, const void* x, const void* w_krsc, const seg_epilogue* epi,
+                             void* y, void* bits, int ld_bits, void* stream);
+int seg_conv2d_bwd_data_bits_ok(const seg_conv_desc* d);
+int seg_conv2d_bwd_data_bits(const seg_conv_desc* d, const void* dy, const void* w_hwio, const seg_epilogue* epi,
+                             const void* bits, int ld_bits, void* dx, void* ws, size_t ws_bytes, void* stream);
 /* Conv2DBackpropFilter: dw_f32 is the fp32 master-gradient layout
  * [R][S][c_valid][k_valid]; written (not accumulated).  dbias (optional):
  * BiasAddGrad of the same dy, dbias[k] = sum over pixels of dy[p][k]

@@ -147,6 +147,10 @@ SIGNATURES = {
     "seg_conv2d_fwd_pool_ok": (_I, [_DP]),
     "seg_conv2d_fwd_pool": (_I, [_DP, _P, _P, _EP, _P, _I, _P, _I, _P, _Z, _P]),
     "seg_conv2d_bwd_data": (_I, [_DP, _P, _P, _EP, _P, _P, _Z, _P]),
+    "seg_conv2d_fwd_relu_bits_ok": (_I, [_DP]),
+    "seg_conv2d_fwd_relu_bits": (_I, [_DP, _P, _P, _EP, _P, _P, _I, _P]),
+    "seg_conv2d_bwd_data_bits_ok": (_I, [_DP]),
+    "seg_conv2d_bwd_data_bits": (_I, [_DP, _P, _P, _EP, _P, _I, _P, _P, _Z, _P]),
     "seg_conv2d_bwd_data_unpool_ok": (_I, [_DP]),
     "seg_conv2d_bwd_data_unpool": (_I, [_DP, _P, _P, _EP, _P, _I, _I, _P, _I, _P, _Z, _P]),
     "seg_conv2d_fwd_pro": (_I, [_DP, _P, ctypes.POINTER(SegPrologue), _P, _EP, _P, _P, _Z, _P]),

@@ -624,6 +624,43 @@ extern "C" int seg_conv2d_fwd(const seg_conv_desc* d, const void* x, const void*
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Conv2D whose ReLU mask is also written as bits (bits[pixel * ld_bits + k/8],
+// bit k & 7: stored y > 0) for the next conv's seg_conv2d_bwd_data_bits --
+// conv1_1 of FCN / VGG (3 -> 64), on conv_c8_fwd, the one kernel that writes
+// them: 8 bytes per pixel beside the 128 of the map.
+static bool fwd_relu_bits_params(const seg_conv_desc* d, const seg_epilogue* epi, int ld_bits, NTParams* out) {
+    // (K = 64: 8-byte row stores)
+    if (check_desc(d) || d->dil_w != d->dil_h || ld_bits < d->K / 8 || (d->K == 64 && ld_bits % 8)) return false;
+    if (epi && epi->relu_mask) return false;
+    NTParams p = conv_fwd_params(d);
+    p.epi = make_epi(epi, d->k_valid, (long)d->OH * d->OW * (epi ? epi->ld_residual : 0));
+    if (!seg::smallc_fwd_ok(p, d->dtype, d->R, d->S, d->dil_h)) return false;
+    p.epi.ld_bits = ld_bits;
+    *out = p;
+    return true;
+}
+
+extern "C" int seg_conv2d_fwd_relu_bits_ok(const seg_conv_desc* d) {
+    NTParams p;
+    seg_epilogue e = {};
+    e.relu = 1;
+    e.keep_prob = 1.f;
+    return d && fwd_relu_bits_params(d, &e, d->K / 8, &p) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_fwd_relu_bits(const seg_conv_desc* d, const void* x, const void* w, const seg_epilogue* epi,
+                                        void* y, void* bits, int ld_bits, void* stream) {
+    if (!d || !x || !w || !y || !bits) return SEG_EINVAL;
+    if (d->K == 64 && ((uintptr_t)bits & 7)) return SEG_EALIGN;
+    NTParams p;
+    if (!fwd_relu_bits_params(d, epi, ld_bits, &p)) return SEG_EINVAL;
+    p.x = x; p.w = w; p.y = y;
+    p.epi.ybits = reinterpret_cast<unsigned char*>(bits);
+    seg::launch_smallc_fwd(p, d->dtype, (hipStream_t)stream);
+    SEG_CHECK_LAUNCH();
+    return SEG_OK;
+}
+
 // Conv2D reading the HWIO filter copy ([R][S][C][K], the one the input
 // gradient reads) on igemm_nt3's B-transposed form: a weight with one packed
 // copy instead of two (seg_conv2d_fwd_hwio_ok).
@@ -816,6 +853,45 @@ extern "C" int seg_conv2d_bwd_data(const seg_conv_desc* d, const void* dy, const
         p.epi = make_epi(epi, d->C, (long)d->H * d->W * ldr, (long)d->H * d->W, d->ldx);
         if (epi->residual && epi->ld_residual == 0) p.epi.ld_res = d->ldx;
     }
+    return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// Conv2DBackpropInput with the ReluGrad mask given as seg_conv2d_fwd_relu_bits'
+// bits (epi->relu_mask null; epi->mask_scale applies): conv1_2's input
+// gradient reads 8 bytes per pixel instead of conv1_1's 128-byte map row.
+// conv_res64pp only (64 input channels, 3x3, stride 1).
+static bool bwd_data_bits_params(const seg_conv_desc* d, const seg_epilogue* epi, const void* bits, int ld_bits,
+                                 NTParams* out) {
+    if (check_desc(d) || (d->dtype != SEG_BF16 && d->dtype != SEG_F16)) return false;
+    if (d->stride_h != 1 || d->stride_w != 1) return false;
+    if (epi && (epi->relu_mask || epi->residual)) return false;
+    NTParams p = conv_bwd_data_params(d);
+    if (epi) {
+        p.epi = make_epi(epi, d->C, 0, (long)d->H * d->W, d->ldx);
+        if (epi->mask_scale != 0.f) p.epi.mask_scale = epi->mask_scale;
+    }
+    p.epi.mask_bits = reinterpret_cast<const unsigned char*>(bits);
+    p.epi.ld_bits = ld_bits;
+    if (!seg::nt_mask_bits_ok(p, d->dtype)) return false;
+    *out = p;
+    return true;
+}
+
+extern "C" int seg_conv2d_bwd_data_bits_ok(const seg_conv_desc* d) {
+    NTParams p;
+    // shape-only query: an aligned stand-in for the bits
+    const void* a = reinterpret_cast<const void*>(uintptr_t(1) << 20);
+    return d && bwd_data_bits_params(d, nullptr, a, d->C / 8, &p) ? 1 : 0;
+}
+
+extern "C" int seg_conv2d_bwd_data_bits(const seg_conv_desc* d, const void* dy, const void* w, const seg_epilogue* epi,
+                                        const void* bits, int ld_bits, void* dx, void* ws, size_t ws_bytes,
+                                        void* stream) {
+    if (!d || !dy || !w || !bits || !dx) return SEG_EINVAL;
+    if ((uintptr_t)bits & 7) return SEG_EALIGN;
+    NTParams p;
+    if (!bwd_data_bits_params(d, epi, bits, ld_bits, &p)) return SEG_EINVAL;
+    p.x = dy; p.w = w; p.y = dx;
     return seg::launch_nt(p, d->dtype, 1, p.M, ws, ws_bytes, (hipStream_t)stream);
 }
 

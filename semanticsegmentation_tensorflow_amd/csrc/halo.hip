@@ -1233,6 +1233,9 @@ __global__ __launch_bounds__(512, NB == 16 ? (DMA ? 4 : 2) : 1) void conv_res64(
 // The ReluGrad mask of a tile is requested at the start of its compute phase
 // and reduced to one bit per output (mask > 0) after its MFMAs, so no wait for
 // it lands behind the epilogue phase's DMA (vmcnt retires in issue order).
+// Given as bits (EpiParams::mask_bits, round 6: conv_c8_fwd writes them with
+// conv1_1's map) it is 8 B per pixel instead of 128: four 8-byte loads per
+// lane and tile instead of sixteen.
 // ---------------------------------------------------------------------------
 constexpr int RPP_HS = RPP_PIECES * 8 * 128;         // 44,032 B per halo buffer
 
@@ -1319,7 +1322,17 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
                 const int img = t / tpi;
                 const int rem = t - img * tpi;
                 const int ty = rem / tiles_x, tx = rem - (rem / tiles_x) * tiles_x;
-                if (e.mask) {       // ReluGrad mask rows, used in the next phase
+                if (e.mask_bits) {  // the same as bits: one 8-byte row per pixel (64 channels)
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi) {
+                        const int ml = wm * 64 + mi * 16 + fr;
+                        const int oy = ty * R64_BH + ml / R64_BW, ox = tx * R64_BW + ml % R64_BW;
+                        mpre[mi][0] = uint2{0u, 0u};
+                        if (oy < p.OH && ox < p.OW)
+                            mpre[mi][0] = *reinterpret_cast<const uint2*>(
+                                e.mask_bits + (((long)img * p.OH + oy) * p.OW + ox) * e.ld_bits);
+                    }
+                } else if (e.mask) {       // ReluGrad mask rows, used in the next phase
 #pragma unroll
                     for (int mi = 0; mi < TM; ++mi) {
                         const int ml = wm * 64 + mi * 16 + fr;
@@ -1377,7 +1390,16 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
                             acc[mi][ni] = mfma16x16x32<T>(fb[cur][ni], fa[cur][mi], acc[mi][ni]);
                 }
                 __builtin_amdgcn_s_setprio(0);
-                if (e.mask) {       // the loads had the whole MFMA loop to land
+                if (e.mask_bits) {  // channels ni * 16 + 4 fg .. + 3: one nibble per (mi, ni)
+                    mbits = 0;
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi) {
+                        const uint64_t row = (uint64_t)mpre[mi][0].x | ((uint64_t)mpre[mi][0].y << 32);
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni)
+                            mbits |= ((row >> (ni * 16 + 4 * fg)) & 0xFull) << ((mi * TN + ni) * 4);
+                    }
+                } else if (e.mask) {       // the loads had the whole MFMA loop to land
                     mbits = 0;
 #pragma unroll
                     for (int mi = 0; mi < TM; ++mi)
@@ -1466,7 +1488,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64pp(NTParams p, int tiles_x, 
                             if (e.relu) x = fmaxf(x, 0.f);
                             if (e.keep_prob < 1.f) x = drop(x, e.keep_prob, j);
                             x += res[j];
-                            if (e.mask) x = (mbits >> ((mi * TN + ni) * 4 + j)) & 1 ? x * e.mask_scale : 0.f;
+                            if (e.mask || e.mask_bits) x = (mbits >> ((mi * TN + ni) * 4 + j)) & 1 ? x * e.mask_scale : 0.f;
                             o[j] = from_f32<T>(col < e.n_valid ? x : 0.f);
                         }
                         *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.y) + img * p.y_img + pix * p.ldy + col0) =
@@ -1978,14 +2000,16 @@ bool res64_ok(const NTParams& p, int dtype) {
            p.osw == 1 && p.ooh == 0 && p.oow == 0 && p.Ha == p.OH && p.Wa == p.OW && p.C == 64 && p.K == 9 * 64 &&
            p.taps_w == 3 && (p.tsh == 1 || p.tsh == -1) && (p.tsw == 1 || p.tsw == -1) && p.N <= 64 &&
            p.N % 8 == 0 && p.OH > 0 && p.OW > 0 && p.M % (p.OH * p.OW) == 0 &&
-           (!p.epi.mask || ((uintptr_t)p.epi.mask % 8 == 0 && p.epi.ld_mask % 4 == 0 && p.epi.mask_img % 4 == 0));
+           (!p.epi.mask || ((uintptr_t)p.epi.mask % 8 == 0 && p.epi.ld_mask % 4 == 0 && p.epi.mask_img % 4 == 0)) &&
+           (!p.epi.mask_bits || (p.N == 64 && !p.epi.mask && (uintptr_t)p.epi.mask_bits % 8 == 0 &&
+                                 p.epi.ld_bits >= 8 && p.epi.ld_bits % 8 == 0));
 }
 
 int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
     const int tx = (p.OW + R64_BW - 1) / R64_BW, ty = (p.OH + R64_BH - 1) / R64_BH;
     const int ntiles = (p.M / (p.OH * p.OW)) * tx * ty;
     if (p.N <= 16 && g_res16) {
-        if (p.epi.pool_y) return SEG_EINVAL;  // no pooled epilogue in the 16-wide form
+        if (p.epi.pool_y || p.epi.mask_bits) return SEG_EINVAL;  // no pooled epilogue / mask bits in the 16-wide form
         const int grid = std::min(ntiles, 2 * cus);
         if (g_res16_dma) {                    // two blocks per CU (launch bounds: 4 waves / SIMD)
             if (dtype == SEG_F16)
@@ -2000,7 +2024,7 @@ int launch_res64(NTParams& p, int cus, hipStream_t s, int dtype) {
         return SEG_OK;
     }
     const int grid = std::min(ntiles, cus);
-    if (g_res64_pp == 2 || (g_res64_pp == 1 && (p.epi.pool_y || p.epi.mask))) {
+    if (g_res64_pp == 2 || (g_res64_pp == 1 && (p.epi.pool_y || p.epi.mask)) || p.epi.mask_bits) {
         if (dtype == SEG_F16) hipLaunchKernelGGL((conv_res64pp<f16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         else hipLaunchKernelGGL((conv_res64pp<bf16>), dim3(grid), dim3(512), 0, s, p, tx, ty, ntiles);
         return SEG_OK;

@@ -68,6 +68,14 @@ struct EpiParams {
     void* unpool_y;
     const unsigned char* unpool_idx;
     int ld_unpool, ld_uidx, unpool_relu;
+    // The ReLU mask as bits: bit k & 7 of byte k >> 3 of a pixel's ld_bits-byte
+    // row, pixels dense over the batch (seg_conv2d_fwd_relu_bits).  ybits: a
+    // forward also writes stored y > 0 there (conv_c8_fwd only); mask_bits: an
+    // input gradient's ReluGrad mask in place of `mask` (conv_res64pp only) --
+    // 1 bit instead of 2 bytes per element.
+    unsigned char* ybits;
+    const unsigned char* mask_bits;
+    int ld_bits;
 };
 
 // The MaxPoolGrad store of EpiParams::unpool_y for the 8 channels col0.. of
@@ -237,6 +245,7 @@ int launch_nt(NTParams& p, int dtype, int nphases, int max_m, void* ws, size_t w
 bool nt_pool_ok(const NTParams& p, int dtype);   // launch_nt's kernel fuses EpiParams::pool_y
 bool nt_fwd_bt_ok(const NTParams& p, int dtype);
 bool nt_unpool_ok(const NTParams& p, int dtype);
+bool nt_mask_bits_ok(const NTParams& p, int dtype);
 int launch_tn(TNParams& p, int dtype, void* ws, size_t ws_bytes, hipStream_t s);
 void tn_reduce(TNParams& p, int splits, hipStream_t s);   // a pending (p.defer) split-K reduction
 size_t nt_workspace(int M, int N, int K, int dtype, int phase);

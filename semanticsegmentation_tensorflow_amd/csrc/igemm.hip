@@ -874,6 +874,16 @@ static bool nt_plan_bn2(const NTPlan& pl, int dtype) {
 
 bool nt_bn2_ok(const NTParams& p, int dtype) { return nt_plan_bn2(nt_plan(p, dtype, 1, p.M), dtype); }
 
+// Whether the planned launch reads the ReluGrad mask as bits
+// (EpiParams::mask_bits): the 64-wide conv_res64 plan, which launch_res64 runs
+// on conv_res64pp.
+static bool nt_plan_mask_bits(const NTPlan& pl) { return pl.kind == NTK_RES64 && pl.bn == 64; }
+
+bool nt_mask_bits_ok(const NTParams& p, int dtype) {
+    if ((dtype != SEG_BF16 && dtype != SEG_F16) || p.pro.gamma || p.phase || !p.epi.mask_bits) return false;
+    return nt_plan_mask_bits(nt_plan(p, dtype, 1, p.M));
+}
+
 template <typename T>
 static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t ws_bytes, hipStream_t s) {
     constexpr int BK = 128 / sizeof(T);
@@ -886,6 +896,9 @@ static int launch_nt_typed(NTParams& p, int nphases, int max_m, void* ws, size_t
     if (p.epi.unpool_y && (nphases != 1 || !nt_plan_unpools(pl, p))) return SEG_EINVAL;
     if (p.bt && (nphases != 1 || pl.kind != NTK_NT3 || p.C % 64 || p.kv)) return SEG_EINVAL;
     if (p.epi.y2 && (nphases != 1 || !nt_plan_bn2(pl, dt_traits<T>::id))) return SEG_EINVAL;
+    // the mask bits are read by conv_res64pp alone and written by conv_c8_fwd
+    // alone (seg_conv2d_fwd_relu_bits, which does not come here)
+    if (p.epi.ybits || (p.epi.mask_bits && (nphases != 1 || !nt_plan_mask_bits(pl)))) return SEG_EINVAL;
     int splits = pl.splits;
     p.partial = nullptr;
     switch (pl.kind) {

@@ -9,7 +9,10 @@
 //    from the LDS input halo (taps 9..11 read a zero slot);
 //  * the filter (3 k-steps x K/16 fragments) stays in VGPRs for the block;
 //  * block = 8 x 64 output pixels, 4 waves x 2 rows, one 16-pixel fragment
-//    at a time; bias + ReLU, staged through LDS into 16-byte row stores.
+//    at a time; bias + ReLU, staged through LDS into 16-byte row stores;
+//  * optionally the ReLU mask as bits beside the map (EpiParams::ybits: one
+//    byte per 16-byte chunk), read by the next conv's input gradient instead
+//    of the 2-byte map (seg_conv2d_fwd_relu_bits).
 #include "common.h"
 #include "igemm.h"
 
@@ -107,10 +110,29 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
         for (int q = lane; q < 16 * (KN / 8); q += 64) {
             const int px = q / (KN / 8), ch = q - (q / (KN / 8)) * (KN / 8);
             const int ox = ox0 + px0 + px;
-            if (oy < p.OH && ox < p.OW) {
-                const uint4 v = *reinterpret_cast<const uint4*>(st + px * SROW + ch * 8);
+            const bool inb = oy < p.OH && ox < p.OW;
+            const uint4 v = *reinterpret_cast<const uint4*>(st + px * SROW + ch * 8);
+            if (inb)
                 *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p.y) + (long)img * p.y_img +
                                           ((long)oy * p.OW + ox) * p.ldy + ch * 8) = v;
+            if (e.ybits) {         // ReLU mask bits of the stored values: byte ch of the pixel's row
+                const T* tv = reinterpret_cast<const T*>(&v);
+                unsigned b = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) b |= (to_f32(tv[i]) > 0.f ? 1u : 0u) << i;
+                unsigned char* row = e.ybits + (((long)img * p.OH + oy) * p.OW + ox) * e.ld_bits;
+                if constexpr (KN == 64) {
+                    // a pixel's 8 chunks are 8 consecutive lanes: gather its
+                    // 64 bits into lane ch == 0 (two quad swaps, one shift by
+                    // 4 lanes) for one 8-byte store instead of eight 1-byte ones
+                    unsigned wd = b << (8 * (ch & 3));
+                    wd |= (unsigned)__builtin_amdgcn_mov_dpp((int)wd, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+                    wd |= (unsigned)__builtin_amdgcn_mov_dpp((int)wd, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+                    const unsigned hi = __shfl_down(wd, 4);
+                    if (inb && ch == 0) *reinterpret_cast<uint2*>(row) = uint2{wd, hi};
+                } else if (inb) {
+                    row[ch] = (unsigned char)b;
+                }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next writes

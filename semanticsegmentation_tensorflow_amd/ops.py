@@ -359,6 +359,48 @@ def conv2d_bwd_data(desc, dy, w_hwio, dx, ws=None, stream=None, epi=None):
     return dx
 
 
+def conv2d_fwd_relu_bits_ok(desc):
+    """Whether seg_conv2d_fwd_relu_bits (the forward that also writes its ReLU
+    mask as bits) takes this conv."""
+    return bool(_lib.lib().seg_conv2d_fwd_relu_bits_ok(ctypes.byref(desc)))
+
+
+def relu_bits_buffer(n, h, w, k, device):
+    """The bit-packed ReLU mask of an [n, h, w, k] map: k / 8 bytes per pixel."""
+    return torch.empty((n, h, w, (k + 7) // 8), dtype=torch.uint8, device=device)
+
+
+def conv2d_fwd_relu_bits(desc, x, w_krsc, y, bits, epi=None, stream=None):
+    """Conv2D + epilogue that also writes bits[..., k // 8] bit k % 8 = y[..., k] > 0
+    (seg_conv2d_fwd_relu_bits), for conv2d_bwd_data_bits of the next conv."""
+    d = _with_ld(desc, x, y)
+    if not bits.is_contiguous() or bits.dtype != torch.uint8:
+        raise ValueError("relu bits: a contiguous uint8 [N, OH, OW, K/8] buffer")
+    check(_lib.lib().seg_conv2d_fwd_relu_bits(ctypes.byref(d), ptr(x), ptr(w_krsc),
+                                              None if epi is None else ctypes.byref(epi), ptr(y), ptr(bits),
+                                              bits.shape[-1], stream_ptr(stream)), "conv2d_relu_bits")
+    return y
+
+
+def conv2d_bwd_data_bits_ok(desc):
+    """Whether seg_conv2d_bwd_data_bits (the ReluGrad mask read as bits) takes this conv."""
+    return bool(_lib.lib().seg_conv2d_bwd_data_bits_ok(ctypes.byref(desc)))
+
+
+def conv2d_bwd_data_bits(desc, dy, w_hwio, bits, dx, mask_scale=1.0, ws=None, stream=None):
+    """Conv2DBackpropInput with the ReluGrad (x mask_scale) of the layer that
+    produced this conv's input, its mask given as conv2d_fwd_relu_bits' bits."""
+    d = _with_ld(desc, dx, dy)
+    if not bits.is_contiguous() or bits.dtype != torch.uint8:
+        raise ValueError("relu bits: a contiguous uint8 [N, H, W, C/8] buffer")
+    wsp, wss = (ws or Workspace(dy.device)).ptr_size(conv_workspace(d, OP_BWD_DATA))
+    epi = epilogue(mask_scale=mask_scale)
+    check(_lib.lib().seg_conv2d_bwd_data_bits(ctypes.byref(d), ptr(dy), ptr(w_hwio), ctypes.byref(epi), ptr(bits),
+                                              bits.shape[-1], ptr(dx), wsp, wss, stream_ptr(stream)),
+          "conv2d_backprop_input_bits")
+    return dx
+
+
 def conv2d_bwd_data_unpool_ok(desc):
     """Whether seg_conv2d_bwd_data_unpool (Conv2DBackpropInput + MaxPoolGrad in
     one launch) takes this convolution."""

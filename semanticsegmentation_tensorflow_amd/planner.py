@@ -444,6 +444,33 @@ class PlanMixin:
             p.unpool_fuse[id(c)] = m
         p.unpool_pools = {id(m) for m in p.unpool_fuse.values()}
 
+    def _plan_relu_bits(self, p, consumers):
+        """The ReluGrad mask as bits: a mask-fused ReLU conv whose forward runs
+        on the first-layer kernel (FCN / VGG conv1_1, Network/model/FCN.py:55)
+        also writes its ReLU mask at 1 bit per element, and its consumer conv's
+        input gradient (conv1_2's, on conv_res64pp) reads those instead of the
+        16-bit map: 8 instead of 128 bytes per pixel.  p.mask_bits: producer
+        conv id -> uint8 [N, OH, OW, K/8]; p.bits_dgrad: the consumer conv ids."""
+        p.mask_bits = {}
+        p.bits_dgrad = set()
+        if not self.relu_bits or self.cdt == ops.F32:
+            return
+        for n in p.nodes:
+            if n.kind != "conv" or id(n) not in p.mask_fuse:
+                continue
+            if (id(n) in p.pool_fuse or id(n) in p.bn_out2 or getattr(n, "pro", None) is not None
+                    or getattr(n, "fwd_hwio", False) or p.buf.get(id(n.output)) is None):
+                continue
+            c = consumers[id(n.output)][0]
+            if (c.kind != "conv" or getattr(c, "pro", None) is not None or id(c) in p.bn_before
+                    or id(c) in p.unpool_fuse or id(n.output) in p.alias):
+                continue
+            if not (ops.conv2d_fwd_relu_bits_ok(n.desc) and ops.conv2d_bwd_data_bits_ok(c.desc)):
+                continue
+            N, H, W, K = p.shapes[id(n.output)]
+            p.mask_bits[id(n)] = ops.relu_bits_buffer(N, H, W, K, self.device)
+            p.bits_dgrad.add(id(c))
+
     def _plan_bn_outputs(self, p, consumers):
         """Conv -> (its epilogue's dropout) -> BatchNorm(+ReLU): FC-DenseNet's
         bottleneck conv1 -> BN -> ReLU before the growth conv
@@ -517,6 +544,7 @@ class PlanMixin:
             if c.kind in ("conv", "tconv") or (c.kind == "MaxPool" and n.kp is None):
                 p.mask_fuse.add(id(n))
         self._plan_unpool_fusion(p, consumers)
+        self._plan_relu_bits(p, consumers)
         p.adam_fusable = set()
         p.wg_ws = {}                     # per-conv filter-gradient workspace (pending split-K slabs)
         for n in p.nodes:

@@ -180,6 +180,9 @@ class Session(PlanMixin, StreamMixin):
         # filters of >= 8 M elements: one packed copy (HWIO), read by the
         # forward too (igemm_nt3's B-transposed form) -- set before the first run
         self.fwd_hwio = True
+        # conv1_1's ReLU mask written as bits for conv1_2's input gradient
+        # (planner._plan_relu_bits)
+        self.relu_bits = True
         # conv -> BatchNorm(+ReLU): the BN output written by the conv epilogue
         self.fuse_bn_out = True
         # the dgamma / dbeta sums of the BN backwards fused into input-gradient
@@ -710,6 +713,9 @@ class Session(PlanMixin, StreamMixin):
                 elif getattr(n, "fwd_hwio", False):
                     self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd_hwio, n.desc, x,
                                 store.packed[(n.w.var_name, ops.PACK_HWIO)][0], y, epi, self.ws)
+                elif id(n) in getattr(p, "mask_bits", {}):
+                    self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd_relu_bits, n.desc, x,
+                                store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, p.mask_bits[id(n)], epi)
                 else:
                     self._timed(n.desc, ops.OP_FWD, ops.conv2d_fwd, n.desc, x,
                                 store.packed[(n.w.var_name, ops.PACK_KRSC)][0], y, epi, self.ws)
@@ -1190,6 +1196,12 @@ class Session(PlanMixin, StreamMixin):
                                     store.packed[(n.w.var_name, ops.PACK_HWIO)][0], acc, ws, None,
                                     ops.epilogue(residual=acc))
                         dx = acc
+                    elif mepi is not None and acc is None and id(n) in p.bits_dgrad:
+                        # the ReluGrad mask from the producer's bits (planner._plan_relu_bits)
+                        self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data_bits, n.desc, dz,
+                                    store.packed[(n.w.var_name, ops.PACK_HWIO)][0],
+                                    p.mask_bits[id(p.producer[id(x)])], dx, mepi.mask_scale, ws)
+                        done(dx, acc)
                     else:
                         self._timed(n.desc, ops.OP_BWD_DATA, ops.conv2d_bwd_data, n.desc, dz,
                                     store.packed[(n.w.var_name, ops.PACK_HWIO)][0], dx, ws, None, mepi)

@@ -333,6 +333,12 @@ def test_c2_kernel_set_is_the_benchmarked_one(c2):
     # pool1 / pool2's MaxPoolGrad inside conv2_1 / conv3_1's input-gradient
     # launches; conv4_1 / conv5_1 split K and keep the separate MaxPoolGrad
     assert {n for n, r in recs.items() if r["unpool"] is not None} == {"conv2_1/weights", "conv3_1/weights"}
+    # conv1_1's ReLU mask as bits (conv_c8_fwd), read by conv1_2's masked input
+    # gradient (conv_res64pp) -- the layer-local test checks that dx
+    assert len(plan.mask_bits) == 1 and plan.bits_dgrad == {id(n) for n in plan.nodes
+                                                             if getattr(n, "w", None) is not None
+                                                             and n.w.var_name == "conv1_2/weights"}
+    assert recs["conv1_2/weights"]["dx_masked"]
 
 
 def test_c2_layer_local_parity(c2):

@@ -24,7 +24,8 @@ class _Rec:
                              "seg_bias_grad_workspace", "seg_xent_workspace", "seg_status_string",
                              "seg_adam_segments_plan", "seg_tconv_filter_apad",
                              "seg_conv_wgrad_adam_fusable", "seg_conv_bwd_data_bn_workspace",
-                             "seg_conv2d_fwd_pool_ok", "seg_conv2d_fwd_bn2_ok", "seg_conv2d_fwd_hwio_ok")
+                             "seg_conv2d_fwd_pool_ok", "seg_conv2d_fwd_bn2_ok", "seg_conv2d_fwd_hwio_ok",
+                             "seg_conv2d_fwd_relu_bits_ok", "seg_conv2d_bwd_data_bits_ok")
 
         def fn(*a):
             if host_only:
@@ -65,14 +66,19 @@ def test_fcn_train_plan(dry):
     fused = c.count("seg_conv2d_fwd_pool")
     # conv6 / conv7 read their one (HWIO) packed copy
     assert c.count("seg_conv2d_fwd_hwio") == 2
-    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_hwio") + fused == 17
+    # conv1_1 (first-layer kernel) also writes its ReLU mask as bits, read by
+    # conv1_2's input gradient instead of the 16-bit map
+    assert c.count("seg_conv2d_fwd_relu_bits") == 1
+    assert c.count("seg_conv2d_bwd_data_bits") == 1
+    assert (c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_hwio") + c.count("seg_conv2d_fwd_relu_bits")
+            + fused == 17)
     assert c.count("seg_tconv2d_fwd") == 3
     # train plans record the pool switches; MaxPoolGrad reads them instead of x
     assert c.count("seg_maxpool2x2_fwd_argmax") + fused == 5
     assert fused >= 1                                  # conv1_2 (conv_res64) at least
     assert c.count("seg_softmax_xent_fwd_bwd") == 1
     # backward: conv1_1 needs no input gradient (image is a placeholder)
-    assert c.count("seg_conv2d_bwd_data") == 16
+    assert c.count("seg_conv2d_bwd_data") + c.count("seg_conv2d_bwd_data_bits") == 16
     # conv6 / conv7 filters (bf16, 256x256 TN tiles without split-K) take the
     # wgrad+Adam fused launch; the other 15 the plain filter gradient
     assert c.count("seg_conv2d_bwd_filter") == 15
@@ -101,7 +107,7 @@ def test_fcn_train_plan(dry):
     assert plan.nsegs == len(sess.store.vars) - 2
     assert "conv6/weights" not in gk[1] and "conv7/weights" not in gk[1]
     assert (dry.calls.count("seg_conv2d_fwd") + dry.calls.count("seg_conv2d_fwd_pool")
-            + dry.calls.count("seg_conv2d_fwd_hwio")) == 17
+            + dry.calls.count("seg_conv2d_fwd_hwio") + dry.calls.count("seg_conv2d_fwd_relu_bits")) == 17
 
 
 def test_adam_segment_plan_host():

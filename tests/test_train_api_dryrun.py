@@ -54,7 +54,8 @@ def test_accumulate_template_plan(dry):  # noqa: F811
     dry.calls.clear()
     sess.run(accum_ops, feed_dict=feed)
     c = dry.calls
-    assert c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pool") + c.count("seg_conv2d_fwd_hwio") == 17
+    assert (c.count("seg_conv2d_fwd") + c.count("seg_conv2d_fwd_pool") + c.count("seg_conv2d_fwd_hwio")
+            + c.count("seg_conv2d_fwd_relu_bits") == 17)
     # no optimizer in this run: every filter gradient is a plain launch
     assert c.count("seg_conv2d_bwd_filter") == 17 and "seg_conv2d_bwd_filter_adam" not in c
     assert "seg_adam_tf1_pack" not in c
@@ -64,7 +65,7 @@ def test_accumulate_template_plan(dry):  # noqa: F811
     sess.run(train_step, feed_dict=feed)
     c = dry.calls
     assert "seg_conv2d_fwd" not in c and "seg_conv2d_fwd_pool" not in c   # apply_gradients: no forward pass
-    assert "seg_conv2d_fwd_hwio" not in c
+    assert "seg_conv2d_fwd_hwio" not in c and "seg_conv2d_fwd_relu_bits" not in c
     assert c.count("seg_axpy") == 40 and c.count("seg_adam_tf1_pack") == 1
     assert st.step == 1
 
@@ -101,7 +102,7 @@ def test_minimize_var_list_skips_frozen_layer(dry):  # noqa: F811
     # input gradients still flow to the trainable layers below
     assert c.count("seg_conv2d_bwd_filter") == 17 - 1 - 1
     assert c.count("seg_conv2d_bwd_filter_adam") == 1
-    assert c.count("seg_conv2d_bwd_data") == 16
+    assert c.count("seg_conv2d_bwd_data") + c.count("seg_conv2d_bwd_data_bits") == 16
     (gk, plan), = sess._adam_groups.items()
     assert not (set(gk[1]) & frozen)
     assert plan.nsegs == len(var_list) - 1                 # conv7 filter updated in its fused launch

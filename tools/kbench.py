@@ -28,8 +28,8 @@ LAYERS = {"conv1_1": (384, 1248, 3, 64, 3), "conv1_2": (384, 1248, 64, 64, 3),
           "conv3_1": (96, 312, 128, 256, 3), "conv3_2": (96, 312, 256, 256, 3),
           "conv4_1": (48, 156, 256, 512, 3), "conv4_2": (48, 156, 512, 512, 3),
           "conv5_1": (24, 78, 512, 512, 3), "conv6": (12, 39, 512, 4096, 7), "conv7": (12, 39, 4096, 4096, 1)}
-OPS = {"fwd": ops.OP_FWD, "dgrad": ops.OP_BWD_DATA, "wgrad": ops.OP_BWD_FILTER, "wgrad_adam": ops.OP_BWD_FILTER,
-       "fwdp": ops.OP_FWD, "dgradp": ops.OP_BWD_DATA, "fwdpool": ops.OP_FWD, "fwd+pool": ops.OP_FWD}
+OPS = {"fwd": ops.OP_FWD, "dgrad": ops.OP_BWD_DATA, "dgradnm": ops.OP_BWD_DATA, "dgradbits": ops.OP_BWD_DATA,
+       "wgrad": ops.OP_BWD_FILTER, "wgrad_adam": ops.OP_BWD_FILTER, "fwdbits": ops.OP_FWD, "fwdp": ops.OP_FWD, "dgradp": ops.OP_BWD_DATA, "fwdpool": ops.OP_FWD, "fwd+pool": ops.OP_FWD}
 WPAD = 64   # fwdp / dgradp: packed filter rows padded by WPAD elements (diagnostic option "wpad")
 
 
@@ -73,6 +73,24 @@ def setup(spec, N, dev, ws):
             ops.conv2d_fwd(d, x, wk, y, epi, ws)
             ops.maxpool2x2_fwd_argmax(y, yp, idx)
         return d, op, pair
+    if op == "fwdbits":     # the forward that also writes its ReLU mask as bits
+        wk = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_KRSC, d.C), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wk, d.C, d.K, ops.PACK_KRSC)
+        y = torch.empty(N, d.OH, d.OW, d.K, dtype=torch.bfloat16, device=dev)
+        bits = ops.relu_bits_buffer(N, d.OH, d.OW, d.K, dev)
+        b = torch.zeros(K, device=dev)
+        return d, op, lambda: ops.conv2d_fwd_relu_bits(d, x, wk, y, bits, ops.epilogue(bias=b, relu=True))
+    if op == "dgradbits":   # the ReluGrad mask read as bits
+        wh = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wh, d.C, d.K, ops.PACK_HWIO)
+        dx = torch.empty(N, H, W, d.C, dtype=torch.bfloat16, device=dev)
+        bits = torch.randint(0, 256, (N, H, W, d.C // 8), dtype=torch.uint8, device=dev, generator=g)
+        return d, op, lambda: ops.conv2d_bwd_data_bits(d, dy, wh, bits, dx, 1.0, ws)
+    if op == "dgradnm":     # the input gradient without the ReluGrad mask epilogue
+        wh = torch.zeros(ops.packed_shape(R, R, C, K, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
+        ops.pack_filter(w32, wh, d.C, d.K, ops.PACK_HWIO)
+        dx = torch.empty(N, H, W, d.C, dtype=torch.bfloat16, device=dev)
+        return d, op, lambda: ops.conv2d_bwd_data(d, dy, wh, dx, ws, None, None)
     if op in ("dgrad", "dgradp"):
         wh = torch.zeros(ops.packed_shape(R, R, C, K + pad, ops.PACK_HWIO, d.C), dtype=torch.bfloat16, device=dev)
         ops.pack_filter(w32, wh, d.C, d.K + pad, ops.PACK_HWIO)
