@@ -380,6 +380,8 @@ void launch_smallc_wgrad(TNParams& p, int dtype, int splits, hipStream_t s);
 // halo-tiled filter gradient (wgrad.hip) for stride-1 3x3 TN problems
 struct WgradPlan {
     int bw, nt, splits, nbias;
+    int pxs;      // pixel-split waves (wgrad_halo<64, ..., PXS>)
+    int slabs;    // split-K slabs written (splits, x 2 with pxs)
     long blocks;
     int g[10];
 };

@@ -1155,13 +1155,13 @@ static int launch_tn_typed(TNParams& p, void* ws, size_t ws_bytes, hipStream_t s
     WgradPlan wp;
     if (sizeof(T) == 2 && g_tn_variant == 2 && wgrad_plan(p, dt_traits<T>::id, num_cus(), &wp)) {
         if (p.dbias) p.Mp = p.M + wp.nbias;   // wgrad_halo sums dy columns too (nbias partial rows)
-        if (wp.splits > 1) {
+        if (wp.slabs > 1) {
             if (!ws || ws_bytes < wgrad_workspace(wp, p)) return SEG_EWORKSPACE;
             p.partial = reinterpret_cast<float*>(ws);
         }
         launch_wgrad(p, wp, s, dt_traits<T>::id);
         SEG_CHECK_LAUNCH();
-        tn_finish(p, wp.splits, s);
+        tn_finish(p, wp.slabs, s);
         SEG_CHECK_LAUNCH();
         p.dbias = nullptr;                    // done
         return SEG_OK;

@@ -20,6 +20,13 @@
 //  * pipeline: 2 LDS stages, tile t+1 staged right after the barrier that
 //    retires tile t; one barrier per tile (36 x NF MFMAs per wave between).
 //  * split-K over pixel-tile ranges -> fp32 slabs + splitk_reduce_tn.
+//  * PXS (64-wide dy tiles, round 6): the waves split the tile's pixels
+//    instead of its columns -- wave (cf, ph) owns all 64 columns for
+//    substeps 2 ph, 2 ph + 1 -- so each A fragment read feeds 4 MFMAs instead
+//    of 2 (conv1_2's filter gradient, 64 -> 64, was bound by the LDS fragment
+//    reads: 22 per 18 MFMAs); each half writes its own split-K slab (slab
+//    2 split + ph), so the reducer adds twice the partials.  (Adding the
+//    halves through LDS instead spilled 48-65 VGPRs.)
 //
 // Covers the 3x3 layers of FCN (Network/model/FCN.py:55-99) and FC-DenseNet.
 #include "common.h"
@@ -48,12 +55,13 @@ __device__ __forceinline__ int wg_swz(int row) {
 // pieces per wave (8 rows each): 4 covers dilation 1, 5 dilation 2.
 // ABL (diagnostic builds, garbage results): 1 no DMA in the loop, 2 no MFMA,
 // 3 no LDS fragment reads.
-template <int NT, int NST, int HI, int ABL = 0, typename T = bf16>
+template <int NT, int NST, int HI, int ABL = 0, typename T = bf16, bool PXS = false>
 __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
     constexpr int BW = 16;
     using V8 = vec8_t<T>;
     constexpr int NW = 8, BH = 128 / BW;
-    constexpr int NF = NT / 32;               // n fragments per wave
+    constexpr int NF = PXS ? NT / 16 : NT / 32;   // n fragments per wave
+    static_assert(!PXS || NT == 64, "pixel-split waves hold all 64 columns");
     constexpr int DROWB = NT * 2;             // dy tile row bytes
     constexpr int D_RPI = 1024 / DROWB;       // dy rows per DMA instruction
     constexpr int D_INS = 128 / D_RPI / NW;   // dy DMA instructions per wave
@@ -74,7 +82,9 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int cf = w & 3, nh = w >> 2;
+    const int cf = w & 3;
+    const int nh = PXS ? 0 : w >> 2;          // column half (PXS: all columns)
+    const int ph = PXS ? w >> 2 : 0;          // PXS: pixel half (substeps 2 ph, 2 ph + 1)
     const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
     const T* __restrict__ Dy = reinterpret_cast<const T*>(p.b);
     const void* zero = (const void*)wg_zero_page;
@@ -236,17 +246,19 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             return __builtin_bit_cast(V8, v);
         };
+        const int ss0 = 2 * ph;
         V8 b0[NF], b1[NF];
-        read_b(0, b0);
-        V8 a_cur = read_a(0, 0);
+        read_b(ss0, b0);
+        V8 a_cur = read_a(ss0, 0);
         // one substep: 9 taps, A(tap+1) read ahead, next substep's B at tap 4
-        auto substep = [&](int ss, V8* bc, V8* bn) {
+        // (more: a next substep follows in this wave)
+        auto substep = [&](int ss, V8* bc, V8* bn, bool more) {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 V8 a_nxt = a_cur;
                 if (tap < 8) a_nxt = read_a(ss, tap + 1);
-                else if (ss + 1 < 4) a_nxt = read_a(ss + 1, 0);
-                if (tap == 4 && ss + 1 < 4) read_b(ss + 1, bn);
+                else if (more) a_nxt = read_a(ss + 1, 0);
+                if (tap == 4 && more) read_b(ss + 1, bn);
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     if constexpr (ABL == 2) asm volatile("" ::"v"(a_cur), "v"(bc[ni]));
@@ -255,15 +267,20 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 a_cur = a_nxt;
             }
         };
+        if constexpr (PXS) {
+            substep(ss0, b0, b1, true);
+            substep(ss0 + 1, b1, b0, false);
+        } else {
 #pragma unroll 1
-        for (int ss = 0; ss < 4; ss += 2) {
-            substep(ss, b0, b1);
-            substep(ss + 1, b1, b0);
+            for (int ss = 0; ss < 4; ss += 2) {
+                substep(ss, b0, b1, true);
+                substep(ss + 1, b1, b0, ss + 2 < 4);
+            }
         }
         buf = buf == NST - 1 ? 0 : buf + 1;
     }
-
     const int fr = lane & 15;
+    const int slab = PXS ? 2 * split + ph : split;
     if (do_bias) {
 #pragma unroll
         for (int ni = 0; ni < NF; ++ni) {
@@ -276,7 +293,7 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
                 if (ni != cf) continue;
                 const int n = n0 + nh * (NT / 2) + ni * 16 + fr;
                 if (p.partial) {
-                    if (n < p.N) p.partial[((long)split * p.Mp + p.M + ct) * p.N + n] = dsum[ni];
+                    if (n < p.N) p.partial[((long)slab * p.Mp + p.M + ct) * p.N + n] = dsum[ni];
                 } else if (n < p.n_valid) {
                     p.dbias[n] = dsum[ni];
                 }
@@ -290,7 +307,7 @@ __global__ __launch_bounds__(512) void wgrad_halo(TNParams p, WGGeom g) {
             const int c = c0 + cf * 16 + fg * 4 + j;
             const int m = tap * p.Cg + c;
             if (p.partial) {
-                float* prow = p.partial + ((long)split * p.Mp + m) * p.N;
+                float* prow = p.partial + ((long)slab * p.Mp + m) * p.N;
 #pragma unroll
                 for (int ni = 0; ni < NF; ++ni) {
                     const int n = n0 + nh * (NT / 2) + ni * 16 + fr;
@@ -339,6 +356,10 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
     splits = (ptiles + tps - 1) / tps;
     wp->g[5] = nct; wp->g[6] = nnt; wp->g[7] = splits; wp->g[8] = tps; wp->g[9] = ptiles;
     wp->splits = splits;
+    // 64-wide dy tiles (no second column block to share an A fragment read):
+    // pixel-split waves, two slabs per split
+    wp->pxs = wp->nt == 64 && g_wgrad_pxs && splits > 1;
+    wp->slabs = splits * (wp->pxs ? 2 : 1);
     wp->nbias = splits > 1 ? std::max(1, std::min(nct, g_wgrad_nbias)) : 1;
     wp->blocks = (long)nout * splits;
     return true;
@@ -346,7 +367,7 @@ bool wgrad_plan(const TNParams& p, int dtype, int cus, WgradPlan* wp) {
 
 size_t wgrad_workspace(const WgradPlan& wp, const TNParams& p) {
     // + nbias slab rows for the fused BiasAddGrad partials
-    return wp.splits > 1 ? (size_t)wp.splits * (p.M + wp.nbias) * p.N * sizeof(float) : 0;
+    return wp.slabs > 1 ? (size_t)wp.slabs * (p.M + wp.nbias) * p.N * sizeof(float) : 0;
 }
 
 void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
@@ -364,6 +385,16 @@ void launch_wgrad(TNParams& p, const WgradPlan& wp, hipStream_t s, int dtype) {
         return;
     }
 #endif
+    if (wp.pxs) {
+        if (dtype == SEG_F16) {
+            if (small) hipLaunchKernelGGL((wgrad_halo<64, 3, 4, 0, f16, true>), grid, block, 0, s, p, g);
+            else hipLaunchKernelGGL((wgrad_halo<64, 2, 5, 0, f16, true>), grid, block, 0, s, p, g);
+        } else {
+            if (small) hipLaunchKernelGGL((wgrad_halo<64, 3, 4, 0, bf16, true>), grid, block, 0, s, p, g);
+            else hipLaunchKernelGGL((wgrad_halo<64, 2, 5, 0, bf16, true>), grid, block, 0, s, p, g);
+        }
+        return;
+    }
     if (dtype == SEG_F16) {
         if (wp.nt == 128) hipLaunchKernelGGL((wgrad_halo<128, 2, 4, 0, f16>), grid, block, 0, s, p, g);
         else if (wp.nt == 32 && small) hipLaunchKernelGGL((wgrad_halo<32, 3, 4, 0, f16>), grid, block, 0, s, p, g);

@@ -186,8 +186,8 @@ def test_conv2d_bwd_data(dev, ntv, case, dtype, masked):
     assert_close(from_dev(dx, C), want, dtype, f"conv bwd_data {case}")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
-                                                   "wgrad-nbias4", "tn3-half"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["tn1", "tn2", "wgrad-halo", "wgrad-halo128", "tn3",
+                                                      "wgrad-nbias4", "tn3-half", "wgrad-halo-colsplit"])
 def tnv(request, dev):
     """Run filter-gradient tests on every kernel generation: 1 = register-staged
     TN GEMM, 2 = LDS-DMA TN GEMM, 3 = 2 + the halo-tiled 3x3 filter gradient
@@ -196,15 +196,18 @@ def tnv(request, dev):
     in 2 so igemm_tn2 stays covered for wide problems), 6 = 4 with the fused
     BiasAddGrad spread over up to 4 channel blocks (extra slab rows), 7 = 5
     with the 256x128 two-blocks-per-CU tiles also for plain single-split
-    launches."""
+    launches; 3 runs the 64-wide tiles on pixel-split waves (two slabs per
+    split, round 6), 8 the same tiles on column-split waves."""
     v = request.param
     ops.set_option("igemm_tn_variant", 1 if v == 1 else 2)
-    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6) else 0)
+    ops.set_option("wgrad_halo", 1 if v in (3, 4, 6, 8) else 0)
     ops.set_option("wgrad_nt", 128 if v in (4, 6) else 64)
+    ops.set_option("wgrad_pxs", 0 if v == 8 else 1)
     ops.set_option("wgrad_nbias", 4 if v == 6 else 1)
     ops.set_option("tn3", 0 if v == 2 else 1)
     ops.set_option("tn3_half", 7 if v == 7 else 0)
     yield v
+    ops.set_option("wgrad_pxs", 1)
     ops.set_option("tn3_half", 0)
     ops.set_option("tn3", 1)
     ops.set_option("wgrad_nbias", 1)
