@@ -467,8 +467,8 @@ class PlanMixin:
                 continue
             if not (ops.conv2d_fwd_relu_bits_ok(n.desc) and ops.conv2d_bwd_data_bits_ok(c.desc)):
                 continue
-            N, H, W, K = p.shapes[id(n.output)]
-            p.mask_bits[id(n)] = ops.relu_bits_buffer(N, H, W, K, self.device)
+            N, H, W = p.shapes[id(n.output)][:3]
+            p.mask_bits[id(n)] = ops.relu_bits_buffer(N, H, W, n.desc.K, self.device)   # padded channels
             p.bits_dgrad.add(id(c))
 
     def _plan_bn_outputs(self, p, consumers):
