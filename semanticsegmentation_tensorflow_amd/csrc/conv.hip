@@ -548,6 +548,7 @@ const Knob* find_knob(const char* name) {
         {"wgrad_nt", &seg::KnobSet::wgrad_nt, 0, 0, 0, {64, 128}},
         {"wgrad_halo", &seg::KnobSet::wgrad_halo, 0, 1, 1, {}},
         {"wgrad_pxs", &seg::KnobSet::wgrad_pxs, 0, 1, 1, {}},         // 64-wide wgrad_halo tiles: pixel-split waves
+        {"smallc_tr", &seg::KnobSet::smallc_tr, 0, 1, 1, {}},         // conv_c8_fwd: transposed accumulators, 8-byte staging
         {"res16c", &seg::KnobSet::res16c, 0, 1, 1, {}},
         {"res16", &seg::KnobSet::res16, 0, 1, 1, {}},
         {"res64", &seg::KnobSet::res64, 0, 1, 1, {}},

@@ -27,6 +27,7 @@ namespace seg {
     X(res16, 1) \
     X(res64_pp, 1) \
     X(wgrad_pxs, 1) \
+    X(smallc_tr, 1) \
     X(res16_dma, 1) \
     X(res16c_bh, 4) \
     X(res16c, 1) \
@@ -86,6 +87,7 @@ KnobSet& knobs();
 #define g_res16 (::seg::knobs().res16.load(std::memory_order_relaxed))   // conv_res64 with 16-wide output blocks for N <= 16
 #define g_res64_pp (::seg::knobs().res64_pp.load(std::memory_order_relaxed))
 #define g_wgrad_pxs (::seg::knobs().wgrad_pxs.load(std::memory_order_relaxed))
+#define g_smallc_tr (::seg::knobs().smallc_tr.load(std::memory_order_relaxed))
 #define g_res16_dma (::seg::knobs().res16_dma.load(std::memory_order_relaxed))
 #define g_res16c_bh (::seg::knobs().res16c_bh.load(std::memory_order_relaxed))   // tile rows of the BN-backward conv_res16c (8 or 4)
 #define g_res16c (::seg::knobs().res16c.load(std::memory_order_relaxed))   // conv_res16c: 16 input channels (growth-conv input gradients)

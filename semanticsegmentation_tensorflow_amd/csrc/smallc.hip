@@ -24,7 +24,11 @@ constexpr int SC_BH = 8, SC_BW = 64;
 constexpr int SC_HW = SC_BW + 2;                       // halo width (3x3, dilation 1)
 constexpr int SC_HROWS = (SC_BH + 2) * SC_HW;          // 660 halo pixels
 
-template <int NF, typename T>
+// TR (round 6): D^T = W . X^T, so a lane holds 4 consecutive channels of one
+// pixel and stages them with one 8-byte LDS write per fragment column block
+// instead of four 2-byte ones per channel row (16 -> 4 LDS writes per lane
+// and fragment)
+template <int NF, typename T, bool TR = false>
 __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int tiles_y) {
     constexpr int KN = NF * 16;
     constexpr int SROW = KN + 8;                       // staged bf16 row (pad vs bank conflicts)
@@ -66,6 +70,14 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
         }
     }
     const EpiParams& e = p.epi;
+    float bv[NF][4];        // TR: bias of the lane's channels nf * 16 + 4 fg + j
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = nf * 16 + 4 * fg + j;
+            bv[nf][j] = (TR && e.bias && n < e.n_valid) ? e.bias[n] : 0.f;
+        }
     __syncthreads();
 
     // A address of this lane for k-step ks: tap (r, s) of pixel (py, px)
@@ -89,8 +101,23 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
             const uint4 a = halo[hr];
 #pragma unroll
             for (int nf = 0; nf < NF; ++nf)
-                acc[nf] = mfma16x16x32<T>(a, bw[ks][nf], acc[nf]);
+                acc[nf] = TR ? mfma16x16x32<T>(bw[ks][nf], a, acc[nf]) : mfma16x16x32<T>(a, bw[ks][nf], acc[nf]);
         }
+        if constexpr (TR) {
+            // D^T: lane holds channels n0 + j (n0 = nf*16 + 4*fg) of pixel fr
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf) {
+                const int n0 = nf * 16 + 4 * fg;
+                T o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float v = acc[nf][j] + bv[nf][j];
+                    if (e.relu) v = fmaxf(v, 0.f);
+                    o[j] = from_f32<T>(n0 + j < e.n_valid ? v : 0.f);
+                }
+                *reinterpret_cast<uint2*>(st + fr * SROW + n0) = *reinterpret_cast<const uint2*>(o);
+            }
+        } else {
         // D: lane holds rows (pixels) 4*fg + j, column n = nf*16 + fr
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) {
@@ -102,6 +129,7 @@ __global__ __launch_bounds__(256) void conv_c8_fwd(NTParams p, int tiles_x, int 
                 if (e.relu) v = fmaxf(v, 0.f);
                 st[(4 * fg + j) * SROW + n] = from_f32<T>(n < e.n_valid ? v : 0.f);
             }
+        }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own wave's stage writes
         // 16 px x KN/8 chunks of 16 B
@@ -154,6 +182,15 @@ void launch_smallc_fwd_t(NTParams& p, hipStream_t s) {
     const int tx = (p.OW + SC_BW - 1) / SC_BW, ty = (p.OH + SC_BH - 1) / SC_BH;
     const int nimg = p.M / (p.OH * p.OW);
     const dim3 grid(nimg * tx * ty), block(256);
+    if (g_smallc_tr) {
+        switch (p.N / 16) {
+            case 1: hipLaunchKernelGGL((conv_c8_fwd<1, T, true>), grid, block, 0, s, p, tx, ty); break;
+            case 2: hipLaunchKernelGGL((conv_c8_fwd<2, T, true>), grid, block, 0, s, p, tx, ty); break;
+            case 3: hipLaunchKernelGGL((conv_c8_fwd<3, T, true>), grid, block, 0, s, p, tx, ty); break;
+            default: hipLaunchKernelGGL((conv_c8_fwd<4, T, true>), grid, block, 0, s, p, tx, ty); break;
+        }
+        return;
+    }
     switch (p.N / 16) {
         case 1: hipLaunchKernelGGL((conv_c8_fwd<1, T>), grid, block, 0, s, p, tx, ty); break;
         case 2: hipLaunchKernelGGL((conv_c8_fwd<2, T>), grid, block, 0, s, p, tx, ty); break;

@@ -31,10 +31,18 @@ def _pack_bits(y):
     return (pos << torch.arange(8, device=y.device, dtype=torch.int32)).sum(-1).to(torch.uint8)
 
 
+@pytest.fixture(params=[1, 0], ids=["tr", "rows"])
+def smallc_tr(request, dev):
+    """conv_c8_fwd with transposed accumulators (default) and the row form."""
+    ops.set_option("smallc_tr", request.param)
+    yield request.param
+    ops.set_option("smallc_tr", 1)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("K", [64, 32, 16])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_fwd_relu_bits(dev, shape, K, dtype):
+def test_fwd_relu_bits(dev, smallc_tr, shape, K, dtype):
     N, H, W = shape
     d = ops.conv_desc(N, H, W, 3, K, 3, 3, dtype=DT[dtype])
     assert ops.conv_kernel_info(d, ops.OP_FWD)[0].startswith("conv_c8")
