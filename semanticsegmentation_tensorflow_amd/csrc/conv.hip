@@ -868,6 +868,7 @@ static bool bwd_data_bits_params(const seg_conv_desc* d, const seg_epilogue* epi
     if (d->stride_h != 1 || d->stride_w != 1) return false;
     if (epi && (epi->relu_mask || epi->residual)) return false;
     NTParams p = conv_bwd_data_params(d);
+    p.epi.mask_scale = 1.f;              // (epi NULL: the plain ReluGrad)
     if (epi) {
         p.epi = make_epi(epi, d->C, 0, (long)d->H * d->W, d->ldx);
         if (epi->mask_scale != 0.f) p.epi.mask_scale = epi->mask_scale;

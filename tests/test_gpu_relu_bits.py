@@ -5,6 +5,8 @@ map (seg_conv2d_fwd_relu_bits, conv_c8_fwd), and conv1_2's input gradient
 (seg_conv2d_bwd_data_bits).  Every output is compared bit for bit with the
 16-bit-mask launches, which the op-level and full-size tests pin to the
 oracle; the bits themselves against torch's (y > 0) packed."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -87,6 +89,15 @@ def test_bwd_data_bits_equals_16bit_mask(dev, shape, scale, dtype):
     ops.conv2d_bwd_data_bits(d, dy, wh, _pack_bits(mask), got, scale, ws)
     torch.cuda.synchronize()
     assert torch.equal(_i16(got), _i16(ref))
+    if scale == 1.0:     # the C entry with no epilogue at all: the plain ReluGrad
+        bits = _pack_bits(mask)
+        raw = torch.full_like(ref, float("nan"))
+        dd = ops._with_ld(d, raw, dy)
+        wsp, wss = ws.ptr_size(ops.conv_workspace(dd, ops.OP_BWD_DATA))
+        assert ops._lib.lib().seg_conv2d_bwd_data_bits(ctypes.byref(dd), ops.ptr(dy), ops.ptr(wh), None, ops.ptr(bits),
+                                                         bits.shape[-1], ops.ptr(raw), wsp, wss, None) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(_i16(raw), _i16(ref))
     zero = mask == 0
     assert bool((got[zero] == 0).all()) and bool((got[~zero] != 0).any())
 
